@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark of the agent x candidate scoring + welfare hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): Best-of-N, N = 64 candidates x A = 8
+agents per GPU, T = 150 scored tokens per candidate, Llama-3.1-8B vocabulary
+(128,256) in bf16, egalitarian welfare.  One step = one full N x A scoring pass:
+
+    logits [A*N*T, V] (resident in HBM)  --cs_logsoftmax_gather-->  token log-probs
+      --cs_segment_reduce--> per-(agent, candidate) mean log-prob utility
+      --cs_welfare_reduce(MIN)--> [RCCL MIN all-reduce across ranks]
+      --cs_segmented_topk(k=1)--> selected candidate
+
+Multi-GPU: agents shard across ranks (8 per GPU, weak scaling); the only exchange
+is the MIN all-reduce of the N per-candidate welfare values.
+
+Prints ONE JSON line (rank 0).  `value` = agent x candidate scorings per second of
+the whole job; `roofline` prices the dominant kernel (cs_logsoftmax_gather)
+against the 8 TB/s HBM peak from HIP-event timing on its own stream;
+`cpu_baseline` times the CPU oracle (a port of the reference's fp64 scoring
+arithmetic) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG_DIR = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (agents per GPU, candidates, scored tokens per candidate, vocab, welfare, description)
+    "c2": (8, 64, 150, 128_256, "min",
+           "C2 best_of_n: N=64 candidates x A=8 agents per GPU, T=150 tokens, "
+           "Llama-3.1-8B vocab 128256 bf16 logits, egalitarian welfare"),
+    "c4": (32, 256, 4, 128_256, "sumlog",
+           "C4 finite_lookahead depth 4: R=256 paths x A=32 agents per GPU, "
+           "Llama-3.1-8B vocab 128256 bf16 logits, Nash welfare"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU time for the oracle baseline sample (0 disables)")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                    help="rocprofv3 PMC summary giving HBM bytes per launch (optional)")
+    return ap.parse_args()
+
+
+def init_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def make_inputs(A, N, T, V, seed, dev):
+    rows = A * N * T
+    g = torch.Generator(device=dev).manual_seed(seed)
+    logits = torch.empty(rows, V, dtype=torch.bfloat16, device=dev)
+    chunk = 4096
+    for r0 in range(0, rows, chunk):
+        r1 = min(rows, r0 + chunk)
+        logits[r0:r1] = torch.randn(r1 - r0, V, generator=g, device=dev) * 3.0
+    tgt = torch.randint(0, V, (rows, 1), generator=g, device=dev, dtype=torch.int32)
+    offsets = torch.arange(0, rows + 1, T, dtype=torch.int32, device=dev)
+    return logits, tgt, offsets
+
+
+def cpu_baseline(A, N, T, V, welfare_kind, seconds):
+    """Time the CPU oracle on a bounded sample: 2 agents x 8 candidates of the workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    orc.set_threads(threads)
+    a_s, n_s = 2, 8
+    rows = a_s * n_s * T
+    rng = np.random.default_rng(99)
+    logits = orc.bf16_bits((rng.standard_normal((rows, V), dtype=np.float32) * 3.0))
+    tgt = rng.integers(0, V, size=(rows, 1)).astype(np.int32)
+    off = np.arange(0, rows + 1, T, dtype=np.int32)
+    kind = {"min": orc.MIN, "sumlog": orc.SUMLOG}[welfare_kind]
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        tok, _ = orc.logsoftmax_gather(logits, tgt, bf16=True)
+        seg = orc.segment_reduce(tok, off)
+        U = (seg["sum_lp"] / seg["count"]).reshape(a_s, n_s)
+        W = orc.welfare(U, kind)
+        orc.topk(W, 1)
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": a_s * n_s * iters / el, "unit": "scorings/s", "cores": threads, "kind": "port",
+            "sample": f"{a_s} agents x {n_s} candidates x T={T} rows of V={V} bf16 "
+                      f"(oracle/cs_oracle.c fp64, OpenMP {threads} threads), {iters} passes "
+                      f"in {el:.1f} s"}
+
+
+def read_traffic(path, config, rows, V):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        ent = d.get(config)
+        if ent and ent.get("rows") == rows and ent.get("vocab") == V:
+            return ent.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args.gpus)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ops = importlib.import_module(PKG_DIR + ".ops")
+
+    A, N, T, V, wkind, desc = CONFIGS[args.config]
+    rows = A * N * T
+    logits, tgt, offsets = make_inputs(A, N, T, V, 1234 + rank, dev)
+    ws = ops.Workspace()
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        tok, _ = ops.logsoftmax_gather(logits, tgt, workspace=ws)
+        if ev is not None:
+            ev[1].record(stream)
+        seg = ops.segment_reduce(tok, offsets)
+        U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N)
+        if wkind == "sumlog":
+            U = torch.exp(U)  # Nash over geometric-mean token probability
+        W = ops.welfare(U, wkind, eps=1e-30)
+        if world > 1:
+            if wkind == "min":
+                torch.distributed.all_reduce(W, op=torch.distributed.ReduceOp.MIN)
+            else:
+                torch.distributed.all_reduce(W, op=torch.distributed.ReduceOp.SUM)
+        idx, _ = ops.topk(W, 1)
+        return idx
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    ms_per_step = elapsed * 1000.0 / args.steps
+
+    if rank == 0:
+        scorings = A * N * world
+        alg_bytes = rows * V * 2 + rows * 4 * 2  # logits read once + targets in + lp out
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(A, N, T, V, wkind, args.cpu_seconds)
+        line = {
+            "metric": "agent×candidate scorings/sec + decode steps/sec at 1/2/4/8 MI355X; % HBM roofline",
+            "value": scorings * args.steps / elapsed,
+            "unit": "scorings/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "decode_steps_per_s": 1000.0 / ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"workload": desc, "agents_per_gpu": A, "candidates": N,
+                       "tokens_per_candidate": T, "vocab": V, "rows_per_gpu": rows,
+                       "welfare": wkind, "parallelism": f"agents sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": read_traffic(args.pmc_json, args.config, rows, V),
+                         "kernel": "lsg_stream_kernel (cs_logsoftmax_gather)",
+                         "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,36 @@
+"""In-tree build of the gfx950 HIP library (no JIT cache: the .so travels with the repo)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_REPO = os.path.dirname(_HERE)
+SOURCES = [os.path.join(_HERE, "csrc", "consensus_scoring.hip")]
+OUT = os.path.join(_HERE, "libconsensus_scoring.so")
+ARCH = os.environ.get("CS_OFFLOAD_ARCH", "gfx950")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = SOURCES + [os.path.join(_REPO, "include", "consensus_scoring.h")]
+    return any(os.path.getmtime(s) > t for s in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-shared", "-fPIC",
+           "-I", os.path.join(_REPO, "include"), "-o", OUT + ".tmp"] + SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,587 @@
+// consensus_scoring.hip — gfx950 (MI355X / CDNA4) kernels behind include/consensus_scoring.h.
+//
+// What the reference does (serially, remotely): for every (agent, candidate) it
+// asks a hosted LLM for prompt log-probs (src/utils.py:201-281), folds them into a
+// per-agent utility (src/methods/*.py) and reduces across agents with min / sum /
+// sum-of-log (src/methods/beam_search.py:558, src/methods/best_of_n.py:401-408,
+// src/evaluation.py:337-381, core.py:108-113).  Here the same arithmetic runs on
+// the logits rows the local forward produced:
+//
+//   lsg_stream_kernel   HBM-bound: one pass over [rows, vocab] logits, online
+//                       max / sum-exp per lane (exp2 on pre-scaled values), 4 x 16 B
+//                       loads in flight per lane, wave64 butterfly + LDS merge.
+//                       Few rows -> split-V: (row, split) workgroups write (m, s)
+//                       partials and lsg_merge_kernel finishes lse + gather.
+//   seg_reduce_kernel   one wave per candidate segment, fp64 sums in fixed order.
+//   welfare_kernel      one lane per candidate column, agents folded in order.
+//   topk_kernel         per-segment bitonic sort of (order-key, ~index) in LDS.
+//
+// No float atomics anywhere: every output is bitwise reproducible run to run.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "consensus_scoring.h"
+
+namespace {
+
+constexpr int kBlock = 256;   // streaming workgroup: 4 waves of 64
+constexpr int kUnroll = 4;    // 16-byte vectors in flight per lane per iteration
+constexpr int kMergeBlock = 64;
+constexpr int64_t kTargetWgs = 2048;  // ~8 streaming workgroups per CU on 256 CUs
+constexpr float kLog2e = 1.4426950408889634f;
+
+thread_local std::string g_last_error = "";
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    return fail(CS_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
+  return CS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// element decoding
+// ---------------------------------------------------------------------------
+template <int DT>
+struct Elt;
+template <>
+struct Elt<CS_F32> {
+  static constexpr int kSize = 4;
+  static constexpr int kPerVec = 4;
+};
+template <>
+struct Elt<CS_BF16> {
+  static constexpr int kSize = 2;
+  static constexpr int kPerVec = 8;
+};
+template <>
+struct Elt<CS_F16> {
+  static constexpr int kSize = 2;
+  static constexpr int kPerVec = 8;
+};
+
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // one 16-byte global_load_dwordx4
+
+
+template <int DT>
+__device__ __forceinline__ void unpack_vec(const u32x4& q, float* v) {
+  const uint32_t w[4] = {q[0], q[1], q[2], q[3]};
+  if constexpr (DT == CS_F32) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(w[i]);
+  } else if constexpr (DT == CS_BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);             // element 2i: low half
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);  // element 2i+1: high half
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const half2_t h = __builtin_bit_cast(half2_t, w[i]);
+      v[2 * i] = (float)h[0];
+      v[2 * i + 1] = (float)h[1];
+    }
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ float load_one(const char* row, int64_t i) {
+  if constexpr (DT == CS_F32) {
+    return reinterpret_cast<const float*>(row)[i];
+  } else if constexpr (DT == CS_BF16) {
+    return __uint_as_float(static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(row)[i]) << 16);
+  } else {
+    return (float)reinterpret_cast<const _Float16*>(row)[i];
+  }
+}
+
+// Gemma-2 final-logit soft-capping, cap * tanh(x / cap), with tanh written through
+// one exp2 so the vocab stream and the target gather use the identical function.
+__device__ __forceinline__ float softcap_fn(float x, float cap, float inv_cap) {
+  const float z = x * inv_cap;
+  const float e = __builtin_amdgcn_exp2f(2.0f * kLog2e * z);  // exp(2z); inf for large z
+  const float t = 1.0f - 2.0f / (e + 1.0f);
+  return cap * t;
+}
+
+// ---------------------------------------------------------------------------
+// online log-sum-exp state
+// ---------------------------------------------------------------------------
+// (m, s) represents sum_i exp(x_i) = s * exp(m).  m == -inf  <=>  empty.
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  s = s * __builtin_amdgcn_exp2f((m - mn) * kLog2e) + s2 * __builtin_amdgcn_exp2f((m2 - mn) * kLog2e);
+  m = mn;
+}
+
+template <int N>
+__device__ __forceinline__ void lse_accum(float& m, float& s, const float* v) {
+  float cm = v[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) cm = fmaxf(cm, v[i]);
+  const float mn = fmaxf(m, cm);
+  if (mn == -INFINITY) return;
+  const float off = mn * kLog2e;
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc += __builtin_amdgcn_exp2f(fmaf(v[i], kLog2e, -off));
+  s = fmaf(s, __builtin_amdgcn_exp2f(fmaf(m, kLog2e, -off)), acc);
+  m = mn;
+}
+
+__device__ __forceinline__ void wave_lse_reduce(float& m, float& s) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float m2 = __shfl_xor(m, off, 64);
+    const float s2 = __shfl_xor(s, off, 64);
+    lse_merge(m, s, m2, s2);
+  }
+}
+
+__device__ __forceinline__ void gather_targets(const char* row, int64_t vocab, float lse,
+                                               const int32_t* __restrict__ tgt, int32_t k,
+                                               float* __restrict__ out, bool cap_on, float cap,
+                                               float inv_cap, int dt, int lane, int nlanes) {
+  for (int j = lane; j < k; j += nlanes) {
+    const int32_t t = tgt[j];
+    float r = __builtin_nanf("");
+    if (t >= 0 && t < vocab) {
+      float x;
+      if (dt == CS_F32)
+        x = load_one<CS_F32>(row, t);
+      else if (dt == CS_BF16)
+        x = load_one<CS_BF16>(row, t);
+      else
+        x = load_one<CS_F16>(row, t);
+      if (cap_on) x = softcap_fn(x, cap, inv_cap);
+      r = x - lse;
+    }
+    out[j] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// streaming kernel: one workgroup per (row, split)
+// ---------------------------------------------------------------------------
+template <int DT, bool CAP>
+__global__ __launch_bounds__(kBlock) void lsg_stream_kernel(
+    const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nsplit,
+    int64_t split_len, const int32_t* __restrict__ tgt, int32_t k, float cap, float inv_cap,
+    float* __restrict__ out_tok, float* __restrict__ out_lse, float2* __restrict__ part) {
+  constexpr int ESZ = Elt<DT>::kSize;
+  constexpr int EPV = Elt<DT>::kPerVec;
+  __shared__ float sm_m[kBlock / 64];
+  __shared__ float sm_s[kBlock / 64];
+  __shared__ float sm_lse;
+
+  const int tid = threadIdx.x;
+  const int64_t bid = blockIdx.x;
+  const int64_t row = bid / nsplit;
+  const int32_t split = static_cast<int32_t>(bid - row * nsplit);
+  const char* rp = logits + row * ld_bytes;
+  const int64_t v0 = static_cast<int64_t>(split) * split_len;
+  const int64_t v1 = min(vocab, v0 + split_len);
+  const int64_t n = v1 - v0;
+
+  float m = -INFINITY, s = 0.0f;
+
+  // scalar head up to the first 16-byte boundary, scalar tail after the last full vector
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(rp + v0 * ESZ);
+  int64_t head = static_cast<int64_t>(((16u - (a0 & 15u)) & 15u) / ESZ);
+  if (head > n) head = n;
+  const int64_t nvec = (n - head) / EPV;
+  const int64_t tail0 = head + nvec * EPV;
+  {
+    float x = -INFINITY;
+    if (tid < head) {
+      x = load_one<DT>(rp, v0 + tid);
+      if (CAP) x = softcap_fn(x, cap, inv_cap);
+    } else if (tid >= 64 && tid - 64 < n - tail0) {
+      x = load_one<DT>(rp, v0 + tail0 + (tid - 64));
+      if (CAP) x = softcap_fn(x, cap, inv_cap);
+    }
+    if (x != -INFINITY) lse_accum<1>(m, s, &x);
+  }
+
+  const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
+  int64_t i = tid;
+  for (; i + (kUnroll - 1) * kBlock < nvec; i += kUnroll * kBlock) {
+    u32x4 q[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * kBlock);
+    float v[kUnroll * EPV];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) unpack_vec<DT>(q[u], v + u * EPV);
+    if (CAP) {
+#pragma unroll
+      for (int e = 0; e < kUnroll * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+    }
+    lse_accum<kUnroll * EPV>(m, s, v);
+  }
+  for (; i < nvec; i += kBlock) {
+    const u32x4 q = __builtin_nontemporal_load(vp + i);
+    float v[EPV];
+    unpack_vec<DT>(q, v);
+    if (CAP) {
+#pragma unroll
+      for (int e = 0; e < EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+    }
+    lse_accum<EPV>(m, s, v);
+  }
+
+  wave_lse_reduce(m, s);
+  const int wave = tid >> 6;
+  if ((tid & 63) == 0) {
+    sm_m[wave] = m;
+    sm_s[wave] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float mm = sm_m[0], ss = sm_s[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) lse_merge(mm, ss, sm_m[w], sm_s[w]);
+    if (nsplit > 1) {
+      part[bid] = make_float2(mm, ss);
+    } else {
+      const float lse = mm + logf(ss);
+      sm_lse = lse;
+      if (out_lse) out_lse[row] = lse;
+    }
+  }
+  if (nsplit > 1) return;
+  __syncthreads();
+  if (k > 0)
+    gather_targets(rp, vocab, sm_lse, tgt + row * k, k, out_tok + row * k, CAP, cap, inv_cap, DT,
+                   tid, kBlock);
+}
+
+// split-V finish: merge the (m, s) partials of one row in split order, then gather.
+template <int DT, bool CAP>
+__global__ __launch_bounds__(kMergeBlock) void lsg_merge_kernel(
+    const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nsplit,
+    const float2* __restrict__ part, const int32_t* __restrict__ tgt, int32_t k, float cap,
+    float inv_cap, float* __restrict__ out_tok, float* __restrict__ out_lse) {
+  const int64_t row = blockIdx.x;
+  const int lane = threadIdx.x;
+  float m = -INFINITY, s = 0.0f;
+  for (int j = lane; j < nsplit; j += kMergeBlock) {
+    const float2 p = part[row * nsplit + j];
+    lse_merge(m, s, p.x, p.y);
+  }
+  wave_lse_reduce(m, s);
+  const float lse = m + logf(s);
+  if (lane == 0 && out_lse) out_lse[row] = lse;
+  if (k > 0)
+    gather_targets(logits + row * ld_bytes, vocab, lse, tgt + row * k, k, out_tok + row * k, CAP,
+                   cap, inv_cap, DT, lane, kMergeBlock);
+}
+
+// ---------------------------------------------------------------------------
+// per-candidate folding
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void seg_reduce_kernel(const float* __restrict__ lp,
+                                                         const int32_t* __restrict__ off,
+                                                         int64_t n_seg, float* __restrict__ sum_lp,
+                                                         float* __restrict__ sum_p,
+                                                         int32_t* __restrict__ cnt,
+                                                         float* __restrict__ last) {
+  const int64_t seg = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (seg >= n_seg) return;  // wave-uniform
+  const int64_t b = off[seg], e = off[seg + 1];
+  double a = 0.0, p = 0.0;
+  int c = 0;
+  for (int64_t i = b + lane; i < e; i += 64) {
+    const float v = lp[i];
+    if (!__builtin_isnan(v)) {
+      a += static_cast<double>(v);
+      p += exp(static_cast<double>(v));
+      c += 1;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    p += __shfl_xor(p, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if (lane == 0) {
+    if (sum_lp) sum_lp[seg] = static_cast<float>(a);
+    if (sum_p) sum_p[seg] = static_cast<float>(p);
+    if (cnt) cnt[seg] = c;
+    if (last) last[seg] = (e > b) ? lp[e - 1] : __builtin_nanf("");
+  }
+}
+
+__global__ __launch_bounds__(256) void welfare_kernel(const float* __restrict__ U, int32_t A,
+                                                      int32_t C, int64_t ldu, int kind, double eps,
+                                                      int nonfinite, float nan_val,
+                                                      float posinf_val, float neginf_val,
+                                                      float* __restrict__ W) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (c >= C) return;
+  double acc = 0.0;
+  bool any = false;
+  for (int32_t a = 0; a < A; ++a) {
+    float u = U[a * ldu + c];
+    if (!__builtin_isfinite(u)) {
+      if (nonfinite == CS_NONFINITE_SKIP) continue;
+      u = __builtin_isnan(u) ? nan_val : (u > 0.0f ? posinf_val : neginf_val);
+    }
+    const double d = static_cast<double>(u);
+    switch (kind) {
+      case CS_WELFARE_MIN:
+        acc = any ? fmin(acc, d) : d;
+        break;
+      case CS_WELFARE_MAX:
+        acc = any ? fmax(acc, d) : d;
+        break;
+      case CS_WELFARE_SUM:
+        acc += d;
+        break;
+      default:  // CS_WELFARE_SUMLOG
+        acc += log(fmax(d, eps));
+        break;
+    }
+    any = true;
+  }
+  W[c] = any ? static_cast<float>(acc) : __builtin_nanf("");
+}
+
+// Order key: larger float -> larger key; NaN below everything; -0 == +0.
+__device__ __forceinline__ uint32_t order_key(float f) {
+  if (__builtin_isnan(f)) return 0u;
+  if (f == 0.0f) f = 0.0f;
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ W, int32_t seg_len,
+                                                   int64_t ld, int32_t n2, int32_t k,
+                                                   int32_t* __restrict__ out_idx,
+                                                   float* __restrict__ out_val) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long ck[];
+  const int64_t seg = blockIdx.x;
+  const float* base = W + seg * ld;
+  const int tid = threadIdx.x;
+  // composite key: (order key, ~index) -> descending sort = value desc, index asc.
+  for (int i = tid; i < n2; i += 256) {
+    ck[i] = (i < seg_len) ? ((static_cast<unsigned long long>(order_key(base[i])) << 32) |
+                             static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(i)))
+                          : 0ull;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < (n2 >> 1); t += 256) {
+        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const unsigned long long a = ck[lo], b = ck[hi];
+        if ((a < b) == desc) {
+          ck[lo] = b;
+          ck[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int r = tid; r < k; r += 256) {
+    const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(ck[r] & 0xffffffffull);
+    out_idx[seg * k + r] = static_cast<int32_t>(idx);
+    if (out_val) out_val[seg * k + r] = base[idx];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side planning
+// ---------------------------------------------------------------------------
+int elt_size(int dtype) { return dtype == CS_F32 ? 4 : 2; }
+int elt_per_vec(int dtype) { return dtype == CS_F32 ? 4 : 8; }
+
+struct SplitPlan {
+  int32_t nsplit;
+  int64_t split_len;
+};
+
+SplitPlan plan_split(int64_t rows, int64_t vocab, int dtype) {
+  SplitPlan p{1, vocab};
+  if (rows <= 0 || vocab <= 0 || rows >= kTargetWgs) return p;
+  const int64_t grain = static_cast<int64_t>(kBlock) * elt_per_vec(dtype);  // one vector per lane
+  const int64_t min_len = grain * kUnroll;  // >= one full unrolled sweep per split
+  int64_t want = (kTargetWgs + rows - 1) / rows;
+  int64_t max_split = vocab / min_len;
+  if (max_split < 1) max_split = 1;
+  if (want > max_split) want = max_split;
+  if (want <= 1) return p;
+  int64_t len = (vocab + want - 1) / want;
+  len = ((len + grain - 1) / grain) * grain;
+  p.split_len = len;
+  p.nsplit = static_cast<int32_t>((vocab + len - 1) / len);
+  if (p.nsplit <= 1) {
+    p.nsplit = 1;
+    p.split_len = vocab;
+  }
+  return p;
+}
+
+template <int DT, bool CAP>
+void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_bytes,
+                const SplitPlan& plan, const int32_t* tgt, int32_t k, float cap, float* out_tok,
+                float* out_lse, float2* part, hipStream_t st) {
+  const float inv_cap = CAP ? 1.0f / cap : 0.0f;
+  const int64_t grid = rows * plan.nsplit;
+  hipLaunchKernelGGL((lsg_stream_kernel<DT, CAP>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
+                     0, st, static_cast<const char*>(logits), vocab, ld_bytes, plan.nsplit,
+                     plan.split_len, tgt, k, cap, inv_cap, out_tok, out_lse, part);
+  if (plan.nsplit > 1) {
+    hipLaunchKernelGGL((lsg_merge_kernel<DT, CAP>), dim3(static_cast<uint32_t>(rows)),
+                       dim3(kMergeBlock), 0, st, static_cast<const char*>(logits), vocab, ld_bytes,
+                       plan.nsplit, part, tgt, k, cap, inv_cap, out_tok, out_lse);
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* cs_version(void) { return "consensus_scoring 0.1.0 (gfx950)"; }
+
+const char* cs_last_error(void) { return g_last_error.c_str(); }
+
+size_t cs_workspace_size(int64_t rows, int64_t vocab, int32_t k) {
+  (void)k;
+  const SplitPlan p = plan_split(rows, vocab, CS_BF16);
+  const SplitPlan q = plan_split(rows, vocab, CS_F32);
+  const int32_t ns = p.nsplit > q.nsplit ? p.nsplit : q.nsplit;
+  if (ns <= 1) return 0;
+  return static_cast<size_t>(rows) * static_cast<size_t>(ns) * sizeof(float2);
+}
+
+int cs_logsoftmax_gather(const void* logits, int dtype, int64_t rows, int64_t vocab, int64_t ld,
+                         const int32_t* target_ids, int32_t k, float softcap, float* out_tok_lp,
+                         float* out_row_lse, void* workspace, size_t workspace_bytes,
+                         cs_stream_t stream) {
+  if (dtype != CS_F32 && dtype != CS_BF16 && dtype != CS_F16)
+    return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: unknown dtype");
+  if (rows < 0 || vocab <= 0 || ld < vocab || k < 0)
+    return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: need rows >= 0, vocab > 0, ld >= vocab, k >= 0");
+  if (rows > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: rows exceeds 2^31-1");
+  if (rows == 0) return CS_OK;
+  if (!logits) return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: logits is NULL");
+  if (k > 0 && (!target_ids || !out_tok_lp))
+    return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: k > 0 needs target_ids and out_tok_lp");
+  if (!(softcap >= 0.0f) || std::isinf(softcap))
+    return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: softcap must be finite and >= 0");
+  if (reinterpret_cast<uintptr_t>(logits) % elt_size(dtype) != 0)
+    return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: logits not element-aligned");
+  const SplitPlan plan = plan_split(rows, vocab, dtype);
+  const int64_t grid = rows * plan.nsplit;
+  if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_logsoftmax_gather: grid too large");
+  float2* part = nullptr;
+  if (plan.nsplit > 1) {
+    const size_t need = static_cast<size_t>(rows) * plan.nsplit * sizeof(float2);
+    if (!workspace || workspace_bytes < need)
+      return fail(CS_ERR_WORKSPACE, "cs_logsoftmax_gather: workspace smaller than cs_workspace_size()");
+    if (reinterpret_cast<uintptr_t>(workspace) % 8 != 0)
+      return fail(CS_ERR_WORKSPACE, "cs_logsoftmax_gather: workspace not 8-byte aligned");
+    part = static_cast<float2*>(workspace);
+  }
+  const int64_t ld_bytes = ld * elt_size(dtype);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool cap = softcap > 0.0f;
+  switch (dtype) {
+    case CS_F32:
+      if (cap)
+        launch_lsg<CS_F32, true>(logits, rows, vocab, ld_bytes, plan, target_ids, k, softcap,
+                                 out_tok_lp, out_row_lse, part, st);
+      else
+        launch_lsg<CS_F32, false>(logits, rows, vocab, ld_bytes, plan, target_ids, k, softcap,
+                                  out_tok_lp, out_row_lse, part, st);
+      break;
+    case CS_BF16:
+      if (cap)
+        launch_lsg<CS_BF16, true>(logits, rows, vocab, ld_bytes, plan, target_ids, k, softcap,
+                                  out_tok_lp, out_row_lse, part, st);
+      else
+        launch_lsg<CS_BF16, false>(logits, rows, vocab, ld_bytes, plan, target_ids, k, softcap,
+                                   out_tok_lp, out_row_lse, part, st);
+      break;
+    default:
+      if (cap)
+        launch_lsg<CS_F16, true>(logits, rows, vocab, ld_bytes, plan, target_ids, k, softcap,
+                                 out_tok_lp, out_row_lse, part, st);
+      else
+        launch_lsg<CS_F16, false>(logits, rows, vocab, ld_bytes, plan, target_ids, k, softcap,
+                                  out_tok_lp, out_row_lse, part, st);
+      break;
+  }
+  return check_launch("cs_logsoftmax_gather");
+}
+
+int cs_segment_reduce(const float* tok_lp, int64_t n, const int32_t* seg_offsets, int64_t n_seg,
+                      float* out_sum_lp, float* out_sum_p, int32_t* out_count, float* out_last,
+                      cs_stream_t stream) {
+  if (n < 0 || n_seg < 0) return fail(CS_ERR_INVALID, "cs_segment_reduce: negative size");
+  if (n_seg == 0) return CS_OK;
+  if (!seg_offsets || (n > 0 && !tok_lp))
+    return fail(CS_ERR_INVALID, "cs_segment_reduce: NULL input");
+  const int64_t blocks = (n_seg + 3) / 4;
+  if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_segment_reduce: too many segments");
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), tok_lp, seg_offsets, n_seg, out_sum_lp,
+                     out_sum_p, out_count, out_last);
+  return check_launch("cs_segment_reduce");
+}
+
+int cs_welfare_reduce(const float* U, int32_t A, int32_t C, int64_t ldu, int kind, float eps,
+                      int nonfinite, float nan_val, float posinf_val, float neginf_val, float* W,
+                      cs_stream_t stream) {
+  if (A < 0 || C < 0 || ldu < C) return fail(CS_ERR_INVALID, "cs_welfare_reduce: bad shape");
+  if (kind < CS_WELFARE_MIN || kind > CS_WELFARE_MAX)
+    return fail(CS_ERR_INVALID, "cs_welfare_reduce: unknown welfare kind");
+  if (nonfinite != CS_NONFINITE_SKIP && nonfinite != CS_NONFINITE_REPLACE)
+    return fail(CS_ERR_INVALID, "cs_welfare_reduce: unknown nonfinite mode");
+  if (C == 0) return CS_OK;
+  if (!W || (A > 0 && !U)) return fail(CS_ERR_INVALID, "cs_welfare_reduce: NULL pointer");
+  const int64_t blocks = (static_cast<int64_t>(C) + 255) / 256;
+  hipLaunchKernelGGL(welfare_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), U, A, C, ldu, kind,
+                     static_cast<double>(eps), nonfinite, nan_val, posinf_val, neginf_val, W);
+  return check_launch("cs_welfare_reduce");
+}
+
+int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld, int32_t k,
+                      int32_t* out_idx, float* out_val, cs_stream_t stream) {
+  if (n_seg < 0 || seg_len < 0 || k < 0 || ld < seg_len)
+    return fail(CS_ERR_INVALID, "cs_segmented_topk: bad shape");
+  if (seg_len > 16384) return fail(CS_ERR_INVALID, "cs_segmented_topk: seg_len > 16384");
+  if (k > seg_len) return fail(CS_ERR_INVALID, "cs_segmented_topk: k > seg_len");
+  if (n_seg == 0 || k == 0) return CS_OK;
+  if (!W || !out_idx) return fail(CS_ERR_INVALID, "cs_segmented_topk: NULL pointer");
+  int32_t n2 = 2;
+  while (n2 < seg_len) n2 <<= 1;
+  hipLaunchKernelGGL(topk_kernel, dim3(static_cast<uint32_t>(n_seg)), dim3(256),
+                     static_cast<size_t>(n2) * sizeof(unsigned long long),
+                     static_cast<hipStream_t>(stream), W, seg_len, ld, n2, k, out_idx, out_val);
+  return check_launch("cs_segmented_topk");
+}
+
+}  // extern "C"

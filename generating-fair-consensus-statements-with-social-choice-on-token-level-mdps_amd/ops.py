@@ -1,0 +1,190 @@
+"""Torch-tensor front end of the C-ABI (``include/consensus_scoring.h``).
+
+Every function here launches a hand-written gfx950 kernel through
+``libconsensus_scoring.so`` on torch's *current* HIP stream and returns device
+tensors.  Inputs must already live on the GPU; nothing is copied to the host and
+nothing falls back to a CPU path (a missing library raises ``CSError``).
+
+Reference semantics each op restates are cited on the op.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import CSError
+
+WELFARE = {"min": _lib.WELFARE_MIN, "egalitarian": _lib.WELFARE_MIN,
+           "sum": _lib.WELFARE_SUM, "utilitarian": _lib.WELFARE_SUM,
+           "sumlog": _lib.WELFARE_SUMLOG, "nash": _lib.WELFARE_SUMLOG,
+           "max": _lib.WELFARE_MAX}
+
+_DTYPE = {torch.float32: _lib.CS_F32, torch.bfloat16: _lib.CS_BF16, torch.float16: _lib.CS_F16}
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _require_cuda(*ts: torch.Tensor) -> None:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise CSError("consensus_scoring ops take device tensors (got a CPU tensor); "
+                          "there is no CPU path")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise CSError(f"tensors on different devices: {dev} vs {t.device}")
+
+
+class Workspace:
+    """Grow-only device scratch for split-V partials (allocation happens here, never
+    inside a launch, so a captured graph can reuse a pre-sized workspace)."""
+
+    def __init__(self) -> None:
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int, device: torch.device) -> Optional[torch.Tensor]:
+        if nbytes == 0:
+            return None
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+_default_ws: dict = {}
+
+
+def workspace_size(rows: int, vocab: int, k: int = 1) -> int:
+    return int(_lib.load().cs_workspace_size(rows, vocab, k))
+
+
+def logsoftmax_gather(logits: torch.Tensor, targets: Optional[torch.Tensor], *, vocab: Optional[int] = None,
+                      softcap: float = 0.0, out: Optional[torch.Tensor] = None,
+                      lse_out: Optional[torch.Tensor] = None, want_lse: bool = False,
+                      workspace: Optional[Workspace] = None):
+    """Fused log-softmax over the vocab + gather at ``targets``.
+
+    logits  [rows, ld] bf16/f16/f32 with unit column stride (only the first
+            ``vocab`` columns are used); targets [rows, k] int32 (ids outside
+            [0, vocab) give NaN, the reference's ``None``).
+    Returns (tok_lp [rows, k] f32, lse [rows] f32 or None).
+
+    Restates: remote echo=True prompt log-probs read by get_prompt_logprobs
+    (src/utils.py:249-263); core.log_softmax_rows + gather (core.py:64-68, 89-90).
+    """
+    L = _lib.load()
+    if logits.dim() != 2 or logits.stride(1) != 1:
+        raise CSError("logits must be 2-D with unit column stride")
+    if logits.dtype not in _DTYPE:
+        raise CSError(f"unsupported logits dtype {logits.dtype}")
+    rows, ld = logits.shape[0], logits.stride(0) if logits.shape[0] > 1 else logits.shape[1]
+    vocab = logits.shape[1] if vocab is None else int(vocab)
+    if vocab > logits.shape[1]:
+        raise CSError("vocab exceeds logits width")
+    if targets is None:
+        k = 0
+        targets = torch.empty((rows, 0), dtype=torch.int32, device=logits.device)
+    else:
+        if targets.dtype != torch.int32:
+            raise CSError("targets must be int32")
+        targets = targets.reshape(rows, -1)
+        if not targets.is_contiguous():
+            targets = targets.contiguous()
+        k = targets.shape[1]
+    _require_cuda(logits, targets, out, lse_out)
+    if out is None:
+        out = torch.empty((rows, k), dtype=torch.float32, device=logits.device)
+    elif out.dtype != torch.float32 or not out.is_contiguous() or out.numel() != rows * k:
+        raise CSError("out must be contiguous float32 with rows*k elements")
+    if lse_out is None and want_lse:
+        lse_out = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    nbytes = workspace_size(rows, vocab, k)
+    if workspace is None:
+        workspace = _default_ws.setdefault(logits.device, Workspace())
+    ws = workspace.get(nbytes, logits.device)
+    rc = L.cs_logsoftmax_gather(
+        logits.data_ptr(), _DTYPE[logits.dtype], rows, vocab, ld,
+        targets.data_ptr() if k else None, k, float(softcap), out.data_ptr() if k else None,
+        lse_out.data_ptr() if lse_out is not None else None,
+        ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, _stream())
+    _lib.check(rc, "cs_logsoftmax_gather")
+    return out, lse_out
+
+
+def segment_reduce(tok_lp: torch.Tensor, offsets: torch.Tensor):
+    """Per-segment Σlp, Σexp(lp), count of non-NaN, last value (fp64 accumulation).
+
+    Restates best_of_n.py:303-305, finite_lookahead.py:508-520, evaluation.py:203-213,
+    beam_search.py:389-390 and core.py:90.
+    """
+    L = _lib.load()
+    tok = tok_lp.reshape(-1)
+    if tok.dtype != torch.float32 or not tok.is_contiguous():
+        raise CSError("tok_lp must be contiguous float32")
+    if offsets.dtype != torch.int32 or offsets.dim() != 1 or not offsets.is_contiguous():
+        raise CSError("offsets must be a contiguous 1-D int32 tensor")
+    _require_cuda(tok, offsets)
+    n_seg = offsets.numel() - 1
+    dev = tok.device
+    sum_lp = torch.empty(n_seg, dtype=torch.float32, device=dev)
+    sum_p = torch.empty(n_seg, dtype=torch.float32, device=dev)
+    cnt = torch.empty(n_seg, dtype=torch.int32, device=dev)
+    last = torch.empty(n_seg, dtype=torch.float32, device=dev)
+    rc = L.cs_segment_reduce(tok.data_ptr(), tok.numel(), offsets.data_ptr(), n_seg,
+                             sum_lp.data_ptr(), sum_p.data_ptr(), cnt.data_ptr(), last.data_ptr(),
+                             _stream())
+    _lib.check(rc, "cs_segment_reduce")
+    return {"sum_lp": sum_lp, "sum_p": sum_p, "count": cnt, "last": last}
+
+
+def welfare(U: torch.Tensor, kind, *, eps: float = 1e-9, nonfinite: str = "skip",
+            nan_val: float = -10.0, posinf_val: float = 20.0, neginf_val: float = -20.0,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Welfare over agents (rows of U [A, C]) for every candidate column.
+
+    kind: 'min'|'egalitarian', 'sum'|'utilitarian', 'sumlog'|'nash', 'max'.
+    Restates evaluation.py:337-381, beam_search.py:558-560, best_of_n.py:384-408,
+    core.py:108-113 (point mass) and core.py:374.
+    """
+    L = _lib.load()
+    if isinstance(kind, str):
+        kind = WELFARE[kind]
+    if U.dim() != 2 or U.dtype != torch.float32 or U.stride(1) != 1:
+        raise CSError("U must be 2-D float32 with unit column stride")
+    _require_cuda(U, out)
+    A, C = U.shape
+    ldu = U.stride(0) if A > 1 else C
+    if out is None:
+        out = torch.empty(C, dtype=torch.float32, device=U.device)
+    mode = {"skip": _lib.NONFINITE_SKIP, "replace": _lib.NONFINITE_REPLACE}[nonfinite]
+    rc = L.cs_welfare_reduce(U.data_ptr(), A, C, ldu, int(kind), float(eps), mode, float(nan_val),
+                             float(posinf_val), float(neginf_val), out.data_ptr(), _stream())
+    _lib.check(rc, "cs_welfare_reduce")
+    return out
+
+
+def topk(W: torch.Tensor, k: int, *, with_values: bool = True):
+    """Stable descending top-k per row of W [n_seg, seg_len] (value desc, index asc;
+    NaN last).  Restates beam_search.py:558-560 (stable sorted, reverse=True),
+    best_of_n.py:198 (np.argmax) and finite_lookahead.py:527 (max, first wins)."""
+    L = _lib.load()
+    W2 = W.reshape(1, -1) if W.dim() == 1 else W
+    if W2.dim() != 2 or W2.dtype != torch.float32 or W2.stride(1) != 1:
+        raise CSError("W must be float32 with unit column stride")
+    _require_cuda(W2)
+    n_seg, seg_len = W2.shape
+    ld = W2.stride(0) if n_seg > 1 else seg_len
+    idx = torch.empty((n_seg, k), dtype=torch.int32, device=W.device)
+    val = torch.empty((n_seg, k), dtype=torch.float32, device=W.device) if with_values else None
+    rc = L.cs_segmented_topk(W2.data_ptr(), n_seg, seg_len, ld, int(k), idx.data_ptr(),
+                             val.data_ptr() if val is not None else None, _stream())
+    _lib.check(rc, "cs_segmented_topk")
+    if W.dim() == 1:
+        return idx[0], (val[0] if val is not None else None)
+    return idx, val

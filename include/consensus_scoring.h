@@ -1,0 +1,145 @@
+/*
+ * consensus_scoring.h — C-ABI of the MI355X (gfx950) agent x candidate scoring path.
+ *
+ * The reference (cartgr/Generating-Fair-Consensus-Statements-with-Social-Choice-on-Token-Level-MDPs)
+ * has no native code and no FFI: every log-probability comes back from a remote
+ * HTTPS call (`get_prompt_logprobs`, src/utils.py:201-281) and is folded into
+ * per-agent utilities and welfare by serial Python loops.  This header is the
+ * boundary that replaces those loops.  Each entry point names the reference code
+ * it replaces (file:line, relative to the reference root).
+ *
+ * Conventions
+ *   - All data pointers are caller-owned DEVICE buffers (e.g. torch tensors'
+ *     data_ptr()).  The library never allocates on the hot path; the only scratch
+ *     is the caller-provided workspace sized by cs_workspace_size().
+ *   - Every call is asynchronous and stream-ordered on `stream` (a hipStream_t
+ *     passed as an opaque pointer; NULL = the default stream).  No host sync.
+ *   - Return value: CS_OK (0) on success, a negative cs_status otherwise; the
+ *     message is available from cs_last_error() (thread-local).
+ *   - Kernels are re-entrant: no global mutable device state.
+ *   - Results are deterministic run-to-run: no float atomics, fixed reduction order.
+ */
+#ifndef CONSENSUS_SCORING_H
+#define CONSENSUS_SCORING_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* cs_stream_t; /* hipStream_t */
+
+/* element type of the logits buffer */
+enum cs_dtype { CS_F32 = 0, CS_BF16 = 1, CS_F16 = 2 };
+
+/* welfare over agents (applied per candidate column) */
+enum cs_welfare {
+  CS_WELFARE_MIN = 0,    /* egalitarian: min_a u[a,c]                                  */
+  CS_WELFARE_SUM = 1,    /* utilitarian: sum_a u[a,c]                                  */
+  CS_WELFARE_SUMLOG = 2, /* log-Nash:    sum_a log(max(u[a,c], eps))                   */
+  CS_WELFARE_MAX = 3     /* max_a u[a,c] (egalitarian over a cost, e.g. perplexity)    */
+};
+
+/* what cs_welfare_reduce does with a non-finite utility */
+enum cs_nonfinite {
+  CS_NONFINITE_SKIP = 0,   /* drop it (src/evaluation.py:316-319, `np.isfinite` filter)        */
+  CS_NONFINITE_REPLACE = 1 /* nan_to_num(nan, posinf, neginf) (src/methods/best_of_n.py:384-389) */
+};
+
+enum cs_status {
+  CS_OK = 0,
+  CS_ERR_INVALID = -1,   /* bad argument (shape, dtype, null pointer)          */
+  CS_ERR_WORKSPACE = -2, /* workspace missing or smaller than cs_workspace_size */
+  CS_ERR_HIP = -3        /* a HIP launch failed                                 */
+};
+
+/* Library identification and last error (thread-local, never NULL). */
+const char* cs_version(void);
+const char* cs_last_error(void);
+
+/* Bytes of device workspace cs_logsoftmax_gather needs for this shape (0 when the
+ * single-pass path is used).  Pure host function. */
+size_t cs_workspace_size(int64_t rows, int64_t vocab, int32_t k);
+
+/*
+ * cs_logsoftmax_gather — fused vocab-wide log-softmax + candidate-token gather.
+ *
+ * For every row r of logits[rows][ld] (first `vocab` columns used):
+ *     x'       = softcap > 0 ? softcap * tanh(x / softcap) : x
+ *     lse[r]   = log(sum_v exp(x'[r,v]))
+ *     out_tok_lp[r*k + j] = x'[r, target_ids[r*k + j]] - lse[r]      (j < k)
+ * A target id outside [0, vocab) yields NaN (the reference's `None` log-prob,
+ * src/utils.py:262-263, which every caller filters).
+ * One HBM pass over the logits; fp32 accumulation.
+ *
+ * Replaces: the remote log-softmax + gather behind get_prompt_logprobs
+ *   (src/utils.py:249-263, echo=True prompt log-probs), the per-token read in
+ *   _get_agent_token_logprob (src/methods/beam_search.py:389-390; one row per
+ *   (agent, beam) gathered at k candidate tokens), and core.log_softmax_rows +
+ *   gather (core.py:64-68, 88-90).
+ *
+ * out_row_lse may be NULL.  workspace may be NULL iff cs_workspace_size() == 0.
+ */
+int cs_logsoftmax_gather(const void* logits, int dtype, int64_t rows, int64_t vocab, int64_t ld,
+                         const int32_t* target_ids, int32_t k, float softcap, float* out_tok_lp,
+                         float* out_row_lse, void* workspace, size_t workspace_bytes,
+                         cs_stream_t stream);
+
+/*
+ * cs_segment_reduce — per-candidate folding of token log-probs.
+ *
+ * Segment s covers tok_lp[seg_offsets[s] .. seg_offsets[s+1]) (CSR, non-decreasing).
+ * NaN entries (None log-probs) are skipped.  Sums are accumulated in fp64 in a
+ * fixed order.  Outputs (any may be NULL):
+ *     out_sum_lp[s] = sum lp        out_sum_p[s] = sum exp(lp)
+ *     out_count[s]  = #non-NaN      out_last[s]  = tok_lp[seg_offsets[s+1]-1] (NaN if empty)
+ *
+ * Replaces: mean of valid log-probs (src/methods/best_of_n.py:303-305),
+ *   np.mean(logprobs[-len(path):]) (src/methods/finite_lookahead.py:508-520),
+ *   avg_logprob / avg_prob (src/evaluation.py:203-213), sum(full_logprobs[-1:])
+ *   (src/methods/beam_search.py:389-390), logu[:, j] += ls[:, a_t] (core.py:90).
+ */
+int cs_segment_reduce(const float* tok_lp, int64_t n, const int32_t* seg_offsets, int64_t n_seg,
+                      float* out_sum_lp, float* out_sum_p, int32_t* out_count, float* out_last,
+                      cs_stream_t stream);
+
+/*
+ * cs_welfare_reduce — welfare across agents for every candidate.
+ *
+ * U is [A][C] with row stride ldu (agent-major, agent order = dict order of
+ * agent_opinions).  W[c] = welfare_kind over a of U[a*ldu + c], folded in agent
+ * order in fp64.  Non-finite utilities are skipped or replaced (cs_nonfinite);
+ * a column with no usable utility gives NaN.
+ *
+ * Replaces: min over agents (src/methods/beam_search.py:558-560,
+ *   src/methods/best_of_n.py:401-408, src/methods/finite_lookahead.py:527);
+ *   utilitarian / log-Nash welfare (src/evaluation.py:337-349, 367-381);
+ *   F_val at a point-mass lottery (core.py:108-113); utilitarian column sums
+ *   (core.py:374).
+ */
+int cs_welfare_reduce(const float* U, int32_t A, int32_t C, int64_t ldu, int kind, float eps,
+                      int nonfinite, float nan_val, float posinf_val, float neginf_val, float* W,
+                      cs_stream_t stream);
+
+/*
+ * cs_segmented_topk — stable descending top-k inside each segment.
+ *
+ * Segment s is W[s*ld .. s*ld + seg_len).  out_idx[s*k + r] is the index (within
+ * the segment) of the element of rank r, ranks ordered by (value desc, index asc);
+ * NaN ranks below every number.  out_val may be NULL.  k <= seg_len <= 16384.
+ *
+ * Replaces: sorted(candidates, key=min(rewards), reverse=True) — stable, so ties
+ *   keep insertion order (src/methods/beam_search.py:558-560, 646-648);
+ *   np.argmax, first max wins (src/methods/best_of_n.py:198, core.py:374);
+ *   max(range, key=...) (src/methods/finite_lookahead.py:527).
+ */
+int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld, int32_t k,
+                      int32_t* out_idx, float* out_val, cs_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CONSENSUS_SCORING_H */

@@ -1,0 +1,218 @@
+"""GPU parity: every C-ABI kernel vs the CPU oracle on identical seeded inputs.
+
+Tolerances (north_star): per-token / per-agent log-probs within 1e-3 absolute
+(fp32 accumulation on the GPU vs fp64 oracle); selected indices bit-exact given
+identical scores.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LP_TOL = 1e-3
+
+
+def _bits(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().view(torch.int16).numpy().view(np.uint16)
+
+
+def _host_logits(t: torch.Tensor):
+    """(numpy array, bf16 flag) of a CPU/GPU logits tensor for the oracle."""
+    if t.dtype == torch.bfloat16:
+        return _bits(t), True
+    if t.dtype == torch.float16:
+        return t.cpu().numpy(), False
+    return t.cpu().numpy(), False
+
+
+CASES = [
+    # dtype, rows, vocab, ld_pad, k, softcap           path exercised
+    (torch.bfloat16, 64, 4096, 0, 1, 0.0),            # split-V, aligned
+    (torch.bfloat16, 3, 128256, 0, 10, 0.0),          # split-V, Llama-3 vocab, beam-style k
+    (torch.float32, 16, 128256, 0, 10, 0.0),          # C1 shape (fp32), split-V
+    (torch.bfloat16, 2, 256000, 0, 50, 30.0),         # Gemma-2 vocab + soft-cap, k=50
+    (torch.float16, 33, 5003, 3, 2, 0.0),             # odd vocab, padded ld -> misaligned rows
+    (torch.bfloat16, 2500, 1000, 1, 1, 0.0),          # single pass, odd ld (every row misaligned)
+    (torch.float32, 1, 7, 0, 7, 0.0),                 # tiny row, k = vocab
+    (torch.bfloat16, 4096, 4096, 0, 1, 0.0),          # single pass, many rows
+    (torch.float32, 2049, 515, 0, 3, 5.0),            # single pass, soft-cap, scalar tail
+]
+
+
+@pytest.mark.parametrize("dtype,rows,vocab,ld_pad,k,softcap", CASES)
+def test_logsoftmax_gather_matches_oracle(ops, orc, dev, dtype, rows, vocab, ld_pad, k, softcap):
+    g = torch.Generator().manual_seed(rows * 7 + vocab)
+    full = (torch.randn(rows, vocab + ld_pad, generator=g) * 3.0).to(dtype)
+    logits = full[:, :vocab]  # row stride vocab + ld_pad
+    tgt = torch.randint(0, vocab, (rows, k), generator=g, dtype=torch.int32)
+    tok, lse = ops.logsoftmax_gather(full.to(dev)[:, :vocab], tgt.to(dev), softcap=softcap,
+                                     want_lse=True)
+    host, bf16 = _host_logits(full)
+    o_tok, o_lse = orc.logsoftmax_gather(np.ascontiguousarray(host), tgt.numpy(), softcap=softcap,
+                                         bf16=bf16, vocab=vocab)
+    assert np.max(np.abs(tok.cpu().numpy() - o_tok)) < LP_TOL
+    assert np.max(np.abs(lse.cpu().numpy() - o_lse)) < LP_TOL
+    del logits
+
+
+def test_out_of_range_targets_are_nan_and_masked_vocab(ops, orc, dev):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(5, 3000, generator=g) * 2
+    x[:, 100:200] = -float("inf")  # logit-bias style masked tokens
+    tgt = torch.tensor([[0, -1], [150, 5], [2999, 3000], [7, 8], [9, 10]], dtype=torch.int32)
+    tok, _ = ops.logsoftmax_gather(x.to(dev), tgt.to(dev))
+    o_tok, _ = orc.logsoftmax_gather(x.numpy(), tgt.numpy())
+    t = tok.cpu().numpy()
+    assert np.isnan(t[0, 1]) and np.isnan(t[2, 1])
+    assert t[1, 0] == -np.inf and o_tok[1, 0] == -np.inf
+    m = np.isfinite(o_tok)
+    assert np.max(np.abs(t[m] - o_tok[m])) < LP_TOL
+
+
+def test_zero_rows_is_noop(ops, dev):
+    x = torch.empty(0, 128, device=dev, dtype=torch.bfloat16)
+    t = torch.empty(0, 1, device=dev, dtype=torch.int32)
+    tok, _ = ops.logsoftmax_gather(x, t)
+    assert tok.shape == (0, 1)
+
+
+@pytest.mark.parametrize("rows", [8, 3000])
+def test_bitwise_deterministic(ops, dev, rows):
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(rows, 32000, generator=g) * 3).to(torch.bfloat16).to(dev)
+    t = torch.randint(0, 32000, (rows, 4), generator=g, dtype=torch.int32).to(dev)
+    a, la = ops.logsoftmax_gather(x, t, want_lse=True)
+    b, lb = ops.logsoftmax_gather(x, t, want_lse=True)
+    assert torch.equal(a, b) and torch.equal(la, lb)
+
+
+def test_row_shift_invariance(ops, dev):
+    """log-softmax is invariant to adding a constant to a row (size-independent property)."""
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(40, 50000, generator=g, dtype=torch.float32) * 2
+    c = torch.linspace(-20, 20, 40)[:, None]
+    t = torch.randint(0, 50000, (40, 3), generator=g, dtype=torch.int32).to(dev)
+    a, _ = ops.logsoftmax_gather(x.to(dev), t)
+    b, _ = ops.logsoftmax_gather((x + c).to(dev), t)
+    assert torch.max(torch.abs(a - b)).item() < 1e-4
+
+
+def test_full_vocab_probabilities_sum_to_one(ops, dev):
+    x = (torch.randn(6, 128256, device=dev) * 4).to(torch.bfloat16)
+    t = torch.arange(128256, dtype=torch.int32, device=dev).repeat(6, 1)
+    tok, _ = ops.logsoftmax_gather(x, t)
+    s = torch.exp(tok.double()).sum(dim=1)
+    assert torch.max(torch.abs(s - 1)).item() < 1e-4
+
+
+def test_segment_reduce_matches_oracle(ops, orc, dev):
+    rng = np.random.default_rng(2)
+    lens = rng.integers(0, 300, size=257)
+    lens[[3, 100]] = 0
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    lp = -np.abs(rng.normal(size=int(off[-1]))).astype(np.float32) * 3
+    lp[rng.integers(0, off[-1], size=40)] = np.nan
+    out = ops.segment_reduce(torch.as_tensor(lp, device=dev), torch.as_tensor(off, device=dev))
+    ref = orc.segment_reduce(lp.astype(np.float64), off)
+    assert np.max(np.abs(out["sum_lp"].cpu().numpy() - ref["sum_lp"])) < 1e-3
+    assert np.max(np.abs(out["sum_p"].cpu().numpy() - ref["sum_p"])) < 1e-4
+    assert np.array_equal(out["count"].cpu().numpy(), ref["count"])
+    lo, lr = out["last"].cpu().numpy(), ref["last"]
+    assert np.array_equal(np.isnan(lo), np.isnan(lr))
+    assert np.array_equal(lo[~np.isnan(lo)], lr[~np.isnan(lr)].astype(np.float32))
+
+
+@pytest.mark.parametrize("kind", ["min", "sum", "sumlog", "max"])
+@pytest.mark.parametrize("nonfinite", ["skip", "replace"])
+def test_welfare_matches_oracle(ops, orc, dev, kind, nonfinite):
+    rng = np.random.default_rng(4)
+    U = rng.uniform(-5, 1, size=(37, 1000)).astype(np.float32)
+    U[0, :5] = [np.nan, np.inf, -np.inf, 0.0, 1e-12]
+    U[:, 7] = np.nan  # an all-None column
+    codes = {"min": orc.MIN, "sum": orc.SUM, "sumlog": orc.SUMLOG, "max": orc.MAX}
+    W = ops.welfare(torch.as_tensor(U, device=dev), kind, eps=1e-9, nonfinite=nonfinite)
+    ref = orc.welfare(U.astype(np.float64), codes[kind], eps=1e-9,
+                      nonfinite=0 if nonfinite == "skip" else 1)
+    w = W.cpu().numpy()
+    assert np.array_equal(np.isnan(w), np.isnan(ref))
+    m = ~np.isnan(ref)
+    np.testing.assert_allclose(w[m], ref[m], rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("seg_len", [1, 2, 7, 64, 800, 1000, 4096, 16384])
+def test_topk_matches_stable_sort(ops, orc, dev, seg_len):
+    rng = np.random.default_rng(seg_len)
+    n_seg = 3
+    W = rng.integers(-20, 20, size=(n_seg, seg_len)).astype(np.float32)  # heavy ties
+    W[:, rng.integers(0, seg_len, size=max(1, seg_len // 50))] = np.nan
+    if seg_len > 2:
+        W[0, 1] = -0.0
+        W[0, 2] = 0.0
+    k = seg_len if seg_len <= 1000 else 64
+    idx, val = ops.topk(torch.as_tensor(W, device=dev), k)
+    ref = orc.topk(W.astype(np.float64), k)
+    assert np.array_equal(idx.cpu().numpy(), ref)
+    v = val.cpu().numpy()
+    assert np.array_equal(np.isnan(v), np.isnan(np.take_along_axis(W, ref, 1)))
+
+
+def test_core_drop_in_matches_reference_golden(pkg, golden_dir, dev):
+    import importlib
+    core = importlib.import_module(pkg.__name__ + ".core")
+    g = np.load(os.path.join(golden_dir, "core_golden.npz"))
+    for name in ("ls_small", "ls_wide", "ls_big"):
+        np.testing.assert_allclose(core.log_softmax_rows(g[f"{name}_in"]), g[f"{name}_out"],
+                                   atol=1e-4)
+    for s in g["seeds"]:
+        v, w = g[f"v_{s}"], g[f"w_{s}"]
+        for ri, rho in zip((0, 9, 19), g["rho"]):
+            U, leaves = core.compute_utilities(v, w, rho)
+            np.testing.assert_allclose(U, g[f"U_{s}_{ri}"], rtol=1e-4, atol=1e-12)
+            assert [tuple(x) for x in g["leaves"]] == leaves
+            # selection bit-exact given identical scores (the reference's U)
+            Uref = g[f"U_{s}_{ri}"]
+            assert core.point_mass_select(Uref, "utilitarian") == g[f"jutil_{s}_{ri}"]
+            assert core.point_mass_select(Uref, "egalitarian") == g[f"jegal_{s}_{ri}"]
+            F = core.point_mass_welfare(Uref, "nash")
+            np.testing.assert_allclose(F, g[f"Fpoint_{s}_{ri}"], rtol=1e-5)
+
+
+def test_published_perplexity_welfare_on_gpu(ops, golden_dir, dev):
+    import pandas as pd
+    df = pd.read_csv(os.path.join(golden_dir, "eval_welfare_published.csv"))
+    for n_agents, g in df.groupby("n_agents"):
+        lp = g[[f"avg_logprob_{j}" for j in range(n_agents)]].to_numpy().T.astype(np.float32)
+        ppl = torch.exp(-torch.as_tensor(lp, device=dev))
+        np.testing.assert_allclose(ops.welfare(ppl, "max").cpu().numpy(),
+                                   g["egalitarian_welfare_perplexity"], rtol=1e-5)
+        np.testing.assert_allclose(ops.welfare(ppl, "sum").cpu().numpy(),
+                                   g["utilitarian_welfare_perplexity"], rtol=1e-5)
+        inv = 1.0 / torch.clamp(ppl, min=1e-9)
+        np.testing.assert_allclose(ops.welfare(inv, "sumlog", eps=1e-30).cpu().numpy(),
+                                   g["log_nash_welfare_perplexity"], rtol=1e-5, atol=1e-4)
+
+
+def test_c2_full_size_sampled_rows(ops, orc, dev):
+    """BASELINE C2 at full size (76,800 x 128,256 bf16 = 19.7 GB): sampled rows vs oracle,
+    every row's log-sum-exp vs torch, and run-to-run bitwise determinism."""
+    rows, V = 76_800, 128_256
+    g = torch.Generator(device=dev).manual_seed(1234)
+    x = torch.empty(rows, V, dtype=torch.bfloat16, device=dev)
+    for r0 in range(0, rows, 4096):
+        x[r0:r0 + 4096] = (torch.randn(min(4096, rows - r0), V, generator=g, device=dev) * 3)
+    t = torch.randint(0, V, (rows, 1), generator=g, device=dev, dtype=torch.int32)
+    tok, lse = ops.logsoftmax_gather(x, t, want_lse=True)
+    tok2, _ = ops.logsoftmax_gather(x, t)
+    assert torch.equal(tok, tok2)
+    pick = torch.tensor([0, 1, 4095, 4096, 38_400, 76_799], device=dev)
+    host = _bits(x[pick])
+    o_tok, o_lse = orc.logsoftmax_gather(host, t[pick].cpu().numpy(), bf16=True)
+    assert np.max(np.abs(tok[pick].cpu().numpy() - o_tok)) < LP_TOL
+    ref_lse = torch.cat([torch.logsumexp(x[r0:r0 + 2048].float(), dim=1)
+                         for r0 in range(0, rows, 2048)])
+    assert torch.max(torch.abs(ref_lse - lse)).item() < LP_TOL
+    del x
+    torch.cuda.empty_cache()
