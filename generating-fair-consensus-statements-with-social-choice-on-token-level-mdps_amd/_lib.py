@@ -22,7 +22,8 @@ NONFINITE_SKIP, NONFINITE_REPLACE = 0, 1
 
 EXPORTED = (
     "cs_version", "cs_last_error", "cs_workspace_size", "cs_logsoftmax_gather",
-    "cs_segment_reduce", "cs_welfare_reduce", "cs_segmented_topk",
+    "cs_segment_reduce", "cs_welfare_reduce", "cs_segmented_topk", "cs_vocab_topk_workspace_size",
+    "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
 )
 
 
@@ -68,6 +69,16 @@ def load():
     L.cs_welfare_reduce.restype = ctypes.c_int
     L.cs_segmented_topk.argtypes = [vp, i32, i32, i64, i32, vp, vp, vp]
     L.cs_segmented_topk.restype = ctypes.c_int
+    L.cs_vocab_topk_workspace_size.argtypes = [i64, i64, i32]
+    L.cs_vocab_topk_workspace_size.restype = ctypes.c_size_t
+    L.cs_vocab_topk.argtypes = [vp, ctypes.c_int, i64, i64, i64, i32, f32, vp, vp, vp,
+                                ctypes.c_size_t, vp]
+    L.cs_vocab_topk.restype = ctypes.c_int
+    L.cs_vocab_sample_workspace_size.argtypes = [i64, i64, i32]
+    L.cs_vocab_sample_workspace_size.restype = ctypes.c_size_t
+    L.cs_vocab_sample.argtypes = [vp, ctypes.c_int, i64, i64, i64, f32, f32, vp, i32, vp, vp, vp,
+                                  ctypes.c_size_t, vp]
+    L.cs_vocab_sample.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -1,0 +1,214 @@
+"""Batched agent x candidate scoring engine.
+
+The reference issues one remote call per (agent, candidate) and re-encodes the
+whole ~150-800-token prompt every time (src/methods/beam_search.py:495-538,
+best_of_n.py:266-321, finite_lookahead.py:464-524).  Here:
+
+  1. ``prefill``: every agent's prompt prefix (system + template + the statement so
+     far) is encoded ONCE per decode call -> per-layer K/V [A, Hkv, P, D] plus the
+     hidden state at its last position.
+  2. ``score``: all (agent, candidate) continuations of a step run as one batch of
+     streams that attend to their agent's prefix K/V; the LM head produces one
+     logits row per scored token; ``cs_logsoftmax_gather`` turns the rows into token
+     log-probs and ``cs_segment_reduce`` folds them per (agent, candidate).
+  3. ``BeamState``: beam search keeps per-(prefix, beam) generated K/V and advances
+     every stream by one position per step (one logits row per (agent, beam),
+     gathered at the K candidate tokens of that beam).
+
+Everything after the LM head runs in the HIP kernels (ops.*).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import ops
+from .model import Model
+
+
+@dataclass
+class PrefixCache:
+    kv: list                    # per layer (k, v): [n_prefix, Hkv, Pmax, D]
+    lengths: torch.Tensor       # [n_prefix] int64
+    last_hidden: torch.Tensor   # [n_prefix, d] final-norm hidden at position length-1
+    pos: torch.Tensor           # [n_prefix, Pmax] key positions
+    valid: torch.Tensor         # [n_prefix, Pmax] bool
+
+
+def _pad(seqs: Sequence[Sequence[int]], device, fill: int = 0):
+    n = len(seqs)
+    T = max((len(s) for s in seqs), default=0)
+    out = torch.full((n, max(T, 1)), fill, dtype=torch.long)
+    lens = torch.zeros(n, dtype=torch.long)
+    for i, s in enumerate(seqs):
+        if len(s):
+            out[i, :len(s)] = torch.as_tensor(list(s), dtype=torch.long)
+        lens[i] = len(s)
+    return out.to(device, non_blocking=True), lens.to(device, non_blocking=True)
+
+
+class ScoringEngine:
+    """Owns a model on one device and scores continuations under many prefixes."""
+
+    def __init__(self, model: Model, max_rows_per_chunk: int = 32768,
+                 max_streams_per_chunk: int = 1024):
+        self.model = model
+        self.device = model.device
+        self.softcap = model.cfg.final_softcap
+        self.max_rows = max_rows_per_chunk
+        self.max_streams = max_streams_per_chunk
+        self.ws = ops.Workspace()
+
+    # --- prefixes ---------------------------------------------------------------
+    @torch.no_grad()
+    def prefill(self, prefixes: Sequence[Sequence[int]]) -> PrefixCache:
+        if any(len(p) == 0 for p in prefixes):
+            raise ValueError("every prefix needs at least one token (BOS)")
+        ids, lens = _pad(prefixes, self.device)
+        kv, h, valid = self.model.prefill(ids, lens)
+        last = h[torch.arange(h.shape[0], device=self.device), lens - 1]
+        P = ids.shape[1]
+        pos = torch.arange(P, device=self.device)[None].expand(ids.shape[0], P)
+        return PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid)
+
+    # --- one logits block -> token log-probs --------------------------------------
+    def rows_logprobs(self, hidden: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        """hidden [rows, d] -> logits [rows, V] (LM head) -> log p(targets) [rows, k]."""
+        logits = self.model.lm_head(hidden)
+        tok, _ = ops.logsoftmax_gather(logits, targets.to(torch.int32), softcap=self.softcap,
+                                       workspace=self.ws)
+        return tok
+
+    # --- continuation scoring ---------------------------------------------------
+    @torch.no_grad()
+    def score(self, cache: PrefixCache, owner: Sequence[int],
+              conts: Sequence[Sequence[int]]) -> torch.Tensor:
+        """Token log-probs of every continuation under its owner's prefix.
+
+        Returns a flat float32 tensor: for stream r the slice
+        [off[r], off[r+1]) holds log p(conts[r][t] | prefix[owner[r]], conts[r][:t]).
+        Use ``offsets(conts)`` for the CSR boundaries.
+        """
+        R = len(conts)
+        lens = [len(c) for c in conts]
+        out = torch.empty(sum(lens), dtype=torch.float32, device=self.device)
+        # chunk streams so that the logits block stays bounded
+        r0, o0 = 0, 0
+        while r0 < R:
+            r1, rows = r0, 0
+            while r1 < R and (r1 == r0 or (rows + lens[r1] <= self.max_rows and
+                                           r1 - r0 < self.max_streams)):
+                rows += lens[r1]
+                r1 += 1
+            self._score_chunk(cache, owner[r0:r1], conts[r0:r1], out[o0:o0 + rows])
+            r0, o0 = r1, o0 + rows
+        return out
+
+    def _score_chunk(self, cache, owner, conts, out):
+        dev = self.device
+        m = self.model
+        R = len(conts)
+        own = torch.as_tensor(list(owner), dtype=torch.long, device=dev)
+        toks, lens = _pad(conts, dev)
+        T = toks.shape[1]
+        # hidden state that predicts each continuation token:
+        # t = 0 -> last prefix position; t > 0 -> continuation position t-1
+        need_ext = T > 1
+        if need_ext:
+            inp = toks[:, :T - 1]
+            plen = cache.lengths[own]
+            pos = plen[:, None] + torch.arange(T - 1, device=dev)[None]
+            ctx = [(k[own], v[own]) for k, v in cache.kv]
+            h, _ = m.extend(inp, pos, ctx, cache.valid[own], cache.pos[own])
+        flat_h, flat_t = [], []
+        lens_l = lens.tolist()
+        last = cache.last_hidden[own]
+        # gather rows in stream-major order
+        idx_r = torch.repeat_interleave(torch.arange(R, device=dev), lens)
+        idx_t = torch.cat([torch.arange(L, device=dev) for L in lens_l]) if R else \
+            torch.empty(0, dtype=torch.long, device=dev)
+        if need_ext:
+            hpad = torch.cat([last[:, None, :], h], dim=1)   # [R, T, d]
+        else:
+            hpad = last[:, None, :]
+        rows_h = hpad[idx_r, idx_t]
+        rows_t = toks[idx_r, idx_t][:, None]
+        tok = self.rows_logprobs(rows_h, rows_t)
+        out.copy_(tok.view(-1))
+        del flat_h, flat_t
+
+    @staticmethod
+    def offsets(conts: Sequence[Sequence[int]], device) -> torch.Tensor:
+        off = [0]
+        for c in conts:
+            off.append(off[-1] + len(c))
+        return torch.as_tensor(off, dtype=torch.int32, device=device)
+
+
+class BeamState:
+    """Per-(prefix, beam) incremental decode state for beam search.
+
+    Streams are laid out prefix-major: stream s = p * n_beams + b.  Each step
+    appends one token to every live beam (all beams share one length), so the
+    generated K/V is a dense [S, Hkv, G, D] tensor per layer.
+    """
+
+    def __init__(self, engine: ScoringEngine, cache: PrefixCache, n_prefix: int):
+        self.e = engine
+        self.cache = cache
+        self.n_prefix = n_prefix
+        self.n_beams = 1
+        self.gen_kv: Optional[list] = None   # per layer (k, v) [S, Hkv, G, D]
+        self.G = 0
+        # hidden that predicts the next token of each stream: start = last prefix position
+        self.next_hidden = cache.last_hidden.clone()          # [S, d] with n_beams = 1
+
+    def next_logprobs(self, targets: torch.Tensor) -> torch.Tensor:
+        """targets [n_prefix, n_beams, k] int -> log-probs [n_prefix, n_beams, k]."""
+        P, B, K = targets.shape
+        tok = self.e.rows_logprobs(self.next_hidden, targets.reshape(P * B, K))
+        return tok.view(P, B, K)
+
+    def next_logits(self, prefix_idx: int) -> torch.Tensor:
+        """Raw logits rows [n_beams, V] of one prefix (e.g. the reference policy)."""
+        B = self.n_beams
+        h = self.next_hidden[prefix_idx * B:(prefix_idx + 1) * B]
+        return self.e.model.lm_head(h)
+
+    @torch.no_grad()
+    def advance(self, parent: Sequence[int], tokens: Sequence[int]) -> None:
+        """New beams j = (parent beam parent[j], appended token tokens[j]) for every prefix."""
+        dev = self.e.device
+        m = self.e.model
+        P, Bo, Bn = self.n_prefix, self.n_beams, len(parent)
+        par = torch.as_tensor(list(parent), dtype=torch.long, device=dev)
+        src = (torch.arange(P, device=dev)[:, None] * Bo + par[None, :]).reshape(-1)   # [P*Bn]
+        own = torch.arange(P, device=dev).repeat_interleave(Bn)
+        tok = torch.as_tensor(list(tokens), dtype=torch.long, device=dev).repeat(P)[:, None]
+        c = self.cache
+        plen = c.lengths[own]
+        pos = (plen + self.G)[:, None]
+        ctx, cmask, cpos = [], None, None
+        pre_mask = c.valid[own]
+        pre_pos = c.pos[own]
+        if self.G > 0:
+            gpos = plen[:, None] + torch.arange(self.G, device=dev)[None]
+            cmask = torch.cat([pre_mask, torch.ones(len(own), self.G, dtype=torch.bool,
+                                                    device=dev)], 1)
+            cpos = torch.cat([pre_pos, gpos], 1)
+            for (pk, pv), (gk, gv) in zip(c.kv, self.gen_kv):
+                ctx.append((torch.cat([pk[own], gk[src]], 2), torch.cat([pv[own], gv[src]], 2)))
+        else:
+            cmask, cpos = pre_mask, pre_pos
+            ctx = [(pk[own], pv[own]) for pk, pv in c.kv]
+        h, new = m.extend(tok, pos, ctx, cmask, cpos)
+        if self.G > 0:
+            self.gen_kv = [(torch.cat([gk[src], nk], 2), torch.cat([gv[src], nv], 2))
+                           for (gk, gv), (nk, nv) in zip(self.gen_kv, new)]
+        else:
+            self.gen_kv = new
+        self.G += 1
+        self.n_beams = Bn
+        self.next_hidden = h[:, 0, :]

@@ -1,0 +1,297 @@
+"""Minimal Llama-3 / Gemma-2 decoder forward with an explicit KV layout.
+
+PyTorch here is plumbing: it runs the transformer GEMMs (hipBLASLt) and attention
+(SDPA).  What the scoring path needs from it is narrow and is shaped for reuse:
+
+  * ``prefill(ids)``       one pass over a batch of prompt prefixes -> per-layer K/V
+                           [n_prefix, Hkv, P, D] and the final-norm hidden state of
+                           every position (the last one predicts the first
+                           continuation token).
+  * ``extend(...)``        T new tokens for each of R streams; stream r attends to
+                           prefix ``owner[r]`` (shared, never copied per candidate
+                           in HBM beyond the transient SDPA operand), to its own
+                           generated history (beam search) and causally to itself.
+  * ``lm_head(h)``         hidden -> logits in the weight dtype (bf16); the
+                           log-softmax / gather / welfare after it are the HIP kernels.
+
+The Gemma-2 final-logit soft-cap (30) is NOT applied here: cs_logsoftmax_gather
+applies it on load (one fewer HBM pass over the logits).
+
+Weights are random-init (seeded, architecture-exact shapes): no checkpoints are
+available offline and throughput is independent of weight values.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, replace
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+
+@dataclass
+class ModelConfig:
+    name: str
+    family: str            # "llama3" | "gemma2"
+    vocab: int
+    d_model: int
+    n_layers: int
+    n_heads: int
+    n_kv_heads: int
+    head_dim: int
+    d_ff: int
+    rope_theta: float = 500000.0
+    rms_eps: float = 1e-5
+    tie_embeddings: bool = False
+    rope_scaling: Optional[dict] = None      # llama3-style frequency scaling
+    final_softcap: float = 0.0               # gemma2: 30.0 (applied in the HIP kernel)
+    attn_softcap: float = 0.0                # gemma2: 50.0
+    sliding_window: int = 0                  # gemma2: 4096 on even layers
+    query_pre_attn_scalar: Optional[float] = None
+    init_std: float = 0.02
+    extra: Dict = field(default_factory=dict)
+
+
+LLAMA31_ROPE = {"factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                "original_max_position_embeddings": 8192}
+LLAMA32_ROPE = {"factor": 32.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                "original_max_position_embeddings": 8192}
+
+PRESETS = {
+    "llama-3.2-1b": ModelConfig("llama-3.2-1b", "llama3", 128256, 2048, 16, 32, 8, 64, 8192,
+                                tie_embeddings=True, rope_scaling=LLAMA32_ROPE),
+    "llama-3.1-8b": ModelConfig("llama-3.1-8b", "llama3", 128256, 4096, 32, 32, 8, 128, 14336,
+                                rope_scaling=LLAMA31_ROPE),
+    "llama-3.3-70b": ModelConfig("llama-3.3-70b", "llama3", 128256, 8192, 80, 64, 8, 128, 28672,
+                                 rope_scaling=LLAMA31_ROPE),
+    "gemma-2-9b": ModelConfig("gemma-2-9b", "gemma2", 256000, 3584, 42, 16, 8, 256, 14336,
+                              rope_theta=10000.0, rms_eps=1e-6, tie_embeddings=True,
+                              final_softcap=30.0, attn_softcap=50.0, sliding_window=4096,
+                              query_pre_attn_scalar=256.0),
+    # small architecture-faithful models for parity fixtures
+    "tiny-llama": ModelConfig("tiny-llama", "llama3", 384, 64, 2, 4, 2, 16, 128,
+                              rope_scaling=LLAMA31_ROPE, init_std=0.15),
+    "tiny-gemma": ModelConfig("tiny-gemma", "gemma2", 384, 64, 2, 4, 2, 16, 128,
+                              rope_theta=10000.0, rms_eps=1e-6, tie_embeddings=True,
+                              final_softcap=30.0, attn_softcap=50.0, sliding_window=8,
+                              query_pre_attn_scalar=16.0, init_std=0.15),
+}
+
+
+def preset(name: str, **overrides) -> ModelConfig:
+    return replace(PRESETS[name], **overrides)
+
+
+def rope_inv_freq(cfg: ModelConfig, device) -> torch.Tensor:
+    D = cfg.head_dim
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, D, 2, dtype=torch.float64, device=device) / D))
+    rs = cfg.rope_scaling
+    if rs:
+        factor, lo, hi = rs["factor"], rs["low_freq_factor"], rs["high_freq_factor"]
+        old = rs["original_max_position_embeddings"]
+        wavelen = 2 * math.pi / inv
+        scaled = torch.where(wavelen > old / lo, inv / factor, inv)
+        smooth = (old / wavelen - lo) / (hi - lo)
+        smoothed = (1 - smooth) * scaled / factor + smooth * scaled
+        medium = (wavelen >= old / hi) & (wavelen <= old / lo)
+        inv = torch.where(medium, smoothed, scaled)
+    return inv.to(torch.float32)
+
+
+class Model:
+    """Decoder weights + forward.  ``dtype`` is the weight/activation dtype."""
+
+    def __init__(self, cfg: ModelConfig, device, dtype=torch.bfloat16, seed: int = 0,
+                 weights: Optional[Dict[str, torch.Tensor]] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.w = weights if weights is not None else self._init(seed)
+        self.inv_freq = rope_inv_freq(cfg, self.device)
+
+    # --- weights ----------------------------------------------------------------
+    def shapes(self) -> Dict[str, tuple]:
+        c = self.cfg
+        s = {"embed": (c.vocab, c.d_model), "norm": (c.d_model,)}
+        if not c.tie_embeddings:
+            s["lm_head"] = (c.vocab, c.d_model)
+        for i in range(c.n_layers):
+            p = f"l{i}."
+            s[p + "attn_norm"] = (c.d_model,)
+            s[p + "wq"] = (c.n_heads * c.head_dim, c.d_model)
+            s[p + "wk"] = (c.n_kv_heads * c.head_dim, c.d_model)
+            s[p + "wv"] = (c.n_kv_heads * c.head_dim, c.d_model)
+            s[p + "wo"] = (c.d_model, c.n_heads * c.head_dim)
+            s[p + "mlp_norm"] = (c.d_model,)
+            s[p + "w_gate"] = (c.d_ff, c.d_model)
+            s[p + "w_up"] = (c.d_ff, c.d_model)
+            s[p + "w_down"] = (c.d_model, c.d_ff)
+            if c.family == "gemma2":
+                s[p + "post_attn_norm"] = (c.d_model,)
+                s[p + "post_mlp_norm"] = (c.d_model,)
+        return s
+
+    def _init(self, seed: int) -> Dict[str, torch.Tensor]:
+        c = self.cfg
+        gen_dev = self.device if self.device.type == "cuda" else torch.device("cpu")
+        g = torch.Generator(device=gen_dev).manual_seed(seed)
+        w = {}
+        for name, shp in self.shapes().items():
+            if "norm" in name:
+                # llama: weight ~ 1; gemma: (1 + weight) with weight ~ 0
+                base = 0.0 if c.family == "gemma2" else 1.0
+                t = base + 0.1 * torch.randn(shp, generator=g, device=gen_dev)
+            elif name == "embed":
+                t = torch.randn(shp, generator=g, device=gen_dev) * (1.0 if c.family == "llama3" else
+                                                                    1.0 / math.sqrt(c.d_model))
+            else:
+                t = torch.randn(shp, generator=g, device=gen_dev) * c.init_std
+            w[name] = t.to(self.device, self.dtype)
+        return w
+
+    def num_params(self) -> int:
+        return sum(t.numel() for t in self.w.values())
+
+    # --- building blocks --------------------------------------------------------
+    def _rms(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        xf = x.float()
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + c.rms_eps)
+        if c.family == "gemma2":
+            return (y * (1.0 + w.float())).to(x.dtype)
+        return (w * y.to(x.dtype)) if x.dtype != torch.float32 else (w.float() * y)
+
+    def _rope(self, x: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+        """x [B, H, T, D], pos [B, T] (half-rotation convention)."""
+        ang = pos.to(torch.float32)[:, None, :, None] * self.inv_freq[None, None, None, :]
+        cos = torch.cat([ang.cos(), ang.cos()], dim=-1).to(x.dtype)
+        sin = torch.cat([ang.sin(), ang.sin()], dim=-1).to(x.dtype)
+        h = x.shape[-1] // 2
+        rot = torch.cat([-x[..., h:], x[..., :h]], dim=-1)
+        return x * cos + rot * sin
+
+    def _embed(self, ids: torch.Tensor) -> torch.Tensor:
+        h = self.w["embed"][ids]
+        if self.cfg.family == "gemma2":
+            h = h * torch.tensor(self.cfg.d_model ** 0.5, dtype=h.dtype, device=h.device)
+        return h
+
+    def _mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        p = f"l{i}."
+        g = x @ self.w[p + "w_gate"].t()
+        u = x @ self.w[p + "w_up"].t()
+        act = F.gelu(g, approximate="tanh") if self.cfg.family == "gemma2" else F.silu(g)
+        return (act * u) @ self.w[p + "w_down"].t()
+
+    def _attend(self, i: int, q, k, v, mask, q_pos, k_pos):
+        """q [B,H,T,D]; k,v [B,Hkv,S,D]; mask [B,1,T,S] bool (True = attend)."""
+        c = self.cfg
+        rep = c.n_heads // c.n_kv_heads
+        if rep > 1:
+            k = k.repeat_interleave(rep, dim=1)
+            v = v.repeat_interleave(rep, dim=1)
+        if c.sliding_window and i % 2 == 0:
+            mask = mask & ((q_pos[:, None, :, None] - k_pos[:, None, None, :]) < c.sliding_window)
+        scale = (c.query_pre_attn_scalar ** -0.5) if c.query_pre_attn_scalar else c.head_dim ** -0.5
+        if c.attn_softcap > 0:
+            s = (q.float() @ k.float().transpose(-1, -2)) * scale
+            s = c.attn_softcap * torch.tanh(s / c.attn_softcap)
+            s = s.masked_fill(~mask, float("-inf"))
+            p = torch.softmax(s, dim=-1).to(v.dtype)
+            return p @ v
+        return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=scale)
+
+    def _layer(self, i, h, pos, ctx_k, ctx_v, ctx_mask, ctx_pos, self_causal=True):
+        """One decoder layer over new tokens h [B,T,d] at positions pos [B,T].
+
+        ctx_k/ctx_v [B,Hkv,S,D] is the earlier context (prefix + history), visible
+        where ctx_mask [B,S] is True.  Returns (h, k_new, v_new)."""
+        c = self.cfg
+        p = f"l{i}."
+        B, T, _ = h.shape
+        x = self._rms(h, self.w[p + "attn_norm"])
+        q = (x @ self.w[p + "wq"].t()).view(B, T, c.n_heads, c.head_dim).transpose(1, 2)
+        k = (x @ self.w[p + "wk"].t()).view(B, T, c.n_kv_heads, c.head_dim).transpose(1, 2)
+        v = (x @ self.w[p + "wv"].t()).view(B, T, c.n_kv_heads, c.head_dim).transpose(1, 2)
+        q = self._rope(q, pos)
+        k = self._rope(k, pos)
+        causal = torch.ones(T, T, dtype=torch.bool, device=h.device).tril()
+        if ctx_k is not None:
+            K = torch.cat([ctx_k, k], dim=2)
+            V = torch.cat([ctx_v, v], dim=2)
+            S = ctx_k.shape[2]
+            m = torch.cat([ctx_mask[:, None, :].expand(B, T, S), causal[None].expand(B, T, T)], -1)
+            kp = torch.cat([ctx_pos, pos], dim=1)
+        else:
+            K, V, kp = k, v, pos
+            m = causal[None].expand(B, T, T)
+        o = self._attend(i, q, K, V, m[:, None], pos, kp)
+        o = o.transpose(1, 2).reshape(B, T, c.n_heads * c.head_dim) @ self.w[p + "wo"].t()
+        if c.family == "gemma2":
+            o = self._rms(o, self.w[p + "post_attn_norm"])
+        h = h + o
+        x = self._rms(h, self.w[p + "mlp_norm"])
+        y = self._mlp(i, x)
+        if c.family == "gemma2":
+            y = self._rms(y, self.w[p + "post_mlp_norm"])
+        return h + y, k, v
+
+    # --- public forward ----------------------------------------------------------
+    @torch.no_grad()
+    def prefill(self, ids: torch.Tensor, lengths: torch.Tensor):
+        """ids [B, P] right-padded, lengths [B].  Returns (kv list of (k, v) per layer,
+        final-norm hidden [B, P, d])."""
+        B, P = ids.shape
+        pos = torch.arange(P, device=ids.device)[None].expand(B, P)
+        valid = pos < lengths[:, None]
+        h = self._embed(ids)
+        kv = []
+        for i in range(self.cfg.n_layers):
+            # padding keys sit after every valid key, so the causal mask already hides them
+            h, k, v = self._layer(i, h, pos, None, None, None, None)
+            kv.append((k, v))
+        h = self._rms(h, self.w["norm"])
+        return kv, h, valid
+
+    @torch.no_grad()
+    def extend(self, tokens: torch.Tensor, pos: torch.Tensor, ctx_kv, ctx_mask: torch.Tensor,
+               ctx_pos: torch.Tensor):
+        """tokens [R, T], pos [R, T]; ctx_kv per layer (k, v) [R, Hkv, S, D] with
+        ctx_mask [R, S].  Returns (final-norm hidden [R, T, d], new kv per layer)."""
+        h = self._embed(tokens)
+        new = []
+        for i in range(self.cfg.n_layers):
+            ck, cv = ctx_kv[i] if ctx_kv is not None else (None, None)
+            h, k, v = self._layer(i, h, pos, ck, cv, ctx_mask, ctx_pos)
+            new.append((k, v))
+        return self._rms(h, self.w["norm"]), new
+
+    def lm_head(self, h: torch.Tensor) -> torch.Tensor:
+        W = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
+        return h.to(W.dtype) @ W.t()
+
+
+def hf_state_dict(model: Model) -> Dict[str, torch.Tensor]:
+    """Map weights to Hugging Face Llama/Gemma2 names (for the independent CPU oracle)."""
+    c = model.cfg
+    w = model.w
+    sd = {"model.embed_tokens.weight": w["embed"], "model.norm.weight": w["norm"]}
+    sd["lm_head.weight"] = w["embed"] if c.tie_embeddings else w["lm_head"]
+    for i in range(c.n_layers):
+        p, q = f"l{i}.", f"model.layers.{i}."
+        sd[q + "self_attn.q_proj.weight"] = w[p + "wq"]
+        sd[q + "self_attn.k_proj.weight"] = w[p + "wk"]
+        sd[q + "self_attn.v_proj.weight"] = w[p + "wv"]
+        sd[q + "self_attn.o_proj.weight"] = w[p + "wo"]
+        sd[q + "mlp.gate_proj.weight"] = w[p + "w_gate"]
+        sd[q + "mlp.up_proj.weight"] = w[p + "w_up"]
+        sd[q + "mlp.down_proj.weight"] = w[p + "w_down"]
+        sd[q + "input_layernorm.weight"] = w[p + "attn_norm"]
+        if c.family == "gemma2":
+            sd[q + "post_attention_layernorm.weight"] = w[p + "post_attn_norm"]
+            sd[q + "pre_feedforward_layernorm.weight"] = w[p + "mlp_norm"]
+            sd[q + "post_feedforward_layernorm.weight"] = w[p + "post_mlp_norm"]
+        else:
+            sd[q + "post_attention_layernorm.weight"] = w[p + "mlp_norm"]
+    return sd

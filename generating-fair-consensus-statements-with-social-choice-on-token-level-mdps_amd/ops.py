@@ -93,7 +93,10 @@ def logsoftmax_gather(logits: torch.Tensor, targets: Optional[torch.Tensor], *, 
     else:
         if targets.dtype != torch.int32:
             raise CSError("targets must be int32")
-        targets = targets.reshape(rows, -1)
+        if targets.dim() != 2 or targets.shape[0] != rows:
+            if rows == 0 or targets.numel() % rows != 0:
+                raise CSError("targets must be [rows, k]")
+            targets = targets.reshape(rows, -1)
         if not targets.is_contiguous():
             targets = targets.contiguous()
         k = targets.shape[1]
@@ -188,3 +191,64 @@ def topk(W: torch.Tensor, k: int, *, with_values: bool = True):
     if W.dim() == 1:
         return idx[0], (val[0] if val is not None else None)
     return idx, val
+
+
+def _logits_args(logits: torch.Tensor, vocab: Optional[int]):
+    if logits.dim() != 2 or logits.stride(1) != 1:
+        raise CSError("logits must be 2-D with unit column stride")
+    if logits.dtype not in _DTYPE:
+        raise CSError(f"unsupported logits dtype {logits.dtype}")
+    rows = logits.shape[0]
+    ld = logits.stride(0) if rows > 1 else logits.shape[1]
+    vocab = logits.shape[1] if vocab is None else int(vocab)
+    if vocab > logits.shape[1]:
+        raise CSError("vocab exceeds logits width")
+    return rows, ld, vocab
+
+
+def vocab_topk(logits: torch.Tensor, k: int, *, vocab: Optional[int] = None, softcap: float = 0.0,
+               workspace: Optional[Workspace] = None):
+    """Top-k token ids (value desc, id asc) of every logits row -> (ids [rows, k] int32,
+    values [rows, k] f32).  The deterministic beam-candidate proposer replacing the
+    reference's repeated one-token sampling (beam_search.py:199-333)."""
+    L = _lib.load()
+    rows, ld, vocab = _logits_args(logits, vocab)
+    _require_cuda(logits)
+    ids = torch.empty((rows, k), dtype=torch.int32, device=logits.device)
+    vals = torch.empty((rows, k), dtype=torch.float32, device=logits.device)
+    nbytes = int(L.cs_vocab_topk_workspace_size(rows, vocab, k))
+    if workspace is None:
+        workspace = _default_ws.setdefault(logits.device, Workspace())
+    ws = workspace.get(nbytes, logits.device)
+    rc = L.cs_vocab_topk(logits.data_ptr(), _DTYPE[logits.dtype], rows, vocab, ld, int(k),
+                         float(softcap), ids.data_ptr(), vals.data_ptr(),
+                         ws.data_ptr() if ws is not None else None,
+                         ws.numel() if ws is not None else 0, _stream())
+    _lib.check(rc, "cs_vocab_topk")
+    return ids, vals
+
+
+def vocab_sample(logits: torch.Tensor, seeds: torch.Tensor, *, temperature: float = 1.0,
+                 vocab: Optional[int] = None, softcap: float = 0.0,
+                 workspace: Optional[Workspace] = None):
+    """Seeded Gumbel-max draws: seeds [rows, n_draw] int64 (bit pattern used as uint64) ->
+    (ids [rows, n_draw] int32, log-probs [rows, n_draw] f32)."""
+    L = _lib.load()
+    rows, ld, vocab = _logits_args(logits, vocab)
+    seeds = seeds.reshape(rows, -1)
+    if seeds.dtype != torch.int64 or not seeds.is_contiguous():
+        raise CSError("seeds must be a contiguous int64 tensor [rows, n_draw]")
+    _require_cuda(logits, seeds)
+    n_draw = seeds.shape[1]
+    ids = torch.empty((rows, n_draw), dtype=torch.int32, device=logits.device)
+    lp = torch.empty((rows, n_draw), dtype=torch.float32, device=logits.device)
+    nbytes = int(L.cs_vocab_sample_workspace_size(rows, vocab, n_draw))
+    if workspace is None:
+        workspace = _default_ws.setdefault(logits.device, Workspace())
+    ws = workspace.get(nbytes, logits.device)
+    rc = L.cs_vocab_sample(logits.data_ptr(), _DTYPE[logits.dtype], rows, vocab, ld,
+                           float(temperature), float(softcap), seeds.data_ptr(), n_draw,
+                           ids.data_ptr(), lp.data_ptr(), ws.data_ptr() if ws is not None else None,
+                           ws.numel() if ws is not None else 0, _stream())
+    _lib.check(rc, "cs_vocab_sample")
+    return ids, lp

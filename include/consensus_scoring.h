@@ -138,6 +138,44 @@ int cs_welfare_reduce(const float* U, int32_t A, int32_t C, int64_t ldu, int kin
 int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld, int32_t k,
                       int32_t* out_idx, float* out_val, cs_stream_t stream);
 
+/*
+ * cs_vocab_topk — deterministic candidate proposer: the k largest (soft-capped)
+ * logits of every row, ordered by (value desc, token id asc).
+ *
+ * Replaces the serial unique-token sampling loop of the reference's beam search
+ * (_sample_next_tokens, src/methods/beam_search.py:199-333: up to
+ * max_sampling_attempts remote completions per beam) with one HBM pass per step;
+ * k is the build's deterministic "top-k tokens per beam" (BASELINE configs).
+ * Logit-bias masking (beam_search.py:236-251) is applied by the caller to the
+ * logits rows before the call.  k <= 256 and ceil(vocab/4096)*k <= 16384.
+ * out_vals may be NULL.
+ */
+size_t cs_vocab_topk_workspace_size(int64_t rows, int64_t vocab, int32_t k);
+int cs_vocab_topk(const void* logits, int dtype, int64_t rows, int64_t vocab, int64_t ld, int32_t k,
+                  float softcap, int32_t* out_ids, float* out_vals, void* workspace,
+                  size_t workspace_bytes, cs_stream_t stream);
+
+/*
+ * cs_vocab_sample — seeded Gumbel-max sampling, n_draw independent draws per row.
+ *
+ * Draw d of row r returns argmax_v ( x'[r,v] / temperature + g(seeds[r*n_draw+d], v) ),
+ * ties to the lowest id, with g = -log(-log(u)) and u the counter-based uniform
+ * documented in oracle/oracle.py (splitmix64 of (seed, v), top 23 bits + 0.5, scaled by 2^-23).
+ * out_lp (nullable) receives the drawn token's log-probability under
+ * softmax(x'/temperature).  n_draw <= 16.
+ *
+ * Replaces the remote one-token samplers: client.completions.create(max_tokens=1,
+ * seed=base_seed+attempt, logit_bias) (src/methods/beam_search.py:253-297),
+ * generate_text(max_tokens=1, temperature=1, seed) in the lookahead tree
+ * (src/methods/finite_lookahead.py:310-334) and the per-token draws of the
+ * Best-of-N candidate generation (src/methods/best_of_n.py:104-118).
+ */
+size_t cs_vocab_sample_workspace_size(int64_t rows, int64_t vocab, int32_t n_draw);
+int cs_vocab_sample(const void* logits, int dtype, int64_t rows, int64_t vocab, int64_t ld,
+                    float temperature, float softcap, const uint64_t* seeds, int32_t n_draw,
+                    int32_t* out_ids, float* out_lp, void* workspace, size_t workspace_bytes,
+                    cs_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

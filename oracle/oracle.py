@@ -155,3 +155,39 @@ def bf16_bits(x: np.ndarray) -> np.ndarray:
 
 def bf16_to_f32(bits: np.ndarray) -> np.ndarray:
     return (bits.astype(np.uint32) << 16).view(np.float32)
+
+
+# --- candidate proposer (restates the product's counter-based RNG bit for bit) -----
+_M64 = (1 << 64) - 1
+
+
+def cs_uniform(seed: int, v: np.ndarray) -> np.ndarray:
+    """u(seed, v) in (0, 1): splitmix64 finaliser of (seed, v), top 23 bits + 0.5 over 2^23.
+    Exactly the device function cs_uniform in csrc/consensus_scoring.hip."""
+    with np.errstate(over="ignore"):
+        x = (np.uint64(seed & _M64) * np.uint64(0x9E3779B97F4A7C15)
+             + (np.asarray(v, dtype=np.uint64) + np.uint64(1)) * np.uint64(0xD1B54A32D192ED03))
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return ((x >> np.uint64(41)).astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -23)
+
+
+def gumbel_sample(logits_row: np.ndarray, seed: int, temperature: float = 1.0):
+    """argmax_v x[v]/T + g(seed, v), first index on ties; returns (id, log-prob of id)."""
+    x = np.asarray(logits_row, dtype=np.float64) / temperature
+    u = cs_uniform(seed, np.arange(x.shape[0])).astype(np.float64)
+    s = x - np.log(-np.log(u))
+    i = int(np.argmax(s))
+    mx = x.max()
+    lse = mx + np.log(np.exp(x - mx).sum())
+    return i, float(x[i] - lse)
+
+
+def vocab_topk(logits: np.ndarray, k: int):
+    """Top-k ids per row ordered by (value desc, id asc) -> (ids, values)."""
+    x = np.asarray(logits, dtype=np.float64)
+    ids = topk(x, k)
+    return ids, np.take_along_axis(x, ids, 1)

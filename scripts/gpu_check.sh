@@ -1,0 +1,24 @@
+#!/usr/bin/env bash
+# One GPU round-trip: parity tests, smoke, bench, kernel-trace profile.  Every GPU
+# step has its own time limit and the chain stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+OUT="$R/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEP="${1:-all}"
+run_tests() { timeout -k 10 420 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/gpu_tests.log" 2>&1; }
+run_smoke() { timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; }
+run_bench() { timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; }
+run_prof() {
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
+     python3 "$R/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/prof.log" 2>&1)
+}
+case "$STEP" in
+  tests) run_tests ;;
+  bench) run_bench ;;
+  prof) run_prof ;;
+  all) run_tests; rc=$?; echo "tests rc=$rc" ; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+       run_smoke && run_bench && run_prof ;;
+esac

@@ -131,3 +131,11 @@ def test_oracle_softcap_and_out_of_range(orc):
     ref = orc.log_softmax_rows_np(capped)
     assert abs(tok[0, 0] - ref[0, 3]) < 1e-12 and abs(tok[1, 1] - ref[1, 7]) < 1e-12
     assert np.isnan(tok[0, 1]) and np.isnan(tok[1, 0])
+
+
+def test_oracle_uniform_is_strictly_inside_unit_interval(orc):
+    u = orc.cs_uniform(123456789, np.arange(1 << 20))
+    assert u.dtype == np.float32 and u.min() > 0 and u.max() < 1
+    assert abs(float(u.mean()) - 0.5) < 2e-3
+    assert np.array_equal(u, orc.cs_uniform(123456789, np.arange(1 << 20)))
+    assert not np.array_equal(u[:100], orc.cs_uniform(123456790, np.arange(100)))
