@@ -35,6 +35,8 @@ class PrefixCache:
     last_hidden: torch.Tensor   # [n_prefix, d] final-norm hidden at position length-1
     pos: torch.Tensor           # [n_prefix, Pmax] key positions
     valid: torch.Tensor         # [n_prefix, Pmax] bool
+    hidden: torch.Tensor        # [n_prefix, Pmax, d] final-norm hidden of every position
+    ids: torch.Tensor           # [n_prefix, Pmax] prefix token ids (right-padded)
 
 
 def _pad(seqs: Sequence[Sequence[int]], device, fill: int = 0):
@@ -71,7 +73,42 @@ class ScoringEngine:
         last = h[torch.arange(h.shape[0], device=self.device), lens - 1]
         P = ids.shape[1]
         pos = torch.arange(P, device=self.device)[None].expand(ids.shape[0], P)
-        return PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid)
+        return PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid, hidden=h,
+                           ids=ids)
+
+    @torch.no_grad()
+    def prefix_tail_logprobs(self, cache: PrefixCache, m: int) -> torch.Tensor:
+        """log p of the last m tokens of every prefix given what precedes them
+        ([n_prefix, m], NaN where the prefix is shorter than m + 1)."""
+        n = cache.lengths.shape[0]
+        if m <= 0:
+            return torch.empty(n, 0, dtype=torch.float32, device=self.device)
+        j = cache.lengths[:, None] - m + torch.arange(m, device=self.device)[None]   # token pos
+        ok = j >= 1
+        jj = j.clamp(min=1)
+        rows = torch.arange(n, device=self.device)[:, None]
+        h = cache.hidden[rows, jj - 1].reshape(n * m, -1)
+        t = cache.ids[rows, jj].reshape(n * m, 1)
+        lp = self.rows_logprobs(h, t).view(n, m)
+        return torch.where(ok, lp, torch.full_like(lp, float("nan")))
+
+    @torch.no_grad()
+    def next_hidden(self, cache: PrefixCache, owner: Sequence[int],
+                    conts: Sequence[Sequence[int]]) -> torch.Tensor:
+        """Hidden state predicting the token that follows prefix[owner[r]] + conts[r]."""
+        dev = self.device
+        own = torch.as_tensor(list(owner), dtype=torch.long, device=dev)
+        out = cache.last_hidden[own].clone()
+        if not any(len(c) for c in conts):
+            return out
+        toks, lens = _pad(conts, dev)
+        pos = cache.lengths[own][:, None] + torch.arange(toks.shape[1], device=dev)[None]
+        ctx = [(k[own], v[own]) for k, v in cache.kv]
+        h, _ = self.model.extend(toks, pos, ctx, cache.valid[own], cache.pos[own])
+        has = lens > 0
+        idx = (lens - 1).clamp(min=0)
+        hl = h[torch.arange(len(conts), device=dev), idx]
+        return torch.where(has[:, None], hl, out)
 
     # --- one logits block -> token log-probs --------------------------------------
     def rows_logprobs(self, hidden: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:

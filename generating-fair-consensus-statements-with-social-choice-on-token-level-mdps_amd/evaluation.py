@@ -1,0 +1,143 @@
+"""Drop-in for the log-probability utilities + welfare of the reference's evaluator.
+
+``StatementEvaluator(evaluation_model, ...).evaluate_statement(statement, issue,
+agent_opinions) -> dict`` (src/evaluation.py:50-634) with the same result keys for
+the log-probability block (src/evaluation.py:177-394):
+
+  avg_logprob_<agent> / utility_avg_logprob_<agent>   mean token log-prob      (:203-229)
+  perplexity_<agent>                                  exp(-avg_logprob)        (:329-335)
+  egalitarian / utilitarian / log_nash _welfare_avg_prob and utility_*_logprob
+                                                      min / sum / sum log(max(u, 1e-9))
+                                                      over avg_prob = mean exp(lp)  (:337-364)
+  egalitarian / utilitarian / log_nash _welfare_perplexity
+                                                      max / sum / sum log(1/max(ppl, 1e-9))
+                                                                                (:367-394)
+
+All agents of all statements are scored in ONE batched pass (per-agent prefix K/V,
+cs_logsoftmax_gather, cs_segment_reduce for mean log-prob AND mean prob in one
+fold) and every welfare is a cs_welfare_reduce launch over [agents, statements].
+
+Embedding cosine similarity, LLM-as-judge and comparative ranking are remote-API
+metrics outside this build: their keys are present and NaN/None,
+exactly as the reference reports them when those services are unavailable.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import ops, runtime, utils
+from .methods.prompts import EVAL_SYSTEM
+
+EPS = 1e-9
+
+
+class StatementEvaluator:
+    def __init__(self, evaluation_model: str, llm_judge_model: Optional[str] = None,
+                 openai_client: Optional[Any] = None, include_llm_judge: bool = False,
+                 include_comparative_ranking: bool = True,
+                 embedding_model: str = "BAAI/bge-large-en-v1.5", verbose: bool = True):
+        self.evaluation_model = evaluation_model
+        self.embedding_model = embedding_model
+        self.verbose = verbose
+        self.llm_judge_model = llm_judge_model
+        self.openai_client = openai_client
+        # remote-only metrics: disabled, as the reference does without an OpenAI client
+        self.include_llm_judge = False
+        self.include_comparative_ranking = False
+        self._judge_requested = include_llm_judge
+
+    # --- batched core ---------------------------------------------------------------
+    def agent_utilities(self, statements: List[str], issue: str, agent_opinions: Dict[str, str]):
+        """Per (agent, statement): mean log-prob and mean prob, as [A, S] device tensors."""
+        engine, tok = runtime.get_engine(self.evaluation_model)
+        prefixes = [tok.chat_prefix(EVAL_SYSTEM.format(issue=issue, opinion=op), "")
+                    for op in agent_opinions.values()]
+        cache = engine.prefill(prefixes)
+        A, S = len(prefixes), len(statements)
+        ids = [tok.encode(s) for s in statements]
+        owner = [a for a in range(A) for _ in range(S)]
+        conts = [ids[s] for _ in range(A) for s in range(S)]
+        lp = engine.score(cache, owner, conts)
+        seg = ops.segment_reduce(lp, engine.offsets(conts, engine.device))
+        cnt = seg["count"].to(torch.float32).view(A, S)
+        nan = torch.full_like(cnt, float("nan"))
+        avg_lp = torch.where(cnt > 0, seg["sum_lp"].view(A, S) / cnt.clamp(min=1), nan)
+        avg_p = torch.where(cnt > 0, seg["sum_p"].view(A, S) / cnt.clamp(min=1), nan)
+        # pairs whose user prompt the reference's find() locates elsewhere: text-compat path
+        for a, op in enumerate(agent_opinions.values()):
+            system = EVAL_SYSTEM.format(issue=issue, opinion=op)
+            for si, st in enumerate(statements):
+                if not utils.span_found_at_user(tok, system, st):
+                    m_lp, m_p, _ = utils.text_compat_mean(self.evaluation_model, system, st)
+                    avg_lp[a, si] = m_lp
+                    avg_p[a, si] = m_p
+        return avg_lp.contiguous(), avg_p.contiguous()
+
+    def evaluate_statements_batched(self, statements: List[str], issue: str,
+                                    agent_opinions: Dict[str, str]) -> List[Dict[str, Any]]:
+        t0 = time.time()
+        agents = list(agent_opinions)
+        avg_lp, avg_p = self.agent_utilities(statements, issue, agent_opinions)
+        ppl = torch.exp(-avg_lp)
+        inv_ppl = 1.0 / torch.clamp(ppl, min=EPS)
+        w = {
+            "egalitarian_welfare_avg_prob": ops.welfare(avg_p, "min"),
+            "utilitarian_welfare_avg_prob": ops.welfare(avg_p, "sum"),
+            "log_nash_welfare_avg_prob": ops.welfare(avg_p, "sumlog", eps=EPS),
+            "egalitarian_welfare_perplexity": ops.welfare(ppl.contiguous(), "max"),
+            "utilitarian_welfare_perplexity": ops.welfare(ppl.contiguous(), "sum"),
+            "log_nash_welfare_perplexity": ops.welfare(inv_ppl.contiguous(), "sumlog",
+                                                       eps=1e-38),
+        }
+        w = {k: v.double().cpu().numpy() for k, v in w.items()}
+        lp_h = avg_lp.double().cpu().numpy()
+        ppl_h = ppl.double().cpu().numpy()
+        out = []
+        for s in range(len(statements)):
+            r: Dict[str, Any] = {"statement_embedding": None}
+            for a, aid in enumerate(agents):
+                v = lp_h[a, s]
+                r[f"avg_logprob_{aid}"] = None if math.isnan(v) else float(v)
+                r[f"utility_avg_logprob_{aid}"] = r[f"avg_logprob_{aid}"]
+                r[f"cosine_similarity_{aid}"] = None
+                r[f"utility_cosine_similarity_{aid}"] = None
+            for key in ("egalitarian_welfare_cosine", "utilitarian_welfare_cosine",
+                        "log_nash_welfare_cosine", "utility_egalitarian_welfare_cosine",
+                        "utility_utilitarian_welfare_cosine", "utility_log_nash_welfare_cosine"):
+                r[key] = np.nan
+            for a, aid in enumerate(agents):
+                if not math.isnan(lp_h[a, s]) and math.isfinite(lp_h[a, s]):
+                    r[f"perplexity_{aid}"] = float(ppl_h[a, s])
+            for kind in ("egalitarian", "utilitarian", "log_nash"):
+                val = float(w[f"{kind}_welfare_avg_prob"][s])
+                r[f"{kind}_welfare_avg_prob"] = val
+                r[f"utility_{kind}_welfare_logprob"] = val
+            for kind in ("egalitarian", "utilitarian", "log_nash"):
+                r[f"{kind}_welfare_perplexity"] = float(w[f"{kind}_welfare_perplexity"][s])
+            if self._judge_requested:
+                for key in ("egalitarian_welfare_llm_judge", "utilitarian_welfare_llm_judge",
+                            "log_nash_welfare_llm_judge", "llm_judge_egalitarian_welfare",
+                            "llm_judge_utilitarian_welfare", "llm_judge_log_nash_welfare"):
+                    r[key] = np.nan
+            r["evaluation_time_s"] = (time.time() - t0) / max(1, len(statements))
+            out.append(r)
+        return out
+
+    # --- reference entry points -----------------------------------------------------
+    def evaluate_statement(self, statement: str, issue: str,
+                           agent_opinions: Dict[str, str]) -> Dict[str, Any]:
+        r = self.evaluate_statements_batched([statement], issue, agent_opinions)[0]
+        r.pop("evaluation_time_s", None)
+        return r
+
+
+def evaluate_statement(statement: str, issue: str, agent_opinions: dict,
+                       evaluation_model: str) -> dict:
+    """Legacy module-level entry point (src/evaluation.py:1433-1470)."""
+    return StatementEvaluator(evaluation_model, include_comparative_ranking=False,
+                              verbose=False).evaluate_statement(statement, issue, agent_opinions)

@@ -1,0 +1,165 @@
+"""Model-identifier -> scoring engine registry, and seeded generation on the engine.
+
+The reference resolves a model identifier (e.g. "meta-llama/Meta-Llama-3.1-8B-Instruct-Turbo")
+to a remote endpoint through the module-global Together ``client`` (src/utils.py:69-74).
+Here the identifier resolves to a local ``ScoringEngine`` on the current HIP device:
+either one registered explicitly (``register_engine``; tests register the parity
+fixture model this way) or an architecture-exact, random-initialised model built
+from the preset whose name the identifier mentions (no checkpoints offline).
+
+Seed semantics of the local samplers (the replacement for the remote API's
+``seed`` argument) are defined here once and restated by the test fake client:
+  * a one-token draw with seed s uses the counter-based Gumbel noise g(s, v)
+    (cs_vocab_sample);
+  * token t of a multi-token generation with seed s uses seed ``draw_seed(s, t)``.
+"""
+from __future__ import annotations
+
+import os
+import re
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+from .engine import BeamState, ScoringEngine
+from .model import Model, preset
+from .tokenizer import CharTokenizer
+
+_M64 = (1 << 64) - 1
+_lock = threading.RLock()
+_ENGINES: Dict[str, Tuple[ScoringEngine, CharTokenizer]] = {}
+
+_NAME_TO_PRESET = [
+    (r"3\.3-70b|llama-3\.3-70b|70b", "llama-3.3-70b"),
+    (r"3\.1-8b|llama-3\.1-8b|8b", "llama-3.1-8b"),
+    (r"3\.2-1b|1b", "llama-3.2-1b"),
+    (r"gemma-2-9b|gemma", "gemma-2-9b"),
+    (r"tiny-gemma", "tiny-gemma"),
+    (r"tiny", "tiny-llama"),
+]
+
+
+def draw_seed(seed: int, t: int) -> int:
+    """Seed of token t of a seeded multi-token generation."""
+    return (int(seed) * 1000003 + int(t)) & _M64
+
+
+def to_i64(seed: int) -> int:
+    """uint64 seed -> the int64 bit pattern torch stores."""
+    seed &= _M64
+    return seed - (1 << 64) if seed >= (1 << 63) else seed
+
+
+def fresh_seed() -> int:
+    return int.from_bytes(os.urandom(8), "little")
+
+
+def register_engine(model_identifier: str, engine: ScoringEngine, tokenizer: CharTokenizer) -> None:
+    with _lock:
+        _ENGINES[model_identifier] = (engine, tokenizer)
+
+
+def clear_engines() -> None:
+    with _lock:
+        _ENGINES.clear()
+
+
+def resolve_preset(model_identifier: str) -> str:
+    name = model_identifier.lower()
+    for pat, pre in _NAME_TO_PRESET[::-1] if name.startswith("tiny") else _NAME_TO_PRESET:
+        if re.search(pat, name):
+            return pre
+    raise ValueError(f"no local architecture known for model identifier {model_identifier!r}")
+
+
+def get_engine(model_identifier: str) -> Tuple[ScoringEngine, CharTokenizer]:
+    with _lock:
+        if model_identifier in _ENGINES:
+            return _ENGINES[model_identifier]
+        if not torch.cuda.is_available():
+            raise ops.CSError("no HIP device: the scoring engine has no CPU path")
+        cfg = preset(resolve_preset(model_identifier))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        model = Model(cfg, dev, torch.bfloat16, seed=0)
+        tok = CharTokenizer("gemma2" if cfg.family == "gemma2" else "llama3")
+        ent = (ScoringEngine(model), tok)
+        _ENGINES[model_identifier] = ent
+        return ent
+
+
+# --- logit bias -------------------------------------------------------------------
+def bias_token_ids(tok: CharTokenizer, strings: Optional[Sequence[str]]) -> List[int]:
+    """Ids the reference biases for ``strings``.
+
+    Semantics of get_token_ids (src/utils.py:466-525: token map of the chat-rendered
+    single-user-message prompt) followed by the containment filter
+    ``{t: id for t, id in map.items() if s in t}`` (src/utils.py:124-136,
+    src/methods/beam_search.py:240-251).
+    """
+    if not strings:
+        return []
+    if isinstance(strings, str):
+        strings = [strings]
+    out: List[int] = []
+    for s in strings:
+        ids, _ = tok.render_chat(None, s)
+        tmap = {}
+        for i in ids:
+            tmap[tok.token_str(i)] = i
+        for t, i in tmap.items():
+            if s in t and i not in out:
+                out.append(i)
+    return out
+
+
+def apply_bias(logits: torch.Tensor, ids: Sequence[int], value: float) -> torch.Tensor:
+    if ids:
+        idx = torch.as_tensor(list(ids), dtype=torch.long, device=logits.device)
+        logits[:, idx] = logits[:, idx] + value
+    return logits
+
+
+# --- seeded generation on the engine ------------------------------------------------
+@torch.no_grad()
+def generate(engine: ScoringEngine, tok: CharTokenizer, prefix_ids: Sequence[int],
+             seeds: Sequence[Optional[int]], max_tokens: int, temperature: float = 1.0,
+             bias_ids: Sequence[int] = (), bias_value: float = -1e6,
+             stop_ids: Optional[Sequence[int]] = None) -> List[List[int]]:
+    """Sample len(seeds) continuations of one prefix in a batch (token t of stream i
+    drawn with seed draw_seed(seeds[i], t)); a stream stops after a stop token (not
+    included) or max_tokens tokens."""
+    n = len(seeds)
+    seeds = [fresh_seed() if s is None else int(s) for s in seeds]
+    stop = set(tok.eos_ids if stop_ids is None else stop_ids)
+    out: List[List[int]] = [[] for _ in range(n)]
+    if n == 0 or max_tokens <= 0:
+        return out
+    cache = engine.prefill([list(prefix_ids)])
+    st = BeamState(engine, cache, n_prefix=1)
+    alive = list(range(n))          # stream ids, in beam order
+    dev = engine.device
+    for t in range(max_tokens):
+        logits = st.next_logits(0).float() if st.n_beams == len(alive) else None
+        if st.n_beams == 1 and len(alive) > 1:
+            logits = engine.model.lm_head(st.next_hidden).float().expand(len(alive), -1).contiguous()
+        logits = apply_bias(logits, bias_ids, bias_value)
+        sd = torch.tensor([[to_i64(draw_seed(seeds[i], t))] for i in alive], dtype=torch.int64,
+                          device=dev)
+        ids, _ = ops.vocab_sample(logits, sd, temperature=temperature, softcap=engine.softcap)
+        ids = ids[:, 0].tolist()
+        parent, toks, nxt = [], [], []
+        for j, (i, v) in enumerate(zip(alive, ids)):
+            if v in stop:
+                continue
+            out[i].append(v)
+            if t + 1 < max_tokens:
+                parent.append(0 if st.n_beams == 1 else j)
+                toks.append(v)
+                nxt.append(i)
+        if not nxt:
+            break
+        st.advance(parent, toks)
+        alive = nxt
+    return out

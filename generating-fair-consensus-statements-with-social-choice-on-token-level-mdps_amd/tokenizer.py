@@ -50,6 +50,7 @@ class CharTokenizer:
         self.bos_id = self.special_ids[self.bos]
         self.eos_id = self.special_ids[self.eos]
         self.eos_ids = tuple(self.special_ids[s] for s in self.eos_strings)
+        self._specials_by_len = sorted(specials, key=len, reverse=True)
 
     @property
     def vocab_size(self) -> int:
@@ -57,8 +58,29 @@ class CharTokenizer:
 
     # --- plain text ---------------------------------------------------------------
     def encode(self, text: str) -> List[int]:
+        """Characters -> ids; special-token strings in the text map to their special id
+        (so a sampled special token survives the reference's string round trip)."""
         cid = self.char_to_id
-        return [cid.get(c, self.unk_id) for c in text]
+        if "<" not in text:
+            return [cid.get(c, self.unk_id) for c in text]
+        out: List[int] = []
+        i, n = 0, len(text)
+        specials = self._specials_by_len
+        while i < n:
+            c = text[i]
+            if c == "<":
+                for sp in specials:
+                    if text.startswith(sp, i):
+                        out.append(self.special_ids[sp])
+                        i += len(sp)
+                        break
+                else:
+                    out.append(cid.get(c, self.unk_id))
+                    i += 1
+            else:
+                out.append(cid.get(c, self.unk_id))
+                i += 1
+        return out
 
     def decode(self, ids: Iterable[int]) -> str:
         n = len(self.id_to_str)

@@ -1,0 +1,175 @@
+"""Drop-in for the reference's LLM access shim (src/utils.py), served locally.
+
+Same function names, arguments, return shapes and failure sentinels as the
+reference; the remote Together calls are replaced by the local scoring engine:
+
+  get_prompt_logprobs(model, system_prompt, user_prompt, ...)     src/utils.py:201-281
+      chat-template render (with the reference's U+200B marker when the user prompt
+      ends in a space or newline, :224-233) -> one forward over the whole prompt ->
+      cs_logsoftmax_gather over every prompt position (the echo=True prompt
+      log-probs) -> the user span by character overlap (:284-373).
+      Never raises: ([], []) on any failure (:274-281).
+  extract_user_prompt_logprobs(logprobs_data, user_prompt)         src/utils.py:284-373
+  generate_text(...)                                                src/utils.py:77-198
+  get_token_ids(model, text)                                        src/utils.py:466-525
+  create_method_identifier(...)                                     src/utils.py:19-62
+
+This text-compat path reproduces the reference's string-level semantics exactly
+(including its first-occurrence ``find`` of the user prompt).  The methods use the
+batched id-level engine instead (engine.py), which scores the true user span.
+"""
+from __future__ import annotations
+
+import logging
+from types import SimpleNamespace
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+
+import torch
+
+from . import ops
+from . import runtime
+
+logger = logging.getLogger(__name__)
+
+MARKER = "\u200b"  # zero-width space appended by src/utils.py:224-233
+
+IMPORTANT_PARAMETERS = ["n", "num_candidates", "num_rounds", "branching_factor", "max_depth",
+                        "beam_width"]
+
+
+def create_method_identifier(method_name: str, params_dict: Optional[Dict[str, Any]] = None,
+                             include_seed: bool = False,
+                             seed_value: Optional[Union[int, str]] = None) -> str:
+    """'name (k=v, ...) [seed=s]' with the important parameters only, sorted (utils.py:19-62)."""
+    parts = []
+    for key, value in (params_dict or {}).items():
+        name = key[len("param_"):] if key.startswith("param_") else key
+        if name in IMPORTANT_PARAMETERS and value is not None:
+            parts.append(f"{name}={value}")
+    ident = f"{method_name} ({', '.join(sorted(parts))})" if parts else method_name
+    if include_seed and seed_value is not None:
+        ident += f" [seed={seed_value}]"
+    return ident
+
+
+@torch.no_grad()
+def prompt_logprobs_ids(model: str, ids: Sequence[int]) -> List[Optional[float]]:
+    """log p(ids[i] | ids[:i]) for every position (None for position 0): the echo=True
+    prompt log-probs, computed by one forward + cs_logsoftmax_gather."""
+    engine, _ = runtime.get_engine(model)
+    m = engine.model
+    dev = engine.device
+    t = torch.as_tensor(list(ids), dtype=torch.long, device=dev)[None]
+    _, h, _ = m.prefill(t, torch.tensor([len(ids)], device=dev))
+    if len(ids) < 2:
+        return [None] * len(ids)
+    rows = h[0, :-1]
+    tgt = t[0, 1:].to(torch.int32)[:, None]
+    lp = engine.rows_logprobs(rows, tgt).view(-1).double().cpu().tolist()
+    return [None] + lp
+
+
+def get_prompt_logprobs(model, system_prompt, user_prompt, temperature=1.0, terminators=(),
+                        seed=None) -> Tuple[List[str], List[Optional[float]]]:
+    """(user_tokens, user_logprobs) of the user prompt under the chat template."""
+    try:
+        _, tok = runtime.get_engine(model)
+        api_user = user_prompt
+        if user_prompt.endswith("\n") or user_prompt.endswith(" "):
+            api_user += MARKER
+        ids, _ = tok.render_chat(system_prompt or None, api_user)
+        lps = prompt_logprobs_ids(model, ids)
+        data = SimpleNamespace(tokens=tok.tokens(ids), token_logprobs=lps, token_ids=list(ids))
+        return extract_user_prompt_logprobs(data, user_prompt)
+    except Exception as e:  # the reference never raises here (src/utils.py:274-281)
+        logger.error("get_prompt_logprobs failed: %s", e)
+        return [], []
+
+
+def extract_user_prompt_logprobs(logprobs_data, user_prompt):
+    """Tokens whose character span overlaps the first occurrence of ``user_prompt`` in
+    the concatenated token strings, with their log-probs (src/utils.py:284-373)."""
+    if (not logprobs_data or not hasattr(logprobs_data, "tokens")
+            or not hasattr(logprobs_data, "token_logprobs")):
+        return [], []
+    toks, lps = logprobs_data.tokens, logprobs_data.token_logprobs
+    if len(toks) != len(lps):
+        return [], []
+    text = "".join(toks)
+    lo = text.find(user_prompt)
+    if lo == -1:
+        return [], []
+    hi = lo + len(user_prompt)
+    keep = []
+    pos = 0
+    for i, t in enumerate(toks):
+        a, b = pos, pos + len(t)
+        if max(a, lo) < min(b, hi):
+            keep.append(i)
+        pos = b
+        if a >= hi:
+            break
+    if not keep:
+        return [], []
+    return [toks[i] for i in keep], [lps[i] for i in keep]
+
+
+def span_found_at_user(tok, system_prompt, user_prompt) -> bool:
+    """True when the reference's first-occurrence ``find`` of the user prompt lands on the
+    user turn itself (src/utils.py:321-327).  False means the reference scores a span
+    elsewhere in the prompt (e.g. a one-word statement that also occurs in the system
+    text); callers then take the text-compat path to stay result-identical."""
+    api_user = user_prompt + MARKER if user_prompt.endswith(("\n", " ")) else user_prompt
+    ids, (start, _) = tok.render_chat(system_prompt or None, api_user)
+    text = "".join(tok.tokens(ids))
+    return text.find(user_prompt) == len("".join(tok.tokens(ids[:start])))
+
+
+def text_compat_mean(model, system_prompt, user_prompt):
+    """(mean log-prob, mean prob, count) of the reference's user-span log-probs."""
+    _, lps = get_prompt_logprobs(model, system_prompt, user_prompt)
+    vals = [v for v in lps if v is not None]
+    if not vals:
+        return float("nan"), float("nan"), 0
+    import math as _m
+    return sum(vals) / len(vals), sum(_m.exp(v) for v in vals) / len(vals), len(vals)
+
+
+def get_token_ids(model, text) -> Dict[str, int]:
+    """{token string: id} of the chat-rendered single-message prompt (src/utils.py:466-525)."""
+    try:
+        _, tok = runtime.get_engine(model)
+        ids, _ = tok.render_chat(None, text)
+        return {tok.token_str(i): i for i in ids}
+    except Exception as e:
+        logger.error("get_token_ids failed: %s", e)
+        return {}
+
+
+def generate_text(model, user_prompt, system_prompt=None, max_tokens=4096, temperature=1,
+                  terminators=(), seed=None, bias_against_tokens=None, bias_value=-1000000,
+                  use_chat_completions=True, repetition_penalty=1.0) -> str:
+    """Sample a completion locally (src/utils.py:77-198 contract; '[ERROR: ...]' on failure).
+
+    Chat mode renders the chat template with the generation prompt; completions mode
+    uses the raw ``system + "\\n\\n" + user`` prompt.  Token t is drawn with seed
+    draw_seed(seed, t); stop tokens end the text and are not included."""
+    try:
+        engine, tok = runtime.get_engine(model)
+        if use_chat_completions:
+            ids, _ = tok.render_chat(system_prompt or None, user_prompt)
+        else:
+            full = f"{system_prompt}\n\n{user_prompt}" if system_prompt else f"{user_prompt}"
+            ids = tok.render_raw(full)
+        bias = runtime.bias_token_ids(tok, bias_against_tokens)
+        out = runtime.generate(engine, tok, ids, [seed], max_tokens, float(temperature),
+                               bias_ids=bias, bias_value=float(bias_value))[0]
+        text = tok.decode(out)
+        for term in terminators or ():
+            cut = text.find(term)
+            if cut != -1:
+                text = text[:cut]
+        return text
+    except Exception as e:
+        logger.error("generate_text failed: %s", e)
+        return f"[ERROR: {type(e).__name__}]"

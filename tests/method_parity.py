@@ -1,0 +1,113 @@
+"""Shared method-level parity harness (used by the GPU tests and by the CPU tests that
+emulate the C-ABI ops with the oracle to check the methods' HOST logic).
+
+Replays every run recorded in tests/golden/method_traces.json (produced by the
+reference's own generators, see make_method_traces.py) through the product's
+generators on the same seeded fixture model, and compares:
+  * final statements (exact), BoN candidates (exact), BoN agent rewards and welfare
+    (1e-3 abs, north_star tolerance);
+  * StatementEvaluator log-prob metrics (1e-3 abs on log-probs, 1e-3 rel on welfare);
+  * get_prompt_logprobs tokens (exact) and log-probs (1e-3 abs).
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import math
+import os
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+TOL = 1e-3
+
+
+def load_traces():
+    with open(os.path.join(HERE, "golden", "method_traces.json")) as f:
+        return json.load(f)
+
+
+def register_fixture_engine(traces, device):
+    Mm = importlib.import_module(PKG + ".model")
+    T = importlib.import_module(PKG + ".tokenizer")
+    E = importlib.import_module(PKG + ".engine")
+    R = importlib.import_module(PKG + ".runtime")
+    tok = T.CharTokenizer("llama3")
+    cfg = Mm.preset(traces["preset"], vocab=traces["vocab"])
+    cpu = Mm.Model(cfg, "cpu", torch.float32, seed=traces["weight_seed"])
+    w = {k: v.to(device) for k, v in cpu.w.items()}
+    model = Mm.Model(cfg, device, torch.float32, weights=w)
+    eng = E.ScoringEngine(model)
+    R.register_engine(traces["model_id"], eng, tok)
+    return eng, tok
+
+
+def run_methods(traces):
+    methods = importlib.import_module(PKG + ".methods")
+    results = []
+    for run in traces["runs"]:
+        gen = methods.get_method_generator(run["method"], dict(run["config"]), traces["model_id"])
+        stmt = gen.generate_statement(traces["issue"], dict(traces["agent_opinions"]))
+        results.append((run, gen, stmt))
+    return results
+
+
+def check_methods(traces):
+    failures = []
+    for run, gen, stmt in run_methods(traces):
+        tag = f"{run['method']} {run['config']}"
+        if run["method"] == "best_of_n":
+            if gen.last_candidates != run["candidates"]:
+                failures.append(f"{tag}: candidates differ {gen.last_candidates} vs {run['candidates']}")
+                continue
+            for aid, ref in run["agent_rewards"].items():
+                got = gen.last_agent_rewards[aid]
+                d = max(abs(a - b) for a, b in zip(got, ref))
+                if d > TOL:
+                    failures.append(f"{tag}: agent {aid} rewards differ by {d}")
+            d = max(abs(a - b) for a, b in zip(gen.last_welfare, run["welfare"]))
+            if d > TOL:
+                failures.append(f"{tag}: welfare differs by {d}")
+        if stmt != run["statement"]:
+            failures.append(f"{tag}: statement {stmt!r} != reference {run['statement']!r}")
+    return failures
+
+
+def check_evaluations(traces):
+    ev_mod = importlib.import_module(PKG + ".evaluation")
+    ev = ev_mod.StatementEvaluator(traces["model_id"], include_comparative_ranking=False,
+                                   verbose=False)
+    failures = []
+    for rec in traces["evaluations"]:
+        got = ev.evaluate_statement(rec["statement"], traces["issue"], dict(traces["agent_opinions"]))
+        for k, ref in rec["result"].items():
+            g = got.get(k, "MISSING")
+            if g == "MISSING":
+                failures.append(f"eval {rec['statement'][:20]!r}: key {k} missing")
+                continue
+            if ref is None or (isinstance(ref, float) and math.isnan(ref)):
+                if not (g is None or (isinstance(g, float) and math.isnan(g))):
+                    failures.append(f"eval key {k}: {g} vs reference {ref}")
+                continue
+            tol = TOL if (k.startswith("avg_logprob") or k.startswith("utility_avg")) else \
+                TOL * max(1.0, abs(ref))
+            if g is None or abs(float(g) - ref) > tol:
+                failures.append(f"eval key {k}: {g} vs reference {ref}")
+    return failures
+
+
+def check_prompt_logprobs(traces):
+    utils = importlib.import_module(PKG + ".utils")
+    failures = []
+    for rec in traces["prompt_logprobs"]:
+        toks, lps = utils.get_prompt_logprobs(traces["model_id"], rec["system"], rec["user"])
+        if toks != rec["tokens"]:
+            failures.append(f"prompt_logprobs {rec['user']!r}: tokens {toks} vs {rec['tokens']}")
+            continue
+        for a, b in zip(lps, rec["logprobs"]):
+            if (a is None) != (b is None) or (a is not None and abs(a - b) > TOL):
+                failures.append(f"prompt_logprobs {rec['user']!r}: {a} vs {b}")
+                break
+    return failures
