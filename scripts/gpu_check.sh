@@ -15,10 +15,17 @@ run_prof() {
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
      python3 "$R/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/prof.log" 2>&1)
 }
+run_pmc() {
+  (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -f csv -- \
+     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/pmc_fetch.log" 2>&1) && \
+  (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -f csv -- \
+     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/pmc_write.log" 2>&1)
+}
 case "$STEP" in
   tests) run_tests ;;
   bench) run_bench ;;
   prof) run_prof ;;
+  pmc) run_pmc ;;
   all) run_tests; rc=$?; echo "tests rc=$rc" ; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-       run_smoke && run_bench && run_prof ;;
+       run_smoke && run_bench && run_prof && run_pmc ;;
 esac
