@@ -135,12 +135,14 @@ def main():
     world, rank, local = init_dist(args.gpus)
     dev = torch.device("cuda", torch.cuda.current_device())
     ops = importlib.import_module(PKG_DIR + ".ops")
+    par = importlib.import_module(PKG_DIR + ".parallel")
 
     A, N, T, V, wkind, desc = CONFIGS[args.config]
     rows = A * N * T
     logits, tgt, offsets = make_inputs(A, N, T, V, 1234 + rank, dev)
     ws = ops.Workspace()
     stream = torch.cuda.current_stream()
+    shard = par.AgentShard(A * world, rank, world)   # A agents per GPU, round-robin
 
     def step(ev=None):
         if ev is not None:
@@ -152,12 +154,8 @@ def main():
         U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N)
         if wkind == "sumlog":
             U = torch.exp(U)  # Nash over geometric-mean token probability
-        W = ops.welfare(U, wkind, eps=1e-30)
-        if world > 1:
-            if wkind == "min":
-                torch.distributed.all_reduce(W, op=torch.distributed.ReduceOp.MIN)
-            else:
-                torch.distributed.all_reduce(W, op=torch.distributed.ReduceOp.SUM)
+        # agents sharded over ranks: MIN all-reduce (egalitarian) or gather + ordered fold
+        W = par.combine_welfare(U, wkind, shard, eps=1e-30)
         idx, _ = ops.topk(W, 1)
         return idx
 

@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "consensus_scoring.h"
@@ -175,98 +176,144 @@ __device__ __forceinline__ void gather_targets(const char* row, int64_t vocab, f
 }
 
 // ---------------------------------------------------------------------------
-// streaming kernel: one workgroup per (row, split)
+// streaming kernel: one workgroup per (row, split) work item
 // ---------------------------------------------------------------------------
-template <int DT, bool CAP>
-__global__ __launch_bounds__(kBlock) void lsg_stream_kernel(
-    const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nsplit,
-    int64_t split_len, const int32_t* __restrict__ tgt, int32_t k, float cap, float inv_cap,
-    float* __restrict__ out_tok, float* __restrict__ out_lse, float2* __restrict__ part) {
+// BLOCK   threads per workgroup (multiple of 64)
+// UNROLL  16-byte vectors each lane has in flight per iteration
+// NT      non-temporal loads (each logits byte is read exactly once)
+// PIPE    register double-buffering: the next iteration's loads are issued before
+//         the current vectors are reduced
+// Work items (row, split) are walked grid-stride so a capped grid also works.
+template <int DT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p, bool nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+
+template <int DT, bool CAP, int BLOCK, int UNROLL, bool NT, bool PIPE>
+__global__ __launch_bounds__(BLOCK) void lsg_stream_kernel(
+    const char* __restrict__ logits, int64_t n_items, int64_t vocab, int64_t ld_bytes,
+    int32_t nsplit, int64_t split_len, const int32_t* __restrict__ tgt, int32_t k, float cap,
+    float inv_cap, float* __restrict__ out_tok, float* __restrict__ out_lse,
+    float2* __restrict__ part) {
   constexpr int ESZ = Elt<DT>::kSize;
   constexpr int EPV = Elt<DT>::kPerVec;
-  __shared__ float sm_m[kBlock / 64];
-  __shared__ float sm_s[kBlock / 64];
+  constexpr int NW = BLOCK / 64;
+  __shared__ float sm_m[NW];
+  __shared__ float sm_s[NW];
   __shared__ float sm_lse;
-
   const int tid = threadIdx.x;
-  const int64_t bid = blockIdx.x;
-  const int64_t row = bid / nsplit;
-  const int32_t split = static_cast<int32_t>(bid - row * nsplit);
-  const char* rp = logits + row * ld_bytes;
-  const int64_t v0 = static_cast<int64_t>(split) * split_len;
-  const int64_t v1 = min(vocab, v0 + split_len);
-  const int64_t n = v1 - v0;
 
-  float m = -INFINITY, s = 0.0f;
+  for (int64_t bid = blockIdx.x; bid < n_items; bid += gridDim.x) {
+    const int64_t row = bid / nsplit;
+    const int32_t split = static_cast<int32_t>(bid - row * nsplit);
+    const char* rp = logits + row * ld_bytes;
+    const int64_t v0 = static_cast<int64_t>(split) * split_len;
+    const int64_t v1 = min(vocab, v0 + split_len);
+    const int64_t n = v1 - v0;
 
-  // scalar head up to the first 16-byte boundary, scalar tail after the last full vector
-  const uintptr_t a0 = reinterpret_cast<uintptr_t>(rp + v0 * ESZ);
-  int64_t head = static_cast<int64_t>(((16u - (a0 & 15u)) & 15u) / ESZ);
-  if (head > n) head = n;
-  const int64_t nvec = (n - head) / EPV;
-  const int64_t tail0 = head + nvec * EPV;
-  {
-    float x = -INFINITY;
-    if (tid < head) {
-      x = load_one<DT>(rp, v0 + tid);
-      if (CAP) x = softcap_fn(x, cap, inv_cap);
-    } else if (tid >= 64 && tid - 64 < n - tail0) {
-      x = load_one<DT>(rp, v0 + tail0 + (tid - 64));
-      if (CAP) x = softcap_fn(x, cap, inv_cap);
+    float m = -INFINITY, s = 0.0f;
+
+    // scalar head up to the first 16-byte boundary, scalar tail after the last full vector
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(rp + v0 * ESZ);
+    int64_t head = static_cast<int64_t>(((16u - (a0 & 15u)) & 15u) / ESZ);
+    if (head > n) head = n;
+    const int64_t nvec = (n - head) / EPV;
+    const int64_t tail0 = head + nvec * EPV;
+    {
+      float x = -INFINITY;
+      if (tid < head) {
+        x = load_one<DT>(rp, v0 + tid);
+        if (CAP) x = softcap_fn(x, cap, inv_cap);
+      } else if (tid >= 64 && tid - 64 < n - tail0) {
+        x = load_one<DT>(rp, v0 + tail0 + (tid - 64));
+        if (CAP) x = softcap_fn(x, cap, inv_cap);
+      }
+      if (x != -INFINITY) lse_accum<1>(m, s, &x);
     }
-    if (x != -INFINITY) lse_accum<1>(m, s, &x);
-  }
 
-  const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
-  int64_t i = tid;
-  for (; i + (kUnroll - 1) * kBlock < nvec; i += kUnroll * kBlock) {
-    u32x4 q[kUnroll];
+    const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
+    int64_t i = tid;
+    constexpr int STEP = UNROLL * BLOCK;
+    if (PIPE) {
+      u32x4 q[UNROLL];
+      bool have = i + (UNROLL - 1) * BLOCK < nvec;
+      if (have) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * kBlock);
-    float v[kUnroll * EPV];
+        for (int u = 0; u < UNROLL; ++u) q[u] = ld16<DT>(vp + i + u * BLOCK, NT);
+      }
+      while (have) {
+        const bool next = i + STEP + (UNROLL - 1) * BLOCK < nvec;
+        u32x4 qn[UNROLL];
+        if (next) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) unpack_vec<DT>(q[u], v + u * EPV);
-    if (CAP) {
+          for (int u = 0; u < UNROLL; ++u) qn[u] = ld16<DT>(vp + i + STEP + u * BLOCK, NT);
+        }
+        float v[UNROLL * EPV];
 #pragma unroll
-      for (int e = 0; e < kUnroll * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-    }
-    lse_accum<kUnroll * EPV>(m, s, v);
-  }
-  for (; i < nvec; i += kBlock) {
-    const u32x4 q = __builtin_nontemporal_load(vp + i);
-    float v[EPV];
-    unpack_vec<DT>(q, v);
-    if (CAP) {
+        for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
+        if (CAP) {
 #pragma unroll
-      for (int e = 0; e < EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-    }
-    lse_accum<EPV>(m, s, v);
-  }
-
-  wave_lse_reduce(m, s);
-  const int wave = tid >> 6;
-  if ((tid & 63) == 0) {
-    sm_m[wave] = m;
-    sm_s[wave] = s;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float mm = sm_m[0], ss = sm_s[0];
+          for (int e = 0; e < UNROLL * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+        }
+        lse_accum<UNROLL * EPV>(m, s, v);
+        i += STEP;
+        have = next;
+        if (next) {
 #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) lse_merge(mm, ss, sm_m[w], sm_s[w]);
-    if (nsplit > 1) {
-      part[bid] = make_float2(mm, ss);
+          for (int u = 0; u < UNROLL; ++u) q[u] = qn[u];
+        }
+      }
     } else {
-      const float lse = mm + logf(ss);
-      sm_lse = lse;
-      if (out_lse) out_lse[row] = lse;
+      for (; i + (UNROLL - 1) * BLOCK < nvec; i += STEP) {
+        u32x4 q[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) q[u] = ld16<DT>(vp + i + u * BLOCK, NT);
+        float v[UNROLL * EPV];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
+        if (CAP) {
+#pragma unroll
+          for (int e = 0; e < UNROLL * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+        }
+        lse_accum<UNROLL * EPV>(m, s, v);
+      }
     }
+    for (; i < nvec; i += BLOCK) {
+      const u32x4 q = ld16<DT>(vp + i, NT);
+      float v[EPV];
+      unpack_vec<DT>(q, v);
+      if (CAP) {
+#pragma unroll
+        for (int e = 0; e < EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+      }
+      lse_accum<EPV>(m, s, v);
+    }
+
+    wave_lse_reduce(m, s);
+    const int wave = tid >> 6;
+    if ((tid & 63) == 0) {
+      sm_m[wave] = m;
+      sm_s[wave] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float mm = sm_m[0], ss = sm_s[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) lse_merge(mm, ss, sm_m[w], sm_s[w]);
+      if (nsplit > 1) {
+        part[bid] = make_float2(mm, ss);
+      } else {
+        const float lse = mm + logf(ss);
+        sm_lse = lse;
+        if (out_lse) out_lse[row] = lse;
+      }
+    }
+    __syncthreads();
+    if (nsplit == 1 && k > 0)
+      gather_targets(rp, vocab, sm_lse, tgt + row * k, k, out_tok + row * k, CAP, cap, inv_cap,
+                     DT, tid, BLOCK);
+    __syncthreads();  // sm_* are reused by the next work item
   }
-  if (nsplit > 1) return;
-  __syncthreads();
-  if (k > 0)
-    gather_targets(rp, vocab, sm_lse, tgt + row * k, k, out_tok + row * k, CAP, cap, inv_cap, DT,
-                   tid, kBlock);
 }
 
 // split-V finish: merge the (m, s) partials of one row in split order, then gather.
@@ -439,15 +486,53 @@ SplitPlan plan_split(int64_t rows, int64_t vocab, int dtype) {
   return p;
 }
 
+// Streaming-kernel configurations compiled into the library.  Variant 0 is the
+// product default; CS_LSG_VARIANT=<n> (host environment, read per launch) selects
+// another for A/B timing on live data (tools/lsg_variants.py).  Every variant
+// computes the same values (reduction order differs only inside a row's partials).
+template <int DT, bool CAP, int BLOCK, int UNROLL>
+void launch_stream(const void* logits, int64_t items, int64_t vocab, int64_t ld_bytes,
+                   const SplitPlan& plan, const int32_t* tgt, int32_t k, float cap, float inv_cap,
+                   float* out_tok, float* out_lse, float2* part, hipStream_t st) {
+  hipLaunchKernelGGL((lsg_stream_kernel<DT, CAP, BLOCK, UNROLL, true, false>),
+                     dim3(static_cast<uint32_t>(items)), dim3(BLOCK), 0, st,
+                     static_cast<const char*>(logits), items, vocab, ld_bytes, plan.nsplit,
+                     plan.split_len, tgt, k, cap, inv_cap, out_tok, out_lse, part);
+}
+
+int lsg_variant() {
+  const char* e = getenv("CS_LSG_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
 template <int DT, bool CAP>
 void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_bytes,
                 const SplitPlan& plan, const int32_t* tgt, int32_t k, float cap, float* out_tok,
                 float* out_lse, float2* part, hipStream_t st) {
   const float inv_cap = CAP ? 1.0f / cap : 0.0f;
-  const int64_t grid = rows * plan.nsplit;
-  hipLaunchKernelGGL((lsg_stream_kernel<DT, CAP>), dim3(static_cast<uint32_t>(grid)), dim3(kBlock),
-                     0, st, static_cast<const char*>(logits), vocab, ld_bytes, plan.nsplit,
-                     plan.split_len, tgt, k, cap, inv_cap, out_tok, out_lse, part);
+  const int64_t items = rows * plan.nsplit;
+  switch (lsg_variant()) {
+    case 1:
+      launch_stream<DT, CAP, 512, 4>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
+                                     out_tok, out_lse, part, st);
+      break;
+    case 2:
+      launch_stream<DT, CAP, 1024, 1>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
+                                      out_tok, out_lse, part, st);
+      break;
+    case 3:
+      launch_stream<DT, CAP, 1024, 2>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
+                                      out_tok, out_lse, part, st);
+      break;
+    case 4:
+      launch_stream<DT, CAP, 256, 8>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
+                                     out_tok, out_lse, part, st);
+      break;
+    default:
+      launch_stream<DT, CAP, kBlock, kUnroll>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
+                                              inv_cap, out_tok, out_lse, part, st);
+      break;
+  }
   if (plan.nsplit > 1) {
     hipLaunchKernelGGL((lsg_merge_kernel<DT, CAP>), dim3(static_cast<uint32_t>(rows)),
                        dim3(kMergeBlock), 0, st, static_cast<const char*>(logits), vocab, ld_bytes,
