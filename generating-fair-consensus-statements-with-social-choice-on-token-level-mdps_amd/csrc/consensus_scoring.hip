@@ -486,10 +486,13 @@ SplitPlan plan_split(int64_t rows, int64_t vocab, int dtype) {
   return p;
 }
 
-// Streaming-kernel configurations compiled into the library.  Variant 0 is the
-// product default; CS_LSG_VARIANT=<n> (host environment, read per launch) selects
-// another for A/B timing on live data (tools/lsg_variants.py).  Every variant
-// computes the same values (reduction order differs only inside a row's partials).
+// Streaming-kernel configurations compiled into the library.  Variant 0 (default) is
+// shape-aware, from the in-process A/B on the bench's data (profiles/r01_lsg_variants.jsonl):
+//   single pass (rows >= 2048): 1024 threads x 2 vectors in flight  (C2: 7.25 TB/s, 90.6 %)
+//   split-V (fewer rows):        256 threads x 8 vectors in flight
+// CS_LSG_VARIANT=<n> (host environment, read per launch) forces one configuration for
+// A/B timing (tools/lsg_variants.py).  All variants compute the same values up to the
+// order of the fp32 partial merges inside a row (|diff| ~ 1e-6).
 template <int DT, bool CAP, int BLOCK, int UNROLL>
 void launch_stream(const void* logits, int64_t items, int64_t vocab, int64_t ld_bytes,
                    const SplitPlan& plan, const int32_t* tgt, int32_t k, float cap, float inv_cap,
@@ -512,7 +515,7 @@ void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_byte
   const float inv_cap = CAP ? 1.0f / cap : 0.0f;
   const int64_t items = rows * plan.nsplit;
   switch (lsg_variant()) {
-    case 1:
+    case 1:  // 512 x 4
       launch_stream<DT, CAP, 512, 4>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
                                      out_tok, out_lse, part, st);
       break;
@@ -528,9 +531,17 @@ void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_byte
       launch_stream<DT, CAP, 256, 8>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
                                      out_tok, out_lse, part, st);
       break;
-    default:
+    case 5:
       launch_stream<DT, CAP, kBlock, kUnroll>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
                                               inv_cap, out_tok, out_lse, part, st);
+      break;
+    default:
+      if (plan.nsplit == 1)
+        launch_stream<DT, CAP, 1024, 2>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
+                                        inv_cap, out_tok, out_lse, part, st);
+      else
+        launch_stream<DT, CAP, 256, 8>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
+                                       inv_cap, out_tok, out_lse, part, st);
       break;
   }
   if (plan.nsplit > 1) {
