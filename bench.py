@@ -52,22 +52,33 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time for the oracle baseline sample (0 disables)")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
+                         "the multi-rank path with several ranks on one GPU)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the full scoring pass INCLUDING the transformer forward "
+                         "(random-init Llama-3.1-8B bf16, per-agent prefix K/V) and report it "
+                         "under 'end_to_end'")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per launch (optional)")
     return ap.parse_args()
 
 
-def init_dist(n_gpus):
+def init_dist(n_gpus, backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":   # rehearsal: every rank on the one visible GPU
+            torch.cuda.set_device(0)
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -118,6 +129,48 @@ def cpu_baseline(A, N, T, V, welfare_kind, seconds):
                       f"in {el:.1f} s"}
 
 
+def end_to_end(A, N, T, V, wkind, dev, steps=2, prefix_len=200, seed=0):
+    """Full C2 scoring pass incl. the transformer forward: Llama-3.1-8B (random init, bf16)
+    prefills A agent prefixes of `prefix_len` tokens once, then scores N candidates x T
+    tokens under every agent (prefix K/V reused by all candidates), LM head, HIP kernels,
+    welfare, selection."""
+    M = importlib.import_module(PKG_DIR + ".model")
+    E = importlib.import_module(PKG_DIR + ".engine")
+    ops = importlib.import_module(PKG_DIR + ".ops")
+    cfg = M.preset("llama-3.1-8b")
+    t0 = time.perf_counter()
+    model = M.Model(cfg, dev, torch.bfloat16, seed=seed)
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    eng = E.ScoringEngine(model, max_rows_per_chunk=16384)
+    g = torch.Generator().manual_seed(11)
+    prefixes = [torch.randint(300, V, (prefix_len,), generator=g).tolist() for _ in range(A)]
+    cands = [torch.randint(300, V, (T,), generator=g).tolist() for _ in range(N)]
+    owner = [a for a in range(A) for _ in range(N)]
+    conts = [cands[c] for _ in range(A) for c in range(N)]
+    offs = eng.offsets(conts, dev)
+
+    def one_pass():
+        cache = eng.prefill(prefixes)
+        lp = eng.score(cache, owner, conts)
+        seg = ops.segment_reduce(lp, offs)
+        U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N).contiguous()
+        W = ops.welfare(U, wkind)
+        return ops.topk(W, 1)[0]
+
+    one_pass()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"model": "llama-3.1-8b (random init, bf16)", "prefix_tokens": prefix_len,
+            "scored_tokens": A * N * T, "s_per_pass": dt, "scorings_per_s": A * N / dt,
+            "tokens_per_s": A * N * T / dt, "model_init_s": init_s, "passes": steps,
+            "note": "forward = PyTorch/hipBLASLt (plumbing); logits -> HIP C-ABI kernels"}
+
+
 def read_traffic(path, config, rows, V):
     try:
         with open(path) as f:
@@ -132,7 +185,7 @@ def read_traffic(path, config, rows, V):
 
 def main():
     args = parse()
-    world, rank, local = init_dist(args.gpus)
+    world, rank, local = init_dist(args.gpus, args.backend)
     dev = torch.device("cuda", torch.cuda.current_device())
     ops = importlib.import_module(PKG_DIR + ".ops")
     par = importlib.import_module(PKG_DIR + ".parallel")
@@ -188,6 +241,11 @@ def main():
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(A, N, T, V, wkind, args.cpu_seconds)
+        e2e = None
+        if args.e2e and world == 1:
+            del logits
+            torch.cuda.empty_cache()
+            e2e = end_to_end(A, N, T, V, wkind, dev)
         line = {
             "metric": "agent×candidate scorings/sec + decode steps/sec at 1/2/4/8 MI355X; % HBM roofline",
             "value": scorings * args.steps / elapsed,
@@ -212,6 +270,8 @@ def main():
                          "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }
+        if e2e is not None:
+            line["end_to_end"] = e2e
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -106,10 +106,9 @@ class StatementEvaluator:
                 r[f"utility_avg_logprob_{aid}"] = r[f"avg_logprob_{aid}"]
                 r[f"cosine_similarity_{aid}"] = None
                 r[f"utility_cosine_similarity_{aid}"] = None
-            for key in ("egalitarian_welfare_cosine", "utilitarian_welfare_cosine",
-                        "log_nash_welfare_cosine", "utility_egalitarian_welfare_cosine",
-                        "utility_utilitarian_welfare_cosine", "utility_log_nash_welfare_cosine"):
-                r[key] = np.nan
+            for kind in ("egalitarian", "utilitarian", "log_nash"):
+                r[f"{kind}_welfare_cosine"] = np.nan
+                r[f"utility_{kind}_welfare_cosine"] = np.nan
             for a, aid in enumerate(agents):
                 if not math.isnan(lp_h[a, s]) and math.isfinite(lp_h[a, s]):
                     r[f"perplexity_{aid}"] = float(ppl_h[a, s])
@@ -129,11 +128,152 @@ class StatementEvaluator:
         return out
 
     # --- reference entry points -----------------------------------------------------
+    def evaluate_statements(self, statements: Dict[str, Any], issue: str,
+                            agent_opinions: Dict[str, str]):
+        """DataFrame of evaluation rows (src/evaluation.py:895-1019 contract), all statements
+        scored in one batched pass.  Row layout: method, issue, statement,
+        method_with_params, [param_*], [seed], [original_row_index], evaluation_time_s, then
+        the evaluate_statement keys without the embedding."""
+        import pandas as pd
+
+        keys = list(statements)
+        texts, seeds, idxs = [], [], []
+        for k in keys:
+            d = statements[k]
+            if isinstance(d, dict):
+                texts.append(d.get("statement", ""))
+                seeds.append(d.get("seed"))
+                idxs.append(d.get("row_index"))
+            else:
+                texts.append(d)
+                seeds.append(None)
+                idxs.append(None)
+        results = self.evaluate_statements_batched(texts, issue, agent_opinions) if keys else []
+        rows = []
+        for k, text, seed, ridx, res in zip(keys, texts, seeds, idxs, results):
+            base, params, seed_from_key = _parse_method_key(k)
+            row = {"method": base, "issue": issue, "statement": text, "method_with_params": k}
+            row.update(params)
+            final_seed = seed if seed is not None else seed_from_key
+            if final_seed is not None:
+                row["seed"] = final_seed
+            if ridx is not None:
+                row["original_row_index"] = ridx
+            row["evaluation_time_s"] = res.pop("evaluation_time_s", 0.0)
+            for kk, v in res.items():
+                if kk != "statement_embedding":
+                    row[kk] = v
+            rows.append(row)
+        return pd.DataFrame(rows)
+
+    def evaluate_results_file(self, results_path, config_path=None, output_dir=None,
+                              is_seed_specific: bool = False):
+        """Evaluate every statement of a results.csv and write evaluation_results.csv +
+        evaluation_config.yaml in the reference's layout (src/evaluation.py:1072-1428),
+        which improved_aggregation.py consumes unchanged.  Returns the merged rows."""
+        from pathlib import Path
+
+        import pandas as pd
+        import yaml
+
+        results_path = Path(results_path)
+        results_dir = results_path.parent
+        config_path = Path(config_path) if config_path else results_dir / "config.yaml"
+        if not results_path.exists():
+            raise FileNotFoundError(f"Results file not found: {results_path}")
+        df = pd.read_csv(results_path)
+        statements = {}
+        for _, row in df.iterrows():
+            method = row.get("method", "Unknown method")
+            stmt = row.get("statement", "No statement generated")
+            if stmt == "ERROR" or pd.isna(stmt):
+                continue
+            params = {c: row[c] for c in row.index if c.startswith("param_") and pd.notna(row[c])}
+            seed = row["seed"] if "seed" in row and pd.notna(row["seed"]) else None
+            key = utils.create_method_identifier(method, params, include_seed=seed is not None,
+                                                 seed_value=seed)
+            statements[key] = {"statement": stmt, "seed": seed, "row_index": row.name}
+        cfg = yaml.safe_load(open(config_path)) if config_path.exists() else None
+        issue = (cfg or {}).get("scenario", {}).get("issue")
+        opinions = (cfg or {}).get("scenario", {}).get("agent_opinions", {})
+        if not issue or not opinions:
+            raise ValueError("Could not extract issue and agent opinions from config. "
+                             "Please provide a valid config file.")
+        if output_dir is None:
+            name = self.evaluation_model.replace("/", "_")
+            output_dir = results_dir / f"posthoc_eval_{name}_judge_no_judge"
+        output_dir = Path(output_dir)
+        out_dir = output_dir if is_seed_specific else output_dir / "seed_0"
+        out_dir.mkdir(parents=True, exist_ok=True)
+        ev = self.evaluate_statements(statements, issue, opinions)
+        ev.to_csv(out_dir / "evaluation_results.csv", index=False)
+        with open(out_dir / "evaluation_config.yaml", "w") as f:
+            yaml.dump({"original_config": cfg, "evaluation": {
+                "evaluation_model": self.evaluation_model, "embedding_model": self.embedding_model,
+                "include_llm_judge": False, "llm_judge_model": None,
+                "original_results_path": str(results_path), "statements_evaluated": len(statements),
+                "rows_processed": len(ev), "total_rows": len(df)}}, f, default_flow_style=False)
+        combined = df.copy()
+        by_idx = {r["original_row_index"]: r for _, r in ev.iterrows()} \
+            if "original_row_index" in ev.columns else {}
+        for i in combined.index:
+            if i in by_idx:
+                combined.at[i, "evaluation_status"] = "completed"
+                for col, v in by_idx[i].items():
+                    if col not in ("method", "statement", "issue", "original_row_index") \
+                            and col not in df.columns:
+                        combined.at[i, col] = v
+            else:
+                combined.at[i, "evaluation_status"] = "skipped"
+        return combined
+
     def evaluate_statement(self, statement: str, issue: str,
                            agent_opinions: Dict[str, str]) -> Dict[str, Any]:
         r = self.evaluate_statements_batched([statement], issue, agent_opinions)[0]
         r.pop("evaluation_time_s", None)
         return r
+
+
+def _parse_method_key(key: str):
+    """'base (k=v, ...) [seed=s]' -> (base, {param_k: v}, seed) with the reference's parsing
+    (src/evaluation.py:938-976): params only when the key ends with ')'."""
+    base, params, seed = key, {}, None
+    if " (" in key:
+        parts = key.split(" (", 1)
+        base = parts[0]
+        if parts[1].endswith(")"):
+            for item in parts[1].rstrip(")").split(", "):
+                if "=" in item:
+                    name, val = item.split("=", 1)
+                    try:
+                        val = float(val)
+                        if val.is_integer():
+                            val = int(val)
+                    except ValueError:
+                        pass
+                    params[f"param_{name}"] = val
+    if "[seed=" in key and "]" in key:
+        try:
+            seed = int(key.split("[seed=", 1)[1].split("]", 1)[0])
+        except (ValueError, IndexError):
+            pass
+    return base, params, seed
+
+
+def write_results_csv(rows, out_path):
+    """results.csv with the reference's column order (src/experiment.py:339-373):
+    method, statement, error_message, seed, utility_*, param_*, issue, config_file, rest."""
+    import pandas as pd
+
+    df = pd.DataFrame(rows)
+    core = ["method", "statement", "error_message", "seed"]
+    util = sorted(c for c in df.columns if c.startswith("utility_"))
+    par = sorted(c for c in df.columns if c.startswith("param_"))
+    other = sorted(c for c in df.columns if c not in core + util + par + ["issue", "config_file"])
+    order = [c for c in core + util + par + ["issue", "config_file"] + other if c in df.columns]
+    df = df[order]
+    df.to_csv(out_path, index=False)
+    return df
 
 
 def evaluate_statement(statement: str, issue: str, agent_opinions: dict,

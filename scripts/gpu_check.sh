@@ -13,7 +13,7 @@ run_smoke() { timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smo
 run_bench() { timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; }
 run_prof() {
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
-     python3 "$R/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/prof.log" 2>&1)
+     python3 "$R/bench.py" --cpu-seconds 0 > "$OUT/prof.log" 2>&1)
 }
 run_pmc() {
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -f csv -- \

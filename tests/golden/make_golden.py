@@ -114,6 +114,22 @@ def make_eval(ref: str) -> None:
     print(f"wrote eval_welfare_published.csv ({len(out)} rows from {len(files)} files)")
 
 
+def make_results_fixture(ref: str) -> None:
+    """A published run directory (results.csv + config.yaml) and the header of its published
+    evaluation_results.csv: inputs + expected schema of the file-level evaluation path."""
+    import shutil
+
+    src = os.path.join(ref, "results", "appendix", "aamas_gemma_scenario1_beam_search_20250511_222741")
+    dst = os.path.join(HERE, "results_fixture")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copyfile(os.path.join(src, "results.csv"), os.path.join(dst, "results.csv"))
+    shutil.copyfile(os.path.join(src, "config.yaml"), os.path.join(dst, "config.yaml"))
+    pub = os.path.join(src, "evaluation", "google_gemma-2-9b-it", "seed_0", "evaluation_results.csv")
+    with open(pub) as f, open(os.path.join(dst, "published_evaluation_header.csv"), "w") as g:
+        g.write(f.readline())
+    print("wrote results_fixture/")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -121,6 +137,7 @@ def main() -> None:
     core = import_reference(args.reference)
     make_core(core)
     make_eval(args.reference)
+    make_results_fixture(args.reference)
 
 
 if __name__ == "__main__":
