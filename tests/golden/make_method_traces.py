@@ -9,7 +9,7 @@ tests/golden/method_traces.json.  Nothing from the reference is copied: only the
 data its code produced.  The GPU tests replay the same configs through the
 product and compare.
 
-Usage:  python tests/golden/make_method_traces.py [--reference /root/reference]
+Usage:  python tests/golden/make_method_traces.py [--reference /root/reference] [--family llama3|gemma2]
 """
 from __future__ import annotations
 
@@ -31,6 +31,8 @@ PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-md
 
 MODEL_ID = "tiny-llama-fixture"
 WEIGHT_SEED = 3
+FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
+            "gemma2": ("tiny-gemma-fixture", "method_traces_gemma.json")}
 
 
 def fixture_model(family: str = "llama3"):
@@ -62,11 +64,14 @@ def install(reference: str, backend) -> None:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--family", default="llama3", choices=sorted(FAMILIES))
     args = ap.parse_args()
     import yaml
     import fake_together
 
-    cfg, model, tok = fixture_model()
+    global MODEL_ID
+    MODEL_ID, out_name = FAMILIES[args.family]
+    cfg, model, tok = fixture_model(args.family)
     backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok)
     install(args.reference, backend)
     scen = yaml.safe_load(open(os.path.join(args.reference, "configs", "appendix", "llama",
@@ -91,6 +96,7 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
+           "family": args.family,
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
     runs = [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,
@@ -153,9 +159,9 @@ def main() -> None:
         toks, lps = rutils.get_prompt_logprobs(MODEL_ID, system, user)
         out["prompt_logprobs"].append({"system": system, "user": user, "tokens": toks,
                                        "logprobs": lps})
-    with open(os.path.join(HERE, "method_traces.json"), "w") as f:
+    with open(os.path.join(HERE, out_name), "w") as f:
         json.dump(out, f, indent=1)
-    print("wrote method_traces.json")
+    print("wrote", out_name)
 
 
 if __name__ == "__main__":

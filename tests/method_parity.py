@@ -24,8 +24,11 @@ PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-md
 TOL = 1e-3
 
 
-def load_traces():
-    with open(os.path.join(HERE, "golden", "method_traces.json")) as f:
+TRACE_FILES = ["method_traces.json", "method_traces_gemma.json"]
+
+
+def load_traces(name: str = "method_traces.json"):
+    with open(os.path.join(HERE, "golden", name)) as f:
         return json.load(f)
 
 
@@ -34,7 +37,7 @@ def register_fixture_engine(traces, device):
     T = importlib.import_module(PKG + ".tokenizer")
     E = importlib.import_module(PKG + ".engine")
     R = importlib.import_module(PKG + ".runtime")
-    tok = T.CharTokenizer("llama3")
+    tok = T.CharTokenizer(traces.get("family", "llama3"))
     cfg = Mm.preset(traces["preset"], vocab=traces["vocab"])
     cpu = Mm.Model(cfg, "cpu", torch.float32, seed=traces["weight_seed"])
     w = {k: v.to(device) for k, v in cpu.w.items()}

@@ -12,9 +12,9 @@ import method_parity as mp
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def traces(dev):
-    t = mp.load_traces()
+@pytest.fixture(scope="module", params=mp.TRACE_FILES)
+def traces(request, dev):
+    t = mp.load_traces(request.param)
     mp.register_fixture_engine(t, dev)
     yield t
     importlib.import_module(mp.PKG + ".runtime").clear_engines()

@@ -18,12 +18,12 @@ import method_parity as mp
 PKG = mp.PKG
 
 
-@pytest.fixture(scope="module")
-def emulated(orc):
+@pytest.fixture(scope="module", params=mp.TRACE_FILES)
+def emulated(request, orc):
     import cpu_emulation
     R = importlib.import_module(PKG + ".runtime")
     saved = cpu_emulation.install()
-    traces = mp.load_traces()
+    traces = mp.load_traces(request.param)
     mp.register_fixture_engine(traces, torch.device("cpu"))
     yield traces
     cpu_emulation.uninstall(saved)
