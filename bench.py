@@ -48,12 +48,33 @@ CONFIGS = {
 }
 
 
+# Beam-search decode steps (BASELINE configs C1, C3, C5).  Total agents are fixed per
+# config and sharded over the ranks (strong scaling); every rank proposes the same
+# candidates from the replicated reference-policy rows.
+BEAM_CONFIGS = {
+    # name: (agents total, beams, top-k, vocab, softcap, logits dtype, description)
+    "c1": (4, 4, 10, 128_256, 0.0, torch.float32,
+           "C1 beam search: B=4 beams x top-10 x A=4 agents, Llama-3.2-1B vocab 128256 fp32 "
+           "logits, egalitarian welfare"),
+    "c3": (16, 16, 50, 256_000, 30.0, torch.bfloat16,
+           "C3 beam search: B=16 beams x top-50 x A=16 agents sharded over the ranks, "
+           "Gemma-2-9B vocab 256000 bf16 logits (soft-cap 30), egalitarian welfare, "
+           "RCCL MIN all-reduce"),
+    "c5": (64, 8, 32, 128_256, 0.0, torch.bfloat16,
+           "C5 beam search: B=8 beams x top-32 x A=64 agents sharded over the ranks, "
+           "Llama-3.3-70B vocab 128256 bf16 logits, egalitarian welfare, RCCL MIN all-reduce"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--beam", default="c1,c3,c5",
+                    help="beam-search decode-step configs reported under 'beam' ('' disables)")
+    ap.add_argument("--beam-steps", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time for the oracle baseline sample (0 disables)")
     ap.add_argument("--backend", default="nccl",
@@ -171,6 +192,134 @@ def end_to_end(A, N, T, V, wkind, dev, steps=2, prefix_len=200, seed=0):
             "note": "forward = PyTorch/hipBLASLt (plumbing); logits -> HIP C-ABI kernels"}
 
 
+def gpu_busy(stream, ms=20.0):
+    """Keep the GPU busy for ~ms so that the launches queued behind are timed by their
+    events without host launch gaps (small kernels would otherwise be host-bound)."""
+    with torch.cuda.stream(stream):
+        try:
+            torch.cuda._sleep(int(ms * 2.0e6))   # ~2 GHz shader clock
+        except (AttributeError, RuntimeError):
+            a = torch.randn(4096, 4096, device=stream.device)
+            for _ in range(int(ms)):
+                a = a @ a.T * 1e-3
+
+
+def run_beam(name, world, rank, dev, steps, warmup):
+    """Beam-search decode steps on resident logits (BASELINE C1 / C3 / C5).
+
+    One decode step, per rank:
+      reference-policy rows [B, V] --cs_vocab_topk(K)--> candidate tokens [B, K]
+      agent rows [A_local*B, V]   --cs_beam_step-->     U = R + lp, W = min over agents
+      [RCCL MIN all-reduce of W when the agents are sharded] --> stable order (top-k)
+      cumulative rewards of the B kept beams  R <- U[:, order[:B]]
+    At N = 1 the whole step is one captured hipGraph; with agents sharded, the per-rank
+    parts are two graphs around the eager all-reduce.
+    """
+    ops = importlib.import_module(PKG_DIR + ".ops")
+    par = importlib.import_module(PKG_DIR + ".parallel")
+    A, B, K, V, cap, dt, desc = BEAM_CONFIGS[name]
+    shard = par.AgentShard(A, rank, world)
+    A_loc = len(shard.local)
+    C = B * K
+    g = torch.Generator(device=dev).manual_seed(4321 + rank)
+    ref = (torch.randn(B, V, generator=g, device=dev) * 3.0).to(dt)
+    ag = (torch.randn(A_loc * B, V, generator=g, device=dev) * 3.0).to(dt)
+    R = torch.zeros(A_loc, B, dtype=torch.float32, device=dev)
+    ws_p, ws_b = ops.Workspace(), ops.Workspace(zeroed=True)
+    sharded = world > 1
+
+    def score():
+        ids, _ = ops.vocab_topk(ref, K, softcap=cap, workspace=ws_p)
+        if A_loc == 0:   # more ranks than agents: this rank only proposes
+            return (torch.empty(0, C, device=dev),
+                    torch.full((C,), float("inf"), device=dev), None)
+        U, W, order, _ = ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else C,
+                                       softcap=cap, workspace=ws_b)
+        return U, W, order
+
+    def keep(U, order):
+        R.copy_(U.index_select(1, order[:B].long()))
+
+    def select(U, W):
+        W = torch.where(torch.isinf(W) & (W > 0), torch.full_like(W, float("nan")), W)
+        order, _ = ops.topk(W, C)
+        keep(U, order)
+
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):   # warm the workspaces / allocator before capture
+            U, W, order = score()
+            if not sharded:
+                keep(U, order)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1):
+        U, W, order = score()
+        if not sharded:
+            keep(U, order)
+        else:
+            Wx = torch.where(torch.isnan(W), torch.full_like(W, float("inf")), W)
+    if sharded:
+        with torch.cuda.graph(g2):
+            select(U, Wx)
+
+    def step():
+        g1.replay()
+        if sharded:
+            torch.distributed.all_reduce(Wx, op=torch.distributed.ReduceOp.MIN)
+            g2.replay()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if sharded:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if sharded:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    if sharded:
+        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = float(tt.item())
+
+    # kernel-level timing (HIP events on the launch stream): cs_beam_step alone, eager
+    st = torch.cuda.current_stream()
+    n_ev = 50
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(n_ev)]
+    ids, _ = ops.vocab_topk(ref, K, softcap=cap, workspace=ws_p)
+    gpu_busy(st)   # the host enqueues every launch before the GPU reaches the first event
+    for e0, e1 in ev:
+        e0.record(st)
+        if A_loc:
+            ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else C, softcap=cap,
+                          workspace=ws_b)
+        e1.record(st)
+    torch.cuda.synchronize()
+    k_ms = max(float(np.median([a.elapsed_time(b) for a, b in ev])), 1e-6)
+    esz = torch.finfo(dt).bits // 8
+    alg = A_loc * B * V * esz
+    ms = el * 1000.0 / steps
+    return {"workload": desc, "agents": A, "agents_per_gpu": A_loc, "beams": B, "top_k": K,
+            "vocab": V, "dtype": str(dt).replace("torch.", ""),
+            "decode_steps_per_s": 1000.0 / ms, "ms_per_step": ms,
+            "scorings_per_s": A * C / (ms * 1e-3), "steps": steps,
+            "timing": "hipGraph replay" + (" + eager RCCL all-reduce" if sharded else ""),
+            "roofline": {"bound": "hbm", "kernel": "cs_beam_step (lsg_stream_kernel + beam_tail_kernel)",
+                         "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
+                         "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "step_bytes": (A_loc * B + B) * V * esz,
+            "step_frac_of_hbm": (A_loc * B + B) * V * esz / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def read_traffic(path, config, rows, V):
     try:
         with open(path) as f:
@@ -234,6 +383,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     ms_per_step = elapsed * 1000.0 / args.steps
 
+    line = None
     if rank == 0:
         scorings = A * N * world
         alg_bytes = rows * V * 2 + rows * 4 * 2  # logits read once + targets in + lp out
@@ -272,6 +422,12 @@ def main():
         }
         if e2e is not None:
             line["end_to_end"] = e2e
+    beam = {}
+    for name in [b for b in args.beam.split(",") if b]:
+        beam[name] = run_beam(name, world, rank, dev, args.beam_steps, 20)
+    if rank == 0:
+        if beam:
+            line["beam"] = beam
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

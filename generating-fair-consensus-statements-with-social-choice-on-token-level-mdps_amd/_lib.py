@@ -24,6 +24,7 @@ EXPORTED = (
     "cs_version", "cs_last_error", "cs_workspace_size", "cs_logsoftmax_gather",
     "cs_segment_reduce", "cs_welfare_reduce", "cs_segmented_topk", "cs_vocab_topk_workspace_size",
     "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
+    "cs_beam_step_workspace_size", "cs_beam_step",
 )
 
 
@@ -79,6 +80,11 @@ def load():
     L.cs_vocab_sample.argtypes = [vp, ctypes.c_int, i64, i64, i64, f32, f32, vp, i32, vp, vp, vp,
                                   ctypes.c_size_t, vp]
     L.cs_vocab_sample.restype = ctypes.c_int
+    L.cs_beam_step_workspace_size.argtypes = [i64, i64]
+    L.cs_beam_step_workspace_size.restype = ctypes.c_size_t
+    L.cs_beam_step.argtypes = [vp, ctypes.c_int, i32, i32, i64, i64, vp, i32, vp, f32, ctypes.c_int,
+                               f32, vp, vp, i32, vp, vp, vp, ctypes.c_size_t, vp]
+    L.cs_beam_step.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -23,7 +23,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-shared", "-fPIC",
+    # -ffp-contract=off: every FMA in the kernels is an explicit fmaf, so kernels that
+    # share a formula (lse, gather, soft-cap) round identically wherever they are inlined
+    cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-shared",
+           "-fPIC",
            "-I", os.path.join(_REPO, "include"), "-o", OUT + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd))

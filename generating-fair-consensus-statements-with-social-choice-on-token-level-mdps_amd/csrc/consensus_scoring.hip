@@ -33,7 +33,9 @@ namespace {
 constexpr int kBlock = 256;   // streaming workgroup: 4 waves of 64
 constexpr int kUnroll = 4;    // 16-byte vectors in flight per lane per iteration
 constexpr int kMergeBlock = 64;
-constexpr int64_t kTargetWgs = 2048;  // ~8 streaming workgroups per CU on 256 CUs
+// split-V below this many workgroups: one 1024-thread workgroup per row already streams at
+// the launch's floor once rows >= 256 (tools/split_sweep.py; profiles/r01_split_sweep.jsonl)
+constexpr int64_t kTargetWgs = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
 thread_local std::string g_last_error = "";
@@ -111,10 +113,11 @@ __device__ __forceinline__ float load_one(const char* row, int64_t i) {
 
 // Gemma-2 final-logit soft-capping, cap * tanh(x / cap), with tanh written through
 // one exp2 so the vocab stream and the target gather use the identical function.
+// tanh(z) = 1 - 2 / (exp(2z) + 1) with the hardware reciprocal (1 ulp): two
+// transcendental ops per element; |error| ~ 1e-6 * cap, far inside the 1e-3 budget.
 __device__ __forceinline__ float softcap_fn(float x, float cap, float inv_cap) {
-  const float z = x * inv_cap;
-  const float e = __builtin_amdgcn_exp2f(2.0f * kLog2e * z);  // exp(2z); inf for large z
-  const float t = 1.0f - 2.0f / (e + 1.0f);
+  const float e = __builtin_amdgcn_exp2f(x * (2.0f * kLog2e) * inv_cap);  // exp(2x/cap); inf ok
+  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
   return cap * t;
 }
 
@@ -125,12 +128,22 @@ __device__ __forceinline__ float softcap_fn(float x, float cap, float inv_cap) {
 __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
   const float mn = fmaxf(m, m2);
   if (mn == -INFINITY) return;
+  // Symmetric in its two operands (two rounded products, one add; the library is built
+  // with -ffp-contract=off), so both lanes of a butterfly pair compute the same merge
+  // and every lane of a reduced wave holds bit-identical (m, s).
   s = s * __builtin_amdgcn_exp2f((m - mn) * kLog2e) + s2 * __builtin_amdgcn_exp2f((m2 - mn) * kLog2e);
   m = mn;
 }
 
-template <int N>
+template <int N, bool FIXED = false>
 __device__ __forceinline__ void lse_accum(float& m, float& s, const float* v) {
+  if constexpr (FIXED) {  // m stays 0 (bounded soft-capped logits): s += sum exp(v)
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc += __builtin_amdgcn_exp2f(v[i] * kLog2e);
+    s += acc;
+    return;
+  }
   float cm = v[0];
 #pragma unroll
   for (int i = 1; i < N; ++i) cm = fmaxf(cm, v[i]);
@@ -178,28 +191,94 @@ __device__ __forceinline__ void gather_targets(const char* row, int64_t vocab, f
 // ---------------------------------------------------------------------------
 // streaming kernel: one workgroup per (row, split) work item
 // ---------------------------------------------------------------------------
-// BLOCK   threads per workgroup (multiple of 64)
-// UNROLL  16-byte vectors each lane has in flight per iteration
-// NT      non-temporal loads (each logits byte is read exactly once)
-// PIPE    register double-buffering: the next iteration's loads are issued before
-//         the current vectors are reduced
-// Work items (row, split) are walked grid-stride so a capped grid also works.
-template <int DT>
-__device__ __forceinline__ u32x4 ld16(const u32x4* p, bool nt) {
-  return nt ? __builtin_nontemporal_load(p) : *p;
+// One workgroup's (m, s) over logits[v0, v0 + n) of one row: scalar head up to the
+// first 16-byte boundary and scalar tail after the last full vector, UNROLL
+// non-temporal 16-byte loads in flight per lane (each logits byte is read once),
+// wave64 butterfly, then the waves merged in order through LDS.  The result is valid
+// in thread 0.  FIXED (soft-capped logits, |x'| <= cap <= 60): the sum needs no running
+// max, s = sum exp(x') with m = 0, so the inner loop has no max / rescale.
+template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
+__device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp, int64_t v0,
+                                                    int64_t n, float cap, float inv_cap,
+                                                    float* sm_m, float* sm_s) {
+  constexpr int ESZ = Elt<DT>::kSize;
+  constexpr int EPV = Elt<DT>::kPerVec;
+  constexpr int NW = BLOCK / 64;
+  const int tid = threadIdx.x;
+  float m = FIXED ? 0.0f : -INFINITY, s = 0.0f;
+
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(rp + v0 * ESZ);
+  int64_t head = static_cast<int64_t>(((16u - (a0 & 15u)) & 15u) / ESZ);
+  if (head > n) head = n;
+  const int64_t nvec = (n - head) / EPV;
+  const int64_t tail0 = head + nvec * EPV;
+  {
+    float x = -INFINITY;
+    if (tid < head) {
+      x = load_one<DT>(rp, v0 + tid);
+      if (CAP) x = softcap_fn(x, cap, inv_cap);
+    } else if (tid >= 64 && tid - 64 < n - tail0) {
+      x = load_one<DT>(rp, v0 + tail0 + (tid - 64));
+      if (CAP) x = softcap_fn(x, cap, inv_cap);
+    }
+    if (x != -INFINITY) lse_accum<1, FIXED>(m, s, &x);
+  }
+
+  const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
+  int64_t i = tid;
+  constexpr int STEP = UNROLL * BLOCK;
+  for (; i + (UNROLL - 1) * BLOCK < nvec; i += STEP) {
+    u32x4 q[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * BLOCK);
+    float v[UNROLL * EPV];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
+    if (CAP) {
+#pragma unroll
+      for (int e = 0; e < UNROLL * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+    }
+    lse_accum<UNROLL * EPV, FIXED>(m, s, v);
+  }
+  for (; i < nvec; i += BLOCK) {
+    const u32x4 q = __builtin_nontemporal_load(vp + i);
+    float v[EPV];
+    unpack_vec<DT>(q, v);
+    if (CAP) {
+#pragma unroll
+      for (int e = 0; e < EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
+    }
+    lse_accum<EPV, FIXED>(m, s, v);
+  }
+
+  wave_lse_reduce(m, s);
+  const int wave = tid >> 6;
+  if ((tid & 63) == 0) {
+    sm_m[wave] = m;
+    sm_s[wave] = s;
+  }
+  __syncthreads();
+  float mm = sm_m[0], ss = sm_s[0];
+  if (tid == 0) {
+#pragma unroll
+    for (int w = 1; w < NW; ++w) lse_merge(mm, ss, sm_m[w], sm_s[w]);
+  }
+  return make_float2(mm, ss);
 }
 
-template <int DT, bool CAP, int BLOCK, int UNROLL, bool NT, bool PIPE>
+// The fixed-offset sum is exact enough and cannot overflow for |x'| <= 60:
+// e^60 * 2^31 < FLT_MAX and e^-60 is a normal float.
+inline bool fixed_lse_ok(float cap) { return cap > 0.0f && cap <= 60.0f; }
+
+// Work items (row, split) are walked grid-stride so a capped grid also works.
+template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void lsg_stream_kernel(
     const char* __restrict__ logits, int64_t n_items, int64_t vocab, int64_t ld_bytes,
     int32_t nsplit, int64_t split_len, const int32_t* __restrict__ tgt, int32_t k, float cap,
     float inv_cap, float* __restrict__ out_tok, float* __restrict__ out_lse,
     float2* __restrict__ part) {
-  constexpr int ESZ = Elt<DT>::kSize;
-  constexpr int EPV = Elt<DT>::kPerVec;
-  constexpr int NW = BLOCK / 64;
-  __shared__ float sm_m[NW];
-  __shared__ float sm_s[NW];
+  __shared__ float sm_m[BLOCK / 64];
+  __shared__ float sm_s[BLOCK / 64];
   __shared__ float sm_lse;
   const int tid = threadIdx.x;
 
@@ -209,101 +288,13 @@ __global__ __launch_bounds__(BLOCK) void lsg_stream_kernel(
     const char* rp = logits + row * ld_bytes;
     const int64_t v0 = static_cast<int64_t>(split) * split_len;
     const int64_t v1 = min(vocab, v0 + split_len);
-    const int64_t n = v1 - v0;
-
-    float m = -INFINITY, s = 0.0f;
-
-    // scalar head up to the first 16-byte boundary, scalar tail after the last full vector
-    const uintptr_t a0 = reinterpret_cast<uintptr_t>(rp + v0 * ESZ);
-    int64_t head = static_cast<int64_t>(((16u - (a0 & 15u)) & 15u) / ESZ);
-    if (head > n) head = n;
-    const int64_t nvec = (n - head) / EPV;
-    const int64_t tail0 = head + nvec * EPV;
-    {
-      float x = -INFINITY;
-      if (tid < head) {
-        x = load_one<DT>(rp, v0 + tid);
-        if (CAP) x = softcap_fn(x, cap, inv_cap);
-      } else if (tid >= 64 && tid - 64 < n - tail0) {
-        x = load_one<DT>(rp, v0 + tail0 + (tid - 64));
-        if (CAP) x = softcap_fn(x, cap, inv_cap);
-      }
-      if (x != -INFINITY) lse_accum<1>(m, s, &x);
-    }
-
-    const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
-    int64_t i = tid;
-    constexpr int STEP = UNROLL * BLOCK;
-    if (PIPE) {
-      u32x4 q[UNROLL];
-      bool have = i + (UNROLL - 1) * BLOCK < nvec;
-      if (have) {
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) q[u] = ld16<DT>(vp + i + u * BLOCK, NT);
-      }
-      while (have) {
-        const bool next = i + STEP + (UNROLL - 1) * BLOCK < nvec;
-        u32x4 qn[UNROLL];
-        if (next) {
-#pragma unroll
-          for (int u = 0; u < UNROLL; ++u) qn[u] = ld16<DT>(vp + i + STEP + u * BLOCK, NT);
-        }
-        float v[UNROLL * EPV];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
-        if (CAP) {
-#pragma unroll
-          for (int e = 0; e < UNROLL * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-        }
-        lse_accum<UNROLL * EPV>(m, s, v);
-        i += STEP;
-        have = next;
-        if (next) {
-#pragma unroll
-          for (int u = 0; u < UNROLL; ++u) q[u] = qn[u];
-        }
-      }
-    } else {
-      for (; i + (UNROLL - 1) * BLOCK < nvec; i += STEP) {
-        u32x4 q[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) q[u] = ld16<DT>(vp + i + u * BLOCK, NT);
-        float v[UNROLL * EPV];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
-        if (CAP) {
-#pragma unroll
-          for (int e = 0; e < UNROLL * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-        }
-        lse_accum<UNROLL * EPV>(m, s, v);
-      }
-    }
-    for (; i < nvec; i += BLOCK) {
-      const u32x4 q = ld16<DT>(vp + i, NT);
-      float v[EPV];
-      unpack_vec<DT>(q, v);
-      if (CAP) {
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-      }
-      lse_accum<EPV>(m, s, v);
-    }
-
-    wave_lse_reduce(m, s);
-    const int wave = tid >> 6;
-    if ((tid & 63) == 0) {
-      sm_m[wave] = m;
-      sm_s[wave] = s;
-    }
-    __syncthreads();
+    const float2 ms =
+        block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
     if (tid == 0) {
-      float mm = sm_m[0], ss = sm_s[0];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) lse_merge(mm, ss, sm_m[w], sm_s[w]);
       if (nsplit > 1) {
-        part[bid] = make_float2(mm, ss);
+        part[bid] = ms;
       } else {
-        const float lse = mm + logf(ss);
+        const float lse = ms.x + logf(ms.y);
         sm_lse = lse;
         if (out_lse) out_lse[row] = lse;
       }
@@ -435,7 +426,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ W, 
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = tid; t < (n2 >> 1); t += 256) {
-        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int lo = ((t & ~(stride - 1)) << 1) | (t & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
         const unsigned long long a = ck[lo], b = ck[hi];
@@ -465,12 +456,19 @@ struct SplitPlan {
   int64_t split_len;
 };
 
+int64_t target_wgs() {
+  const char* e = getenv("CS_TARGET_WGS");  // tuning knob (tools/beam_ab.py); default 2048
+  const int64_t v = e ? atoll(e) : 0;
+  return v > 0 ? v : kTargetWgs;
+}
+
 SplitPlan plan_split(int64_t rows, int64_t vocab, int dtype) {
   SplitPlan p{1, vocab};
-  if (rows <= 0 || vocab <= 0 || rows >= kTargetWgs) return p;
+  const int64_t target = target_wgs();
+  if (rows <= 0 || vocab <= 0 || rows >= target) return p;
   const int64_t grain = static_cast<int64_t>(kBlock) * elt_per_vec(dtype);  // one vector per lane
   const int64_t min_len = grain * kUnroll;  // >= one full unrolled sweep per split
-  int64_t want = (kTargetWgs + rows - 1) / rows;
+  int64_t want = (target + rows - 1) / rows;
   int64_t max_split = vocab / min_len;
   if (max_split < 1) max_split = 1;
   if (want > max_split) want = max_split;
@@ -497,10 +495,20 @@ template <int DT, bool CAP, int BLOCK, int UNROLL>
 void launch_stream(const void* logits, int64_t items, int64_t vocab, int64_t ld_bytes,
                    const SplitPlan& plan, const int32_t* tgt, int32_t k, float cap, float inv_cap,
                    float* out_tok, float* out_lse, float2* part, hipStream_t st) {
-  hipLaunchKernelGGL((lsg_stream_kernel<DT, CAP, BLOCK, UNROLL, true, false>),
-                     dim3(static_cast<uint32_t>(items)), dim3(BLOCK), 0, st,
-                     static_cast<const char*>(logits), items, vocab, ld_bytes, plan.nsplit,
-                     plan.split_len, tgt, k, cap, inv_cap, out_tok, out_lse, part);
+  const char* lg = static_cast<const char*>(logits);
+  if constexpr (CAP) {
+    if (fixed_lse_ok(cap)) {
+      hipLaunchKernelGGL((lsg_stream_kernel<DT, CAP, true, BLOCK, UNROLL>),
+                         dim3(static_cast<uint32_t>(items)), dim3(BLOCK), 0, st, lg, items, vocab,
+                         ld_bytes, plan.nsplit, plan.split_len, tgt, k, cap, inv_cap, out_tok,
+                         out_lse, part);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((lsg_stream_kernel<DT, CAP, false, BLOCK, UNROLL>),
+                       dim3(static_cast<uint32_t>(items)), dim3(BLOCK), 0, st, lg, items, vocab,
+                       ld_bytes, plan.nsplit, plan.split_len, tgt, k, cap, inv_cap, out_tok,
+                       out_lse, part);
 }
 
 int lsg_variant() {
@@ -511,7 +519,7 @@ int lsg_variant() {
 template <int DT, bool CAP>
 void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_bytes,
                 const SplitPlan& plan, const int32_t* tgt, int32_t k, float cap, float* out_tok,
-                float* out_lse, float2* part, hipStream_t st) {
+                float* out_lse, float2* part, hipStream_t st, bool finish = true) {
   const float inv_cap = CAP ? 1.0f / cap : 0.0f;
   const int64_t items = rows * plan.nsplit;
   switch (lsg_variant()) {
@@ -544,7 +552,7 @@ void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_byte
                                        inv_cap, out_tok, out_lse, part, st);
       break;
   }
-  if (plan.nsplit > 1) {
+  if (plan.nsplit > 1 && finish) {
     hipLaunchKernelGGL((lsg_merge_kernel<DT, CAP>), dim3(static_cast<uint32_t>(rows)),
                        dim3(kMergeBlock), 0, st, static_cast<const char*>(logits), vocab, ld_bytes,
                        plan.nsplit, part, tgt, k, cap, inv_cap, out_tok, out_lse);
@@ -574,7 +582,7 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* ck, int n2, int
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = tid; t < (n2 >> 1); t += nthr) {
-        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int lo = ((t & ~(stride - 1)) << 1) | (t & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
         const unsigned long long a = ck[lo], b = ck[hi];
@@ -766,6 +774,240 @@ int32_t topk_nchunk(int64_t vocab) {
   return static_cast<int32_t>((vocab + kTopkChunk - 1) / kTopkChunk);
 }
 
+// ---------------------------------------------------------------------------
+// beam step: one launch from logits to the ordered candidates
+// ---------------------------------------------------------------------------
+// A whole beam-search scoring step after the LM head (beam_search.py:495-560) in ONE
+// launch, one workgroup per (agent row, vocab split):
+//   1. stream the split -> (m, s) partial (block_lse_partial, as lsg_stream_kernel);
+//   2. the LAST workgroup to finish a row (arrival counter per row) merges the row's
+//      partials in split order (one wave, lanes over splits: lsg_merge_kernel's
+//      arithmetic), gathers the row's K candidate tokens and writes
+//      U[a, b*K+j] = R[a, b] + lp (fp32, the method's cumulative reward);
+//   3. the LAST row to finish (one more counter) folds the welfare of every candidate
+//      over the agents in agent order in fp64 (welfare_kernel's fold, non-finite
+//      skipped) and, when B*K <= kFusedSort, sorts the (value desc, index asc) keys in
+//      LDS (topk_kernel's keys).
+// Bit-identical to cs_logsoftmax_gather + cs_welfare_reduce + cs_segmented_topk.
+// Hand-offs use sc1 stores / loads and arrival counters (no fences, see st_sc1).
+// Nobody waits on anybody, so the launch cannot stall; the last arrivers reset the
+// counters to zero, which keeps the workspace reusable (and graph-replayable) without
+// a memset.
+// Cross-workgroup hand-off without fences (MI355X_MICROARCH.md, hand-off table row 1):
+// every handed-off byte is stored and loaded with sc1 (agent-scope relaxed atomics lower
+// to global_store/global_load ... sc1: write-through past the L2, L1 bypassed), every
+// storing wave waits vmcnt(0), the workgroup barriers, and ONE lane then adds to the
+// arrival counter; the workgroup whose add returns the last count consumes.
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_sc1(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint32_t arrive(uint32_t* cnt) {
+  return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kFusedSort = 1024;      // candidates sorted inside the launch
+constexpr int kBeamMaxRows = 65536;   // A * B (one arrival counter per row)
+constexpr size_t kBeamCounterBytes = 64 + sizeof(uint32_t) * kBeamMaxRows;
+
+__device__ __forceinline__ void welfare_fold(double& acc, bool& any, float u, int kind,
+                                             double eps) {
+  if (!__builtin_isfinite(u)) return;  // SKIP (and the masked tail of a batch)
+  const double d = static_cast<double>(u);
+  switch (kind) {
+    case CS_WELFARE_MIN:
+      acc = any ? fmin(acc, d) : d;
+      break;
+    case CS_WELFARE_MAX:
+      acc = any ? fmax(acc, d) : d;
+      break;
+    case CS_WELFARE_SUM:
+      acc += d;
+      break;
+    default:
+      acc += log(fmax(d, eps));
+      break;
+  }
+  any = true;
+}
+
+// Welfare of NQ candidates (c0, c0 + stride, ...) over all agents, in agent order; NQ x NA
+// sc1 loads in flight per batch so the fold costs about one memory round trip per batch.
+template <int NQ, int NA>
+__device__ __forceinline__ void fold_candidates(uint32_t* U, int32_t A, int32_t C, int32_t c0,
+                                                int32_t stride, int kind, double eps,
+                                                double* acc, bool* any) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    acc[q] = 0.0;
+    any[q] = false;
+  }
+  for (int32_t a0 = 0; a0 < A; a0 += NA) {
+    float ub[NQ][NA];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int32_t c = c0 + q * stride;
+#pragma unroll
+      for (int j = 0; j < NA; ++j)
+        ub[q][j] = (c < C && a0 + j < A)
+                       ? __uint_as_float(ld_sc1(U + static_cast<int64_t>(a0 + j) * C + c))
+                       : __builtin_nanf("");
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) welfare_fold(acc[q], any[q], ub[q][j], kind, eps);
+    }
+  }
+}
+
+template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
+__global__ __launch_bounds__(BLOCK) void beam_step_kernel(
+    const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nsplit,
+    int64_t split_len, int32_t A, int32_t B, int32_t K, const int32_t* __restrict__ tgt,
+    const float* __restrict__ R, float cap, float inv_cap, int kind, double eps,
+    unsigned long long* __restrict__ part, uint32_t* __restrict__ row_cnt,
+    uint32_t* __restrict__ done_cnt, float* __restrict__ U, float* __restrict__ W,
+    int32_t n_order, int32_t n2, int32_t* __restrict__ out_order, float* __restrict__ out_val) {
+  __shared__ float sm_m[BLOCK / 64];
+  __shared__ float sm_s[BLOCK / 64];
+  __shared__ float sm_lse;
+  __shared__ int sm_last;
+  __shared__ __attribute__((aligned(16))) unsigned long long keys[kFusedSort];
+  __shared__ float sm_w[kFusedSort];
+  const int tid = threadIdx.x;
+  const int32_t rows = A * B;
+  const int32_t C = B * K;
+  const int64_t item = blockIdx.x;
+  const int32_t row = static_cast<int32_t>(item / nsplit);
+  const int32_t split = static_cast<int32_t>(item - static_cast<int64_t>(row) * nsplit);
+  const int32_t ag = row / B;
+  const int32_t bm = row - ag * B;
+  const char* rp = logits + row * ld_bytes;
+  const int64_t v0 = static_cast<int64_t>(split) * split_len;
+  const int64_t v1 = min(vocab, v0 + split_len);
+  uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
+  // the candidate ids are read now (not used before the row finish), so the finisher's
+  // logit gather does not wait on a dependent id load
+  const int32_t t_pre = (tid < K) ? tgt[bm * K + tid] : -1;
+
+  // 1. stream
+  const float2 ms =
+      block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
+
+  // 2. row finish by the row's last arriver
+  if (nsplit > 1) {
+    if (tid == 0) {
+      st_sc1(part + item, (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
+                              __float_as_uint(ms.x));
+      wait_stores();
+      sm_last = arrive(&row_cnt[row]) == static_cast<uint32_t>(nsplit - 1);
+    }
+    __syncthreads();
+    if (!sm_last) return;  // block-uniform
+    if (tid < 64) {
+      float m = -INFINITY, s = 0.0f;
+      for (int j = tid; j < nsplit; j += 64) {
+        const unsigned long long p = ld_sc1(part + static_cast<int64_t>(row) * nsplit + j);
+        lse_merge(m, s, __uint_as_float(static_cast<uint32_t>(p)),
+                  __uint_as_float(static_cast<uint32_t>(p >> 32)));
+      }
+      wave_lse_reduce(m, s);
+      if (tid == 0) {
+        sm_lse = m + logf(s);
+        row_cnt[row] = 0u;
+      }
+    }
+  } else if (tid == 0) {
+    sm_lse = ms.x + logf(ms.y);
+  }
+  {
+    // gather (issued before the barrier that publishes the lse)
+    float xg = 0.0f;
+    const bool ok = t_pre >= 0 && t_pre < vocab;
+    if (ok) xg = load_one<DT>(rp, t_pre);
+    __syncthreads();
+    const float r0 = R[row];
+    const float lse = sm_lse;
+    for (int32_t j = tid; j < K; j += BLOCK) {
+      float x = xg;
+      bool okj = ok;
+      if (j >= BLOCK) {  // K > BLOCK: the remaining ids the early read did not cover
+        const int32_t t = tgt[bm * K + j];
+        okj = t >= 0 && t < vocab;
+        if (okj) x = load_one<DT>(rp, t);
+      }
+      float lp = __builtin_nanf("");
+      if (okj) {
+        if (CAP) x = softcap_fn(x, cap, inv_cap);
+        lp = x - lse;
+      }
+      st_sc1(Uw + static_cast<int64_t>(ag) * C + bm * K + j, __float_as_uint(r0 + lp));
+    }
+  }
+
+  // 3. welfare + order by the last row
+  wait_stores();
+  __syncthreads();
+  if (tid == 0) sm_last = arrive(done_cnt) == static_cast<uint32_t>(rows - 1);
+  __syncthreads();
+  if (!sm_last) return;  // block-uniform
+  if (tid == 0) *done_cnt = 0u;
+  const bool sort_here = n_order > 0 && n2 <= kFusedSort;
+  if (C <= BLOCK) {
+    double acc[1];
+    bool any[1];
+    fold_candidates<1, 64>(Uw, A, C, tid, BLOCK, kind, eps, acc, any);
+    if (tid < C) {
+      const float w = any[0] ? static_cast<float>(acc[0]) : __builtin_nanf("");
+      W[tid] = w;
+      if (sort_here) sm_w[tid] = w;
+    }
+  } else {
+    for (int32_t c0 = tid; c0 < C; c0 += 4 * BLOCK) {
+      double acc[4];
+      bool any[4];
+      fold_candidates<4, 16>(Uw, A, C, c0, BLOCK, kind, eps, acc, any);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int32_t c = c0 + q * BLOCK;
+        if (c < C) {
+          const float w = any[q] ? static_cast<float>(acc[q]) : __builtin_nanf("");
+          W[c] = w;
+          if (sort_here) sm_w[c] = w;
+        }
+      }
+    }
+  }
+  if (!sort_here) return;  // block-uniform
+  __syncthreads();
+  for (int32_t c = tid; c < C; c += BLOCK)
+    keys[c] = (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
+              static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c));
+  __syncthreads();
+  // rank of each candidate among all C (keys are distinct: the index is in the low word):
+  // barrier-free, every lane reads the same key at once (LDS broadcast)
+  for (int32_t c = tid; c < C; c += BLOCK) {
+    const unsigned long long kc = keys[c];
+    int32_t r = 0;
+#pragma unroll 8
+    for (int32_t j = 0; j < C; ++j) r += keys[j] > kc ? 1 : 0;
+    if (r < n_order) {
+      out_order[r] = c;
+      if (out_val) out_val[r] = sm_w[c];
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -895,6 +1137,98 @@ int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld
   return check_launch("cs_segmented_topk");
 }
 
+
+// workspace: [done counter | pad to 64 B][row counters: kBeamMaxRows u32][row partials
+// rows*nsplit x 8 B].  The counters sit at fixed offsets whatever the shape, so calls of
+// different shapes can share one workspace: every call leaves them at zero.
+size_t cs_beam_step_workspace_size(int64_t rows, int64_t vocab) {
+  if (rows <= 0 || vocab <= 0) return 0;
+  const SplitPlan p = plan_split(rows, vocab, CS_BF16);
+  const SplitPlan q = plan_split(rows, vocab, CS_F32);
+  const int64_t ns = p.nsplit > q.nsplit ? p.nsplit : q.nsplit;
+  return kBeamCounterBytes + static_cast<size_t>(rows) * ns * sizeof(unsigned long long);
+}
+
+int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vocab, int64_t ld,
+                 const int32_t* targets, int32_t K, const float* rewards_in, float softcap,
+                 int welfare_kind, float eps, float* out_U, float* out_W, int32_t n_order,
+                 int32_t* out_order, float* out_order_val, void* workspace,
+                 size_t workspace_bytes, cs_stream_t stream) {
+  if (dtype != CS_F32 && dtype != CS_BF16 && dtype != CS_F16)
+    return fail(CS_ERR_INVALID, "cs_beam_step: unknown dtype");
+  if (A < 0 || B < 0 || K < 0 || vocab <= 0 || ld < vocab)
+    return fail(CS_ERR_INVALID, "cs_beam_step: need A, B, K >= 0, vocab > 0, ld >= vocab");
+  const int64_t rows = static_cast<int64_t>(A) * B;
+  const int64_t C = static_cast<int64_t>(B) * K;
+  if (C > 16384) return fail(CS_ERR_INVALID, "cs_beam_step: B*K exceeds 16384");
+  if (rows > kBeamMaxRows) return fail(CS_ERR_INVALID, "cs_beam_step: A*B exceeds 65536");
+  if (n_order < 0 || n_order > C) return fail(CS_ERR_INVALID, "cs_beam_step: need 0 <= n_order <= B*K");
+  if (welfare_kind < CS_WELFARE_MIN || welfare_kind > CS_WELFARE_MAX)
+    return fail(CS_ERR_INVALID, "cs_beam_step: unknown welfare kind");
+  if (!(softcap >= 0.0f) || std::isinf(softcap))
+    return fail(CS_ERR_INVALID, "cs_beam_step: softcap must be finite and >= 0");
+  if (C == 0) return CS_OK;
+  if (A == 0) return fail(CS_ERR_INVALID, "cs_beam_step: no agents");
+  if (!logits || !targets || !rewards_in || !out_U || !out_W || (n_order > 0 && !out_order))
+    return fail(CS_ERR_INVALID, "cs_beam_step: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(logits) % elt_size(dtype) != 0)
+    return fail(CS_ERR_INVALID, "cs_beam_step: logits not element-aligned");
+  const SplitPlan plan = plan_split(rows, vocab, dtype);
+  const size_t need = kBeamCounterBytes + static_cast<size_t>(rows) * plan.nsplit * sizeof(unsigned long long);
+  if (!workspace || workspace_bytes < need)
+    return fail(CS_ERR_WORKSPACE, "cs_beam_step: workspace smaller than cs_beam_step_workspace_size()");
+  if (reinterpret_cast<uintptr_t>(workspace) % 8 != 0)
+    return fail(CS_ERR_WORKSPACE, "cs_beam_step: workspace not 8-byte aligned");
+  if (rows * plan.nsplit > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_beam_step: grid too large");
+  char* wsb = static_cast<char*>(workspace);
+  auto* done_cnt = reinterpret_cast<uint32_t*>(wsb);
+  auto* row_cnt = reinterpret_cast<uint32_t*>(wsb + 64);
+  auto* part = reinterpret_cast<unsigned long long*>(wsb + kBeamCounterBytes);
+  const int64_t ld_bytes = ld * elt_size(dtype);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool cap = softcap > 0.0f;
+  const bool fixed = fixed_lse_ok(softcap);
+  const float inv_cap = cap ? 1.0f / softcap : 0.0f;
+  int32_t n2 = 2;
+  while (n2 < C) n2 <<= 1;
+  const char* lg = static_cast<const char*>(logits);
+  const dim3 grid(static_cast<uint32_t>(rows * plan.nsplit));
+  // the same streaming shapes as cs_logsoftmax_gather (bit-identical lse)
+#define CS_BEAM_LAUNCH(DTV, CAPV, FIXV)                                                           \
+  do {                                                                                            \
+    if (plan.nsplit > 1)                                                                          \
+      hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 256, 8>), grid, dim3(256), 0, st, lg, \
+                         vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,          \
+                         rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
+                         part, row_cnt, done_cnt, out_U, out_W, n_order, n2, out_order,           \
+                         out_order_val);                                                          \
+    else                                                                                          \
+      hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 1024, 2>), grid, dim3(1024), 0, st,   \
+                         lg, vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,      \
+                         rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
+                         part, row_cnt, done_cnt, out_U, out_W, n_order, n2, out_order,           \
+                         out_order_val);                                                          \
+  } while (0)
+  if (dtype == CS_F32) {
+    if (fixed) CS_BEAM_LAUNCH(CS_F32, true, true);
+    else if (cap) CS_BEAM_LAUNCH(CS_F32, true, false);
+    else CS_BEAM_LAUNCH(CS_F32, false, false);
+  } else if (dtype == CS_BF16) {
+    if (fixed) CS_BEAM_LAUNCH(CS_BF16, true, true);
+    else if (cap) CS_BEAM_LAUNCH(CS_BF16, true, false);
+    else CS_BEAM_LAUNCH(CS_BF16, false, false);
+  } else {
+    if (fixed) CS_BEAM_LAUNCH(CS_F16, true, true);
+    else if (cap) CS_BEAM_LAUNCH(CS_F16, true, false);
+    else CS_BEAM_LAUNCH(CS_F16, false, false);
+  }
+#undef CS_BEAM_LAUNCH
+  if (n_order > 0 && n2 > kFusedSort)
+    hipLaunchKernelGGL(topk_kernel, dim3(1), dim3(256), static_cast<size_t>(n2) * sizeof(unsigned long long),
+                       st, out_W, static_cast<int32_t>(C), static_cast<int64_t>(C), n2, n_order,
+                       out_order, out_order_val);
+  return check_launch("cs_beam_step");
+}
 
 size_t cs_vocab_topk_workspace_size(int64_t rows, int64_t vocab, int32_t k) {
   if (rows <= 0 || vocab <= 0 || k <= 0) return 0;

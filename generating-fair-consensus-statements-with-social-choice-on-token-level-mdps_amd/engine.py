@@ -62,6 +62,7 @@ class ScoringEngine:
         self.max_rows = max_rows_per_chunk
         self.max_streams = max_streams_per_chunk
         self.ws = ops.Workspace()
+        self.beam_ws = ops.Workspace(zeroed=True)   # cs_beam_step (arrival counters)
 
     # --- prefixes ---------------------------------------------------------------
     @torch.no_grad()
@@ -207,6 +208,11 @@ class BeamState:
         P, B, K = targets.shape
         tok = self.e.rows_logprobs(self.next_hidden, targets.reshape(P * B, K))
         return tok.view(P, B, K)
+
+    def agent_logits(self, n_prefix: int) -> torch.Tensor:
+        """Logits rows [n_prefix * n_beams, V] of the first n_prefix prefixes (the agents),
+        row p * n_beams + b — the layout cs_beam_step takes."""
+        return self.e.model.lm_head(self.next_hidden[:n_prefix * self.n_beams])
 
     def next_logits(self, prefix_idx: int) -> torch.Tensor:
         """Raw logits rows [n_beams, V] of one prefix (e.g. the reference policy)."""

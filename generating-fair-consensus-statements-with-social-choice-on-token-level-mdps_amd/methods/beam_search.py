@@ -8,10 +8,10 @@ Reference step (beam_search.py:439-617), same config keys:
     beam_width unique in draw order.  proposer="topk": the deterministic top-K
     tokens per beam (cs_vocab_topk), K = config "top_k" (BASELINE configs).
   * per (beam, token, agent): log p(token | agent prompt + beam) (:335-404,
-    495-538)  ->  ONE logits row per (agent, beam) from the incremental beam state,
-    gathered at every candidate token of that beam (cs_logsoftmax_gather, k > 1).
-  * cumulative agent rewards; stable sort by min over agents (:534-560)  ->
-    cs_welfare_reduce(MIN) + cs_segmented_topk over all B*K candidates.
+    495-538), cumulative agent rewards and the stable sort by min over agents
+    (:534-560)  ->  ONE logits row per (agent, beam) from the incremental beam state
+    and ONE cs_beam_step launch: stream every row, gather every candidate token of
+    its beam, U = R + lp, min over agents, stable order over all B*K candidates.
   * dedupe / EOS / keep beam_width walk (:562-600) and final >= 5-word filter +
     selection (:619-667): host logic over the kernel's order, as in the reference.
 """
@@ -129,21 +129,25 @@ class BeamSearchGenerator(BaseGenerator):
             if not cb:
                 break
             K = max(len(t) for t in props)
-            tgt = torch.full((A + 1, st.n_beams, K), -1, dtype=torch.int32)
+            tgt = torch.full((st.n_beams, K), -1, dtype=torch.int32)   # -1 = padded slot
             for b, toks in enumerate(props):
                 if toks:
-                    tgt[:, b, :len(toks)] = torch.as_tensor(toks, dtype=torch.int32)
-            lp = st.next_logprobs(tgt.to(dev))[:A]                          # [A, B, K]
+                    tgt[b, :len(toks)] = torch.as_tensor(toks, dtype=torch.int32)
             pos_in_beam, cnt = [], {}
             for b in cb:
                 pos_in_beam.append(cnt.get(b, 0))
                 cnt[b] = cnt.get(b, 0) + 1
-            slot = torch.as_tensor([b * K + k for b, k in zip(cb, pos_in_beam)], dtype=torch.long,
-                                   device=dev)
-            U = (rewards[:, torch.as_tensor(cb, device=dev)] + lp.reshape(A, -1)[:, slot]).contiguous()
-            W = ops.welfare(U, "min")
-            order, _ = ops.topk(W, len(cb))
-            order = order.cpu().tolist()
+            slots = [b * K + k for b, k in zip(cb, pos_in_beam)]
+            # agent rows -> lp at every candidate, U = R + lp, min over agents, stable
+            # order over the B*K slots (padded slots are NaN: ranked after every real one,
+            # so the order of the real candidates is the reference's stable sort)
+            Up, Wp, order, _ = ops.beam_step(st.agent_logits(A), tgt.to(dev), rewards, "min",
+                                             softcap=st.e.softcap, workspace=st.e.beam_ws)
+            slot_t = torch.as_tensor(slots, dtype=torch.long, device=dev)
+            U = Up[:, slot_t].contiguous()                                    # [A, n_cand]
+            W = Wp[slot_t]
+            cand_of = {s: i for i, s in enumerate(slots)}
+            order = [cand_of[c] for c in order.cpu().tolist() if c in cand_of]
             Uh = U.double().cpu().numpy()
             new_beams, new_idx, seen = [], [], set()
             for i in order:

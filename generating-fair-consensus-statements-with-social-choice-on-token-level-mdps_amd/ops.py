@@ -44,20 +44,26 @@ def _require_cuda(*ts: torch.Tensor) -> None:
 
 class Workspace:
     """Grow-only device scratch for split-V partials (allocation happens here, never
-    inside a launch, so a captured graph can reuse a pre-sized workspace)."""
+    inside a launch, so a captured graph can reuse a pre-sized workspace).
 
-    def __init__(self) -> None:
+    ``zeroed=True`` allocates zero-filled memory: cs_beam_step keeps arrival counters in
+    its workspace that must start at zero (every call leaves them at zero again)."""
+
+    def __init__(self, zeroed: bool = False) -> None:
         self.buf: Optional[torch.Tensor] = None
+        self.zeroed = zeroed
 
     def get(self, nbytes: int, device: torch.device) -> Optional[torch.Tensor]:
         if nbytes == 0:
             return None
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
-            self.buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            alloc = torch.zeros if self.zeroed else torch.empty
+            self.buf = alloc(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         return self.buf
 
 
 _default_ws: dict = {}
+_beam_ws: dict = {}
 
 
 def workspace_size(rows: int, vocab: int, k: int = 1) -> int:
@@ -191,6 +197,61 @@ def topk(W: torch.Tensor, k: int, *, with_values: bool = True):
     if W.dim() == 1:
         return idx[0], (val[0] if val is not None else None)
     return idx, val
+
+
+def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor, kind="min", *,
+              n_order: Optional[int] = None, vocab: Optional[int] = None, softcap: float = 0.0,
+              eps: float = 1e-9, workspace: Optional[Workspace] = None):
+    """One beam-search scoring step after the LM head, fused into one launch.
+
+    logits  [A*B, ld] agent rows (row a*B + b = agent a, beam b);
+    targets [B, K] int32 candidate tokens per beam (ids outside [0, vocab) = padding);
+    rewards [A, B] float32 cumulative per-agent rewards of the beams.
+    Returns (U [A, B*K], W [B*K], order [n_order] int32, order_val [n_order]) with
+    U = rewards + log p(token), W = welfare over agents, order = stable descending
+    (n_order defaults to B*K; 0 skips the sort and returns (U, W, None, None)).
+
+    Restates beam_search.py:495-560 (per-candidate agent log-probs :335-404,
+    cumulative rewards :534-536, stable sort by min over agents :558-560).
+    """
+    L = _lib.load()
+    rows, ld, vocab = _logits_args(logits, vocab)
+    if targets.dim() != 2 or targets.dtype != torch.int32:
+        raise CSError("targets must be [B, K] int32")
+    if rewards.dim() != 2 or rewards.dtype != torch.float32:
+        raise CSError("rewards must be [A, B] float32")
+    targets, rewards = targets.contiguous(), rewards.contiguous()
+    A, B = rewards.shape
+    K = targets.shape[1]
+    if targets.shape[0] != B or rows != A * B:
+        raise CSError(f"shape mismatch: logits rows {rows}, rewards {tuple(rewards.shape)}, "
+                      f"targets {tuple(targets.shape)}")
+    _require_cuda(logits, targets, rewards)
+    if isinstance(kind, str):
+        kind = WELFARE[kind]
+    C = B * K
+    n_order = C if n_order is None else int(n_order)
+    dev = logits.device
+    U = torch.empty((A, C), dtype=torch.float32, device=dev)
+    W = torch.empty(C, dtype=torch.float32, device=dev)
+    order = torch.empty(max(n_order, 0), dtype=torch.int32, device=dev)
+    oval = torch.empty(max(n_order, 0), dtype=torch.float32, device=dev)
+    nbytes = int(L.cs_beam_step_workspace_size(rows, vocab))
+    if workspace is None:
+        workspace = _beam_ws.setdefault(dev, Workspace(zeroed=True))
+    if not workspace.zeroed:
+        raise CSError("beam_step needs a Workspace(zeroed=True) of its own (arrival counters)")
+    ws = workspace.get(nbytes, dev)
+    rc = L.cs_beam_step(logits.data_ptr(), _DTYPE[logits.dtype], A, B, vocab, ld,
+                        targets.data_ptr(), K, rewards.data_ptr(), float(softcap), int(kind),
+                        float(eps), U.data_ptr(), W.data_ptr(), n_order,
+                        order.data_ptr() if n_order else None, oval.data_ptr() if n_order else None,
+                        ws.data_ptr() if ws is not None else None,
+                        ws.numel() if ws is not None else 0, _stream())
+    _lib.check(rc, "cs_beam_step")
+    if n_order == 0:
+        return U, W, None, None
+    return U, W, order, oval
 
 
 def _logits_args(logits: torch.Tensor, vocab: Optional[int]):

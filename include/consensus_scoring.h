@@ -139,6 +139,40 @@ int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld
                       int32_t* out_idx, float* out_val, cs_stream_t stream);
 
 /*
+ * cs_beam_step — one scoring step of token-level beam search after the LM head, in ONE
+ * launch (one workgroup per (agent row, vocab split); the last workgroup of each row
+ * finishes that row, the last row folds the welfare and sorts).
+ *
+ * logits holds the agent rows [A*B][ld] (row a*B + b = agent a's prompt + beam b);
+ * targets [B][K] are the candidate tokens of beam b, shared by every agent (an id
+ * outside [0, vocab) is padding and yields NaN); rewards_in [A][B] is each agent's
+ * cumulative reward of each beam.  With C = B*K and c = b*K + j:
+ *     lp           = x'[a*B+b, targets[c]] - lse[a*B+b]           (as cs_logsoftmax_gather)
+ *     out_U[a*C+c] = rewards_in[a*B+b] + lp                      (fp32 add)
+ *     out_W[c]     = welfare_kind over a of out_U[a*C+c]         (as cs_welfare_reduce, SKIP)
+ *     out_order[r] = index of rank r by (W desc, index asc), NaN last, r < n_order
+ *                    (as cs_segmented_topk); out_order_val (nullable) = W at that index.
+ * Bit-identical to cs_logsoftmax_gather + cs_welfare_reduce + cs_segmented_topk on the
+ * same inputs.  n_order = 0 skips the sort (agent-sharded runs all-reduce out_W
+ * first, then call cs_segmented_topk).  B*K <= 16384 (a second launch sorts when
+ * B*K > 1024).
+ *
+ * WORKSPACE: cs_beam_step_workspace_size() bytes, zero-filled before the first call and
+ * used by one stream at a time.  It holds arrival counters that every call leaves at
+ * zero, so it is reused without a memset (and inside captured graphs).
+ *
+ * Replaces: the per-(beam, token, agent) scoring loop, cumulative rewards and the
+ *   stable sort by min over agents of src/methods/beam_search.py:495-560
+ *   (_get_agent_token_logprob :335-404 per candidate).
+ */
+size_t cs_beam_step_workspace_size(int64_t rows, int64_t vocab);
+int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vocab, int64_t ld,
+                 const int32_t* targets, int32_t K, const float* rewards_in, float softcap,
+                 int welfare_kind, float eps, float* out_U, float* out_W, int32_t n_order,
+                 int32_t* out_order, float* out_order_val, void* workspace,
+                 size_t workspace_bytes, cs_stream_t stream);
+
+/*
  * cs_vocab_topk — deterministic candidate proposer: the k largest (soft-capped)
  * logits of every row, ordered by (value desc, token id asc).
  *

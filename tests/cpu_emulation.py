@@ -12,7 +12,8 @@ import torch
 import oracle as orc
 
 PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
-NAMES = ("logsoftmax_gather", "segment_reduce", "welfare", "topk", "vocab_sample", "vocab_topk")
+NAMES = ("logsoftmax_gather", "segment_reduce", "welfare", "topk", "vocab_sample", "vocab_topk",
+         "beam_step")
 
 
 def _lsg(logits, targets, *, vocab=None, softcap=0.0, workspace=None, want_lse=False, **kw):
@@ -64,8 +65,22 @@ def _vt(logits, k, *, vocab=None, softcap=0.0, workspace=None):
     return torch.as_tensor(ids), torch.as_tensor(vals, dtype=torch.float32)
 
 
+def _bs(logits, targets, rewards, kind="min", *, n_order=None, vocab=None, softcap=0.0,
+        eps=1e-9, workspace=None):
+    A, B = rewards.shape
+    K = targets.shape[1]
+    tok, _ = _lsg(logits, targets.repeat(A, 1), vocab=vocab, softcap=softcap)
+    U = (rewards.float()[:, :, None] + tok.view(A, B, K)).reshape(A, B * K)
+    W = _wel(U, kind, eps=eps)
+    n = B * K if n_order is None else n_order
+    if n == 0:
+        return U, W, None, None
+    order, val = _tk(W, n)
+    return U, W, order.to(torch.int32), val
+
+
 _IMPL = {"logsoftmax_gather": _lsg, "segment_reduce": _seg, "welfare": _wel, "topk": _tk,
-         "vocab_sample": _vs, "vocab_topk": _vt}
+         "vocab_sample": _vs, "vocab_topk": _vt, "beam_step": _bs}
 
 
 def install():

@@ -216,3 +216,67 @@ def test_c2_full_size_sampled_rows(ops, orc, dev):
     assert torch.max(torch.abs(ref_lse - lse)).item() < LP_TOL
     del x
     torch.cuda.empty_cache()
+
+
+BEAM_CASES = [
+    # dtype, A, B, K, vocab, softcap, kind          shape exercised
+    (torch.float32, 4, 4, 10, 128256, 0.0, "min"),     # C1 (fp32 Llama-3.2-1B vocab)
+    (torch.bfloat16, 16, 16, 50, 256000, 30.0, "min"),  # C3 (Gemma-2 vocab, soft-cap)
+    (torch.bfloat16, 64, 8, 32, 128256, 0.0, "min"),    # C5 (64 agents, beam 8, top-32)
+    (torch.bfloat16, 64, 40, 3, 4099, 0.0, "sum"),      # single-pass rows (A*B >= 2048)
+    (torch.float16, 5, 3, 7, 5003, 0.0, "sumlog"),      # odd vocab
+    (torch.bfloat16, 3, 1, 1, 777, 0.0, "max"),         # first step: one beam, one token
+]
+
+
+@pytest.mark.parametrize("dtype,A,B,K,vocab,softcap,kind", BEAM_CASES)
+def test_beam_step_matches_oracle_and_unfused_path(ops, orc, dev, dtype, A, B, K, vocab, softcap,
+                                                   kind):
+    g = torch.Generator().manual_seed(A * 131 + B * 7 + K)
+    logits = (torch.randn(A * B, vocab, generator=g) * 3.0).to(dtype)
+    tgt = torch.randint(0, vocab, (B, K), generator=g, dtype=torch.int32)
+    if B > 1 and K > 2:
+        tgt[1, K - 2:] = -1                  # a ragged beam: padded candidate slots
+    tgt[0, 0] = tgt[0, min(1, K - 1)]        # duplicate token in one beam
+    R = (-torch.rand(A, B, generator=g) * 20.0)
+    if kind == "sumlog":
+        R = torch.rand(A, B, generator=g) * 2.0 + 10.0   # positive utilities for the log
+    lg, tg, Rg = logits.to(dev), tgt.to(dev), R.to(dev)
+    U, W, order, oval = ops.beam_step(lg, tg, Rg, kind, softcap=softcap)
+    C = B * K
+
+    # 1) bit-identical to the unfused kernels on the same device inputs
+    tok, _ = ops.logsoftmax_gather(lg, tg.repeat(A, 1), softcap=softcap)
+    U2 = (Rg[:, :, None] + tok.view(A, B, K)).reshape(A, C)
+    W2 = ops.welfare(U2.contiguous(), kind)
+    o2, v2 = ops.topk(W2, C)
+    assert torch.equal(torch.nan_to_num(U, nan=7.0), torch.nan_to_num(U2, nan=7.0))
+    assert torch.equal(torch.nan_to_num(W, nan=7.0), torch.nan_to_num(W2, nan=7.0))
+    assert torch.equal(order, o2) and torch.equal(torch.nan_to_num(oval, nan=7.0),
+                                                  torch.nan_to_num(v2, nan=7.0))
+
+    # 2) the CPU oracle: per-agent log-probs within 1e-3, order bit-exact given the scores
+    host, bf16 = _host_logits(logits)
+    o_tok, _ = orc.logsoftmax_gather(np.ascontiguousarray(host), tgt.repeat(A, 1).numpy(),
+                                     softcap=softcap, bf16=bf16, vocab=vocab)
+    o_U = (R.double().numpy()[:, :, None] + o_tok.reshape(A, B, K)).reshape(A, C)
+    u = U.cpu().numpy()
+    assert np.array_equal(np.isnan(u), np.isnan(o_U))
+    assert np.nanmax(np.abs(u - o_U)) < LP_TOL
+    codes = {"min": orc.MIN, "sum": orc.SUM, "sumlog": orc.SUMLOG, "max": orc.MAX}
+    o_W = orc.welfare(o_U, codes[kind], eps=1e-9)
+    w = W.cpu().numpy()
+    tol = LP_TOL * (A if kind in ("sum",) else 1)
+    assert np.nanmax(np.abs(w - o_W)) < tol
+    assert np.array_equal(order.cpu().numpy(), orc.topk(w.astype(np.float64), C)[0])
+
+
+def test_beam_step_sort_skipped_for_sharded_runs(ops, dev):
+    A, B, K, V = 2, 4, 5, 3000
+    x = torch.randn(A * B, V, device=dev)
+    t = torch.randint(0, V, (B, K), device=dev, dtype=torch.int32)
+    R = torch.zeros(A, B, device=dev)
+    U, W, order, _ = ops.beam_step(x, t, R, "min", n_order=0)
+    assert order is None and U.shape == (A, B * K) and torch.isfinite(W).all()
+    with pytest.raises(ops.CSError):
+        ops.beam_step(x, t, torch.zeros(A, B + 1, device=dev), "min")

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""A/B timing of the beam-step pieces on resident logits (HIP events, GPU kept busy so the
+host never gaps the queue).  python tools/beam_ab.py"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+ops = importlib.import_module(
+    "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd.ops")
+import bench  # noqa: E402
+
+
+def timed(fn, n=40):
+    st = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    bench.gpu_busy(st, 10.0)
+    for a, b in ev:
+        a.record(st)
+        fn()
+        b.record(st)
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev])) * 1000.0
+
+
+def main():
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(0)
+    for name, (A, B, K, V, cap, dt) in {"c3": (16, 16, 50, 256000, 30.0, torch.bfloat16),
+                                         "c3nocap": (16, 16, 50, 256000, 0.0, torch.bfloat16),
+                                         "c5": (64, 8, 32, 128256, 0.0, torch.bfloat16)}.items():
+        g = torch.Generator(device=dev).manual_seed(1)
+        x = (torch.randn(A * B, V, generator=g, device=dev) * 3).to(dt)
+        ref = (torch.randn(B, V, generator=g, device=dev) * 3).to(dt)
+        t = torch.randint(0, V, (B, K), generator=g, device=dev, dtype=torch.int32)
+        R = torch.zeros(A, B, device=dev)
+        ws, wb = ops.Workspace(), ops.Workspace(zeroed=True)
+        r = {"config": name}
+        r["lsg_k0_us"] = timed(lambda: ops.logsoftmax_gather(x, None, softcap=cap, workspace=ws, want_lse=True))
+        r["lsg_kK_us"] = timed(lambda: ops.logsoftmax_gather(x, t.repeat(A, 1), softcap=cap, workspace=ws))
+        r["beam_sort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", softcap=cap, workspace=wb))
+        r["beam_nosort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", n_order=0, softcap=cap, workspace=wb))
+        r["vocab_topk_us"] = timed(lambda: ops.vocab_topk(ref, K, softcap=cap, workspace=ws))
+        r["bytes"] = A * B * V * 2
+        r["ideal_us"] = r["bytes"] / 8e12 * 1e6
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
