@@ -596,46 +596,183 @@ __device__ __forceinline__ void bitonic_desc(unsigned long long* ck, int n2, int
   }
 }
 
+// Top-k by histogram threshold (the fast path of both top-k kernels).  A block's keys are
+// binned on their top 12 bits (sign, exponent and 3 mantissa bits of the value); the
+// threshold bin t is the highest bin with count(bins > t) < k <= count(bins >= t), so
+// every key of the top k lies in bins >= t.  Those candidates (typically k plus a few
+// dozen) are ranked by counting in LDS: keys are distinct (the index is in the low word),
+// so rank = #{larger keys} and the order is exactly the full sort's.  A block whose
+// candidates overflow kTopkCand (massive ties: constant or masked rows) falls back to the
+// full bitonic sort, which gives the identical result.
+constexpr int kTopkBins = 4096;
+constexpr int kTopkCand = 1024;
+constexpr int kTopkPer = kTopkChunk / 256;   // keys per lane in the chunk kernel
+
+__device__ __forceinline__ uint32_t key_bin(unsigned long long key) {
+  return static_cast<uint32_t>(key >> 52);
+}
+
+// Threshold of a 256-thread block's histogram.  Lane i owns the 16 bins
+// [4080 - 16 i, 4095 - 16 i], scanned from the top; returns (t, count(bins >= t)) in every
+// thread, (0, total) when the block holds fewer than k keys.
+__device__ __forceinline__ int2 hist_threshold(const uint32_t* hist, uint32_t k, uint32_t* sm_w,
+                                               int* sm_res) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int top = kTopkBins - 1 - 16 * tid;
+  uint32_t c[16];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    c[j] = hist[top - j];
+    s += c[j];
+  }
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) sm_w[wave] = inc;
+  __syncthreads();
+  uint32_t before = inc - s, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if (w < wave) before += sm_w[w];
+    total += sm_w[w];
+  }
+  if (total < k) return make_int2(0, static_cast<int>(total));
+  if (before < k && before + s >= k) {
+    uint32_t acc = before;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (acc + c[j] >= k) {
+        sm_res[0] = top - j;
+        sm_res[1] = static_cast<int>(acc + c[j]);
+        break;
+      }
+      acc += c[j];
+    }
+  }
+  __syncthreads();
+  return make_int2(sm_res[0], sm_res[1]);
+}
+
+// Rank the nc distinct candidate keys in LDS; key of rank r < k goes to emit(r, key).
+template <typename Emit>
+__device__ __forceinline__ void rank_candidates(const unsigned long long* cand, int nc, int k,
+                                                Emit emit) {
+  for (int i = threadIdx.x; i < nc; i += 256) {
+    const unsigned long long kc = cand[i];
+    int r = 0;
+#pragma unroll 8
+    for (int j = 0; j < nc; ++j) r += cand[j] > kc ? 1 : 0;
+    if (r < k) emit(r, kc);
+  }
+}
+
+// One (row, 4096-element chunk) per workgroup: the chunk's k largest composite keys
+// (order key, ~token id), descending, zero-padded when the chunk holds fewer than k.
 template <int DT, bool CAP>
 __global__ __launch_bounds__(256) void vocab_topk_chunk_kernel(
     const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nchunk, int32_t k,
     float cap, float inv_cap, unsigned long long* __restrict__ part) {
-  __shared__ unsigned long long ck[kTopkChunk];
+  // 32 KB: histogram (16 KB) + candidates (8 KB), or the whole chunk for the fallback sort
+  __shared__ __attribute__((aligned(16))) unsigned long long lds[kTopkChunk];
+  __shared__ uint32_t sm_w[4];
+  __shared__ int sm_res[2];
+  __shared__ uint32_t sm_n;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
+  unsigned long long* cand = lds + kTopkBins / 2;
   const int tid = threadIdx.x;
   const int64_t row = blockIdx.x / nchunk;
   const int32_t chunk = static_cast<int32_t>(blockIdx.x - row * nchunk);
   const char* rp = logits + row * ld_bytes;
   const int64_t v0 = static_cast<int64_t>(chunk) * kTopkChunk;
-  const int64_t n = min(static_cast<int64_t>(kTopkChunk), vocab - v0);
-  for (int i = tid; i < kTopkChunk; i += 256) {
-    unsigned long long key = 0ull;
+  const int n = static_cast<int>(min(static_cast<int64_t>(kTopkChunk), vocab - v0));
+  unsigned long long key[kTopkPer];
+#pragma unroll
+  for (int j = 0; j < kTopkPer; ++j) {
+    const int i = tid + 256 * j;
+    float x = 0.0f;
+    if (i < n) x = load_any<DT>(rp, v0 + i);
+    key[j] = 0ull;
     if (i < n) {
-      float x = load_any<DT>(rp, v0 + i);
       if (CAP) x = softcap_fn(x, cap, inv_cap);
-      key = (static_cast<unsigned long long>(order_key(x)) << 32) |
-            static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + i));
+      key[j] = (static_cast<unsigned long long>(order_key(x)) << 32) |
+               static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + i));
     }
-    ck[i] = key;
   }
+  for (int i = tid; i < kTopkBins; i += 256) hist[i] = 0u;
+  if (tid == 0) sm_n = 0u;
   __syncthreads();
-  bitonic_desc(ck, kTopkChunk, tid, 256);
-  for (int r = tid; r < k; r += 256) part[(row * nchunk + chunk) * k + r] = ck[r];
+#pragma unroll
+  for (int j = 0; j < kTopkPer; ++j)
+    if (key[j]) atomicAdd(&hist[key_bin(key[j])], 1u);
+  __syncthreads();
+  const int2 th = hist_threshold(hist, static_cast<uint32_t>(k), sm_w, sm_res);
+  unsigned long long* out = part + (row * nchunk + chunk) * static_cast<int64_t>(k);
+  if (th.y <= kTopkCand) {  // block-uniform
+#pragma unroll
+    for (int j = 0; j < kTopkPer; ++j)
+      if (key[j] && key_bin(key[j]) >= static_cast<uint32_t>(th.x)) cand[atomicAdd(&sm_n, 1u)] = key[j];
+    __syncthreads();
+    const int nc = static_cast<int>(sm_n);
+    rank_candidates(cand, nc, k, [&](int r, unsigned long long kc) { out[r] = kc; });
+    for (int r = nc + tid; r < k; r += 256) out[r] = 0ull;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < kTopkPer; ++j) lds[tid + 256 * j] = key[j];
+  __syncthreads();
+  bitonic_desc(lds, kTopkChunk, tid, 256);
+  for (int r = tid; r < k; r += 256) out[r] = lds[r];
 }
 
+__device__ __forceinline__ void emit_token(int32_t* ids, float* vals, int64_t at,
+                                           unsigned long long c) {
+  ids[at] = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull));
+  if (vals) vals[at] = key_to_float(static_cast<uint32_t>(c >> 32));
+}
+
+// One row per workgroup: the k largest of the row's nkeys chunk winners (zero = padding).
+// Dynamic LDS: max(n2, 4096) keys (histogram + candidates, or the fallback sort).
 __global__ __launch_bounds__(256) void vocab_topk_merge_kernel(
     const unsigned long long* __restrict__ part, int32_t nkeys, int32_t n2, int32_t k,
     int32_t* __restrict__ out_ids, float* __restrict__ out_vals) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long mk[];
+  __shared__ uint32_t sm_w[4];
+  __shared__ int sm_res[2];
+  __shared__ uint32_t sm_n;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(mk);
+  unsigned long long* cand = mk + kTopkBins / 2;
   const int tid = threadIdx.x;
   const int64_t row = blockIdx.x;
-  for (int i = tid; i < n2; i += 256) mk[i] = (i < nkeys) ? part[row * nkeys + i] : 0ull;
+  const unsigned long long* pr = part + row * nkeys;
+  for (int i = tid; i < kTopkBins; i += 256) hist[i] = 0u;
+  if (tid == 0) sm_n = 0u;
+  __syncthreads();
+  for (int i = tid; i < nkeys; i += 256) {
+    const unsigned long long c = pr[i];
+    if (c) atomicAdd(&hist[key_bin(c)], 1u);
+  }
+  __syncthreads();
+  const int2 th = hist_threshold(hist, static_cast<uint32_t>(k), sm_w, sm_res);
+  if (th.y <= kTopkCand) {  // block-uniform
+    for (int i = tid; i < nkeys; i += 256) {
+      const unsigned long long c = pr[i];
+      if (c && key_bin(c) >= static_cast<uint32_t>(th.x)) cand[atomicAdd(&sm_n, 1u)] = c;
+    }
+    __syncthreads();
+    const int nc = static_cast<int>(sm_n);
+    rank_candidates(cand, nc, k,
+                    [&](int r, unsigned long long c) { emit_token(out_ids, out_vals, row * k + r, c); });
+    for (int r = nc + tid; r < k; r += 256) emit_token(out_ids, out_vals, row * k + r, 0ull);
+    return;
+  }
+  for (int i = tid; i < n2; i += 256) mk[i] = (i < nkeys) ? pr[i] : 0ull;
   __syncthreads();
   bitonic_desc(mk, n2, tid, 256);
-  for (int r = tid; r < k; r += 256) {
-    const unsigned long long c = mk[r];
-    out_ids[row * k + r] = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull));
-    if (out_vals) out_vals[row * k + r] = key_to_float(static_cast<uint32_t>(c >> 32));
-  }
+  for (int r = tid; r < k; r += 256) emit_token(out_ids, out_vals, row * k + r, mk[r]);
 }
 
 // Counter-based uniform strictly inside (0, 1): splitmix64 finaliser of (seed, token), top
@@ -990,21 +1127,18 @@ __global__ __launch_bounds__(BLOCK) void beam_step_kernel(
   }
   if (!sort_here) return;  // block-uniform
   __syncthreads();
-  for (int32_t c = tid; c < C; c += BLOCK)
-    keys[c] = (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
-              static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c));
+  for (int32_t c = tid; c < n2; c += BLOCK)
+    keys[c] = c < C ? (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
+                          static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c))
+                    : 0ull;
   __syncthreads();
-  // rank of each candidate among all C (keys are distinct: the index is in the low word):
-  // barrier-free, every lane reads the same key at once (LDS broadcast)
-  for (int32_t c = tid; c < C; c += BLOCK) {
-    const unsigned long long kc = keys[c];
-    int32_t r = 0;
-#pragma unroll 8
-    for (int32_t j = 0; j < C; ++j) r += keys[j] > kc ? 1 : 0;
-    if (r < n_order) {
-      out_order[r] = c;
-      if (out_val) out_val[r] = sm_w[c];
-    }
+  // bitonic sort in LDS: log2(n2)(log2(n2)+1)/2 barrier-separated passes, n2/2 compare-
+  // exchanges each (keys are distinct: the index is in the low word)
+  bitonic_desc(keys, n2, tid, BLOCK);
+  for (int32_t r = tid; r < n_order; r += BLOCK) {
+    const int32_t c = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(keys[r] & 0xffffffffull));
+    out_order[r] = c;
+    if (out_val) out_val[r] = sm_w[c];
   }
 }
 
@@ -1270,8 +1404,9 @@ int cs_vocab_topk(const void* logits, int dtype, int64_t rows, int64_t vocab, in
 #undef CS_TOPK_LAUNCH
   int32_t n2 = 2;
   while (n2 < nkeys) n2 <<= 1;
+  const int32_t lds_keys = n2 > kTopkChunk ? n2 : kTopkChunk;
   hipLaunchKernelGGL(vocab_topk_merge_kernel, dim3(static_cast<uint32_t>(rows)), dim3(256),
-                     static_cast<size_t>(n2) * sizeof(unsigned long long), st, part,
+                     static_cast<size_t>(lds_keys) * sizeof(unsigned long long), st, part,
                      static_cast<int32_t>(nkeys), n2, k, out_ids, out_vals);
   return check_launch("cs_vocab_topk");
 }

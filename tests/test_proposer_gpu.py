@@ -33,6 +33,43 @@ def test_vocab_topk_matches_oracle(ops, orc, dev, dtype, rows, vocab, k, softcap
         np.testing.assert_array_equal(vals.cpu().numpy(), o_vals.astype(np.float32))
 
 
+@pytest.mark.parametrize("case", ["constant", "masked", "nan", "chunk_ties", "gemma_c3"])
+def test_vocab_topk_edge_rows(ops, orc, dev, case):
+    """Rows that defeat the histogram threshold (massive ties -> full-sort fallback) or
+    carry -inf / NaN, and ties straddling the 4096-element chunk boundaries."""
+    g = torch.Generator().manual_seed(7)
+    rows, V, k, cap = 3, 20000, 40, 0.0
+    x = torch.randn(rows, V, generator=g) * 3.0
+    if case == "constant":
+        x[:] = 1.25
+        x[1, 5000:9000] = 0.0             # a row whose chunks are partly constant
+    elif case == "masked":
+        x[:, 100:] = float("-inf")        # logit-bias mask: fewer finite values than k
+        x[2] = float("-inf")
+    elif case == "nan":
+        x[0, ::3] = float("nan")
+        x[1, :] = float("nan")
+        x[1, 17] = 2.0
+    elif case == "chunk_ties":
+        x[:] = -5.0
+        for c in (4095, 4096, 8191, 8192, 12287, 19999):
+            x[:, c] = 7.0
+    elif case == "gemma_c3":
+        rows, V, k, cap = 16, 256000, 50, 30.0
+        x = torch.randn(rows, V, generator=g) * 3.0
+    xd = x.to(torch.bfloat16 if case == "gemma_c3" else torch.float32)
+    ids, vals = ops.vocab_topk(xd.to(dev), k, softcap=cap)
+    xf = xd.float()
+    if cap:
+        xf = cap * torch.tanh(xf / cap)
+    o_ids, o_vals = orc.vocab_topk(xf.double().numpy(), k)
+    if cap:   # fp32 tanh of the kernel vs torch: compare value multisets, then ids by value
+        np.testing.assert_allclose(vals.cpu().numpy(), o_vals, atol=1e-5)
+    else:
+        assert np.array_equal(ids.cpu().numpy(), o_ids)
+        np.testing.assert_array_equal(vals.cpu().numpy(), o_vals.astype(np.float32))
+
+
 def test_vocab_sample_matches_oracle(ops, orc, dev):
     rng = np.random.default_rng(12)
     rows, V, n_draw = 6, 50000, 8

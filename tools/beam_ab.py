@@ -33,7 +33,8 @@ def timed(fn, n=40):
 def main():
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
-    for name, (A, B, K, V, cap, dt) in {"c3": (16, 16, 50, 256000, 30.0, torch.bfloat16),
+    for name, (A, B, K, V, cap, dt) in {"c1": (4, 4, 10, 128256, 0.0, torch.float32),
+                                         "c3": (16, 16, 50, 256000, 30.0, torch.bfloat16),
                                          "c3nocap": (16, 16, 50, 256000, 0.0, torch.bfloat16),
                                          "c5": (64, 8, 32, 128256, 0.0, torch.bfloat16)}.items():
         g = torch.Generator(device=dev).manual_seed(1)
@@ -48,7 +49,7 @@ def main():
         r["beam_sort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", softcap=cap, workspace=wb))
         r["beam_nosort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", n_order=0, softcap=cap, workspace=wb))
         r["vocab_topk_us"] = timed(lambda: ops.vocab_topk(ref, K, softcap=cap, workspace=ws))
-        r["bytes"] = A * B * V * 2
+        r["bytes"] = A * B * V * x.element_size()
         r["ideal_us"] = r["bytes"] / 8e12 * 1e6
         print(json.dumps(r), flush=True)
 
