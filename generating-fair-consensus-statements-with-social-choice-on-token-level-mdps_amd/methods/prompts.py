@@ -62,6 +62,23 @@ FL = dict(
     stop_tokens=["\n", "\n\n", ".\n\n"],   # finite_lookahead.py:141-144
 )
 
+# src/methods/mcts.py:62-91 (its own, shorter system texts and EOS set)
+MCTS = dict(
+    eos_tokens=frozenset({"<|eot_id|>", "<|end_of_text|>", ".\n\n", ".\n", "\n\n", '."\n\n'}),
+    ref_system=("You are generating a consensus statement that represents the views of multiple "
+                "participants.\nYour task is to continue the statement in a way that addresses the "
+                "issue and considers all participants' opinions. Be concise and coherent. ONLY WRITE "
+                "THE CONSENSUS STATEMENT AND NOTHING ELSE."),
+    agent_system=("You are generating a statement that represents the views of a single "
+                  "participant.\nYour task is to continue the statement in a way that addresses "
+                  "the issue and considers ONLY this participant's opinion. Be concise and "
+                  "coherent. ONLY WRITE THE CONSENSUS STATEMENT AND NOTHING ELSE."),
+    ref_user="Issue:\n{issue}\n\nParticipants' opinions:\n{opinions_text}\n\nConsensus statement:\n",
+    agent_user="Issue:\n{issue}\n\nParticipant's opinion:\n{opinion}\n\n"
+               "Statement reflecting ONLY this participant's opinion:\n",
+    failure_reward=-100.0,     # mcts.py:497, 566, 650 (failed evaluation / empty rollout)
+)
+
 # src/evaluation.py:182-186
 EVAL_SYSTEM = ("Issue: {issue}. Agent's Opinion: {opinion}. Here is a consensus statement that "
                "perfectly aligns with the agent's opinion:")

@@ -135,6 +135,52 @@ def text_compat_mean(model, system_prompt, user_prompt):
     return sum(vals) / len(vals), sum(_m.exp(v) for v in vals) / len(vals), len(vals)
 
 
+@torch.no_grad()
+def user_span_sums(model, systems: Sequence[Optional[str]], users: Sequence[str],
+                   *, device_out: bool = False):
+    """``sum(get_prompt_logprobs(model, systems[i], users[i])[1])`` for every i, batched.
+
+    The reference calls get_prompt_logprobs once per (agent, text) and sums the user-span
+    log-probs (src/methods/mcts.py:270-320, 343-368).  Here every pair whose user span is
+    where the reference's ``find`` lands (span_found_at_user) is scored in ONE engine pass
+    (prefill of the distinct chat prefixes, one logits block, cs_logsoftmax_gather,
+    cs_segment_reduce); the rest take the text-compat path.  Returns a float64 tensor
+    [n] (on the device when ``device_out`` and every pair took the batched path) with NaN
+    where the reference's call yields no usable log-probs (empty span, a None entry).
+    """
+    engine, tok = runtime.get_engine(model)
+    n = len(users)
+    out = torch.full((n,), float("nan"), dtype=torch.float64)
+    fast = [i for i in range(n) if users[i] and span_found_at_user(tok, systems[i], users[i])]
+    fast_set = set(fast)
+    if fast:
+        keys, owner, uniq = {}, [], []
+        for i in fast:
+            s = systems[i] or None
+            if s not in keys:
+                keys[s] = len(uniq)
+                uniq.append(tok.chat_prefix(s, ""))
+            owner.append(keys[s])
+        conts = [tok.encode(users[i]) for i in fast]
+        cache = engine.prefill(uniq)
+        lp = engine.score(cache, owner, conts)
+        seg = ops.segment_reduce(lp, engine.offsets(conts, engine.device))
+        ok = seg["count"] == torch.as_tensor([len(c) for c in conts], dtype=torch.int32,
+                                             device=engine.device)
+        sums = torch.where(ok & (seg["count"] > 0), seg["sum_lp"].double(),
+                           torch.full_like(seg["sum_lp"], float("nan"), dtype=torch.float64))
+        if device_out and len(fast) == n:
+            return sums
+        out[torch.as_tensor(fast)] = sums.cpu()
+    for i in range(n):
+        if i in fast_set or not users[i]:
+            continue
+        _, lps = get_prompt_logprobs(model, systems[i], users[i])
+        if lps and all(v is not None for v in lps):
+            out[i] = float(sum(lps))
+    return out.to(engine.device) if device_out else out
+
+
 def get_token_ids(model, text) -> Dict[str, int]:
     """{token string: id} of the chat-rendered single-message prompt (src/utils.py:466-525)."""
     try:

@@ -79,7 +79,7 @@ def main() -> None:
     issue, opinions = scen["issue"], dict(scen["agent_opinions"])
 
     from src import utils as rutils                      # noqa: E402  (reference)
-    from src.methods import beam_search, best_of_n, finite_lookahead  # noqa: E402
+    from src.methods import beam_search, best_of_n, finite_lookahead, mcts  # noqa: E402
     from src.methods import get_method_generator         # noqa: E402
 
     calls = []
@@ -92,7 +92,11 @@ def main() -> None:
             return toks, lps
         return wrapped
 
-    for mod in (beam_search, best_of_n, finite_lookahead):
+    # mcts.py:615 formats `final_statement` (commented out at :593) in a debug f-string,
+    # so every non-empty rollout raises NameError; bind the name in the module globals so
+    # the reference's search runs to completion (its evident intent; see methods/mcts.py)
+    mcts.final_statement = ""
+    for mod in (beam_search, best_of_n, finite_lookahead, mcts):
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
@@ -107,6 +111,12 @@ def main() -> None:
                          "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
         ("beam_search", {"beam_width": 3, "max_tokens": 6, "max_sampling_attempts": 5, "seed": 5,
                          "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+        ("mcts", {"num_simulations": 5, "max_tokens": 4, "expansion_sample_width": 2,
+                  "max_sampling_attempts": 6, "rollout_depth": 5, "gamma": 0.99, "seed": 13,
+                  "exploration_constant": 1.414, "api_delay": 0, "log_level": "WARNING"}),
+        ("mcts", {"num_simulations": 4, "max_tokens": 3, "expansion_sample_width": 3,
+                  "max_sampling_attempts": 20, "rollout_depth": 3, "gamma": 0.5, "seed": 2,
+                  "api_delay": 0, "log_level": "WARNING"}),
     ]
     for method, mcfg in runs:
         calls.clear()
@@ -130,6 +140,17 @@ def main() -> None:
 
             gen._calculate_candidate_rewards = rec_rewards
             gen._calculate_egalitarian_welfare = rec_welfare
+        if method == "mcts":
+            extra["steps"] = []
+            orig_best = gen._select_best_child
+
+            def rec_best(node):
+                b = orig_best(node)
+                extra["steps"].append({"visits": {t: c.visits for t, c in node.children.items()},
+                                       "chosen": None if b is None else b.token})
+                return b
+
+            gen._select_best_child = rec_best
         stmt = gen.generate_statement(issue, opinions)
         out["runs"].append({"method": method, "config": mcfg, "statement": stmt,
                             "pre_brushup": getattr(gen, "pre_brushup_statement", None),

@@ -5,7 +5,8 @@ Replays every run recorded in tests/golden/method_traces.json (produced by the
 reference's own generators, see make_method_traces.py) through the product's
 generators on the same seeded fixture model, and compares:
   * final statements (exact), BoN candidates (exact), BoN agent rewards and welfare
-    (1e-3 abs, north_star tolerance);
+    (1e-3 abs, north_star tolerance), MCTS root-child visit counts and chosen token of
+    every step (exact);
   * StatementEvaluator log-prob metrics (1e-3 abs on log-probs, 1e-3 rel on welfare);
   * get_prompt_logprobs tokens (exact) and log-probs (1e-3 abs).
 """
@@ -73,6 +74,8 @@ def check_methods(traces):
             d = max(abs(a - b) for a, b in zip(gen.last_welfare, run["welfare"]))
             if d > TOL:
                 failures.append(f"{tag}: welfare differs by {d}")
+        if run["method"] == "mcts" and gen.trace != run["steps"]:
+            failures.append(f"{tag}: search steps {gen.trace} != reference {run['steps']}")
         if stmt != run["statement"]:
             failures.append(f"{tag}: statement {stmt!r} != reference {run['statement']!r}")
     return failures

@@ -43,3 +43,14 @@ def test_evaluator_matches_reference(emulated):
 def test_prompt_logprobs_match_reference(emulated):
     failures = mp.check_prompt_logprobs(emulated)
     assert not failures, "\n".join(failures)
+
+
+def test_mcts_strict_mode_raises_the_reference_nameerror(emulated):
+    """reference_rollout_nameerror reproduces mcts.py:615 (undefined name in the rollout's
+    debug f-string): the first non-empty rollout raises NameError."""
+    methods = importlib.import_module(PKG + ".methods")
+    cfg = {"num_simulations": 2, "max_tokens": 2, "expansion_sample_width": 2, "rollout_depth": 3,
+           "seed": 13, "reference_rollout_nameerror": True}
+    gen = methods.get_method_generator("mcts", cfg, emulated["model_id"])
+    with pytest.raises(NameError, match="final_statement"):
+        gen.generate_statement(emulated["issue"], dict(emulated["agent_opinions"]))
