@@ -212,6 +212,9 @@ def run_beam(name, world, rank, dev, steps, warmup):
       agent rows [A_local*B, V]   --cs_beam_step-->     U = R + lp, W = min over agents
       [RCCL MIN all-reduce of W when the agents are sharded] --> stable order (top-k)
       cumulative rewards of the B kept beams  R <- U[:, order[:B]]
+    (the reference's walk over the sorted candidates, beam_search.py:562-600, keeps the
+    first beam_width; synthetic candidates have no duplicates / EOS, so the B best are
+    exactly what it keeps, and the launch selects just those)
     At N = 1 the whole step is one captured hipGraph; with agents sharded, the per-rank
     parts are two graphs around the eager all-reduce.
     """
@@ -233,7 +236,9 @@ def run_beam(name, world, rank, dev, steps, warmup):
         if A_loc == 0:   # more ranks than agents: this rank only proposes
             return (torch.empty(0, C, device=dev),
                     torch.full((C,), float("inf"), device=dev), None)
-        U, W, order, _ = ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else C,
+        # keep = the B best candidates: the launch selects them (threshold + rank, no
+        # full sort); sharded runs all-reduce W first and select afterwards
+        U, W, order, _ = ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else B,
                                        softcap=cap, workspace=ws_b)
         return U, W, order
 
@@ -242,7 +247,7 @@ def run_beam(name, world, rank, dev, steps, warmup):
 
     def select(U, W):
         W = torch.where(torch.isinf(W) & (W > 0), torch.full_like(W, float("nan")), W)
-        order, _ = ops.topk(W, C)
+        order, _ = ops.topk(W, B)
         keep(U, order)
 
     s = torch.cuda.Stream(device=dev)
@@ -299,7 +304,7 @@ def run_beam(name, world, rank, dev, steps, warmup):
     for e0, e1 in ev:
         e0.record(st)
         if A_loc:
-            ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else C, softcap=cap,
+            ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else B, softcap=cap,
                           workspace=ws_b)
         e1.record(st)
     torch.cuda.synchronize()

@@ -111,14 +111,21 @@ __device__ __forceinline__ float load_one(const char* row, int64_t i) {
   }
 }
 
-// Gemma-2 final-logit soft-capping, cap * tanh(x / cap), with tanh written through
-// one exp2 so the vocab stream and the target gather use the identical function.
-// tanh(z) = 1 - 2 / (exp(2z) + 1) with the hardware reciprocal (1 ulp): two
-// transcendental ops per element; |error| ~ 1e-6 * cap, far inside the 1e-3 budget.
+// Gemma-2 final-logit soft-capping, cap * tanh(x / cap), written through one exp2 and
+// the hardware reciprocal (1 ulp) so the vocab stream and the target gather use the
+// identical function:  r = 1 / (exp(2x/cap) + 1),  cap * tanh(x/cap) = cap - 2 cap r.
+// |error| ~ 1e-6 * cap, far inside the 1e-3 budget.  The constant 2 log2(e) / cap is
+// formed once per kernel (loop-invariant), so an element costs mul, exp2, add, rcp, fma.
+__device__ __forceinline__ float softcap_rcp(float x, float inv_cap) {
+  return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x * ((2.0f * kLog2e) * inv_cap)) + 1.0f);
+}
 __device__ __forceinline__ float softcap_fn(float x, float cap, float inv_cap) {
-  const float e = __builtin_amdgcn_exp2f(x * (2.0f * kLog2e) * inv_cap);  // exp(2x/cap); inf ok
-  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
-  return cap * t;
+  return fmaf(-2.0f * cap, softcap_rcp(x, inv_cap), cap);
+}
+// exp(cap * tanh(x / cap)) for the fixed-offset sum, straight from the reciprocal:
+// exp2(cap log2e - 2 cap log2e r), one fma instead of rebuilding x' and scaling it.
+__device__ __forceinline__ float softcap_exp(float x, float cap, float inv_cap) {
+  return __builtin_amdgcn_exp2f(fmaf((-2.0f * kLog2e) * cap, softcap_rcp(x, inv_cap), kLog2e * cap));
 }
 
 // ---------------------------------------------------------------------------
@@ -155,6 +162,24 @@ __device__ __forceinline__ void lse_accum(float& m, float& s, const float* v) {
   for (int i = 0; i < N; ++i) acc += __builtin_amdgcn_exp2f(fmaf(v[i], kLog2e, -off));
   s = fmaf(s, __builtin_amdgcn_exp2f(fmaf(m, kLog2e, -off)), acc);
   m = mn;
+}
+
+// N raw elements into (m, s): soft-capped first when CAP; with FIXED (bounded capped
+// logits) the sum needs no running max and takes softcap_exp directly.
+template <int N, bool CAP, bool FIXED>
+__device__ __forceinline__ void accum_elems(float& m, float& s, float* v, float cap, float inv_cap) {
+  if constexpr (CAP && FIXED) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc += softcap_exp(v[i], cap, inv_cap);
+    s += acc;
+  } else {
+    if constexpr (CAP) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = softcap_fn(v[i], cap, inv_cap);
+    }
+    lse_accum<N, FIXED>(m, s, v);
+  }
 }
 
 __device__ __forceinline__ void wave_lse_reduce(float& m, float& s) {
@@ -214,14 +239,22 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
   const int64_t tail0 = head + nvec * EPV;
   {
     float x = -INFINITY;
+    bool have = false;
     if (tid < head) {
       x = load_one<DT>(rp, v0 + tid);
-      if (CAP) x = softcap_fn(x, cap, inv_cap);
+      have = true;
     } else if (tid >= 64 && tid - 64 < n - tail0) {
       x = load_one<DT>(rp, v0 + tail0 + (tid - 64));
-      if (CAP) x = softcap_fn(x, cap, inv_cap);
+      have = true;
     }
-    if (x != -INFINITY) lse_accum<1, FIXED>(m, s, &x);
+    if (have) {
+      if constexpr (CAP && FIXED) {
+        s += softcap_exp(x, cap, inv_cap);
+      } else {
+        if (CAP) x = softcap_fn(x, cap, inv_cap);
+        if (x != -INFINITY) lse_accum<1, FIXED>(m, s, &x);
+      }
+    }
   }
 
   const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
@@ -234,21 +267,13 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
     float v[UNROLL * EPV];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
-    if (CAP) {
-#pragma unroll
-      for (int e = 0; e < UNROLL * EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-    }
-    lse_accum<UNROLL * EPV, FIXED>(m, s, v);
+    accum_elems<UNROLL * EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
   }
   for (; i < nvec; i += BLOCK) {
     const u32x4 q = __builtin_nontemporal_load(vp + i);
     float v[EPV];
     unpack_vec<DT>(q, v);
-    if (CAP) {
-#pragma unroll
-      for (int e = 0; e < EPV; ++e) v[e] = softcap_fn(v[e], cap, inv_cap);
-    }
-    lse_accum<EPV, FIXED>(m, s, v);
+    accum_elems<EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
   }
 
   wave_lse_reduce(m, s);
@@ -543,6 +568,14 @@ void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_byte
       launch_stream<DT, CAP, kBlock, kUnroll>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
                                               inv_cap, out_tok, out_lse, part, st);
       break;
+    case 6:
+      launch_stream<DT, CAP, 1024, 4>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
+                                      out_tok, out_lse, part, st);
+      break;
+    case 7:
+      launch_stream<DT, CAP, 512, 8>(logits, items, vocab, ld_bytes, plan, tgt, k, cap, inv_cap,
+                                     out_tok, out_lse, part, st);
+      break;
     default:
       if (plan.nsplit == 1)
         launch_stream<DT, CAP, 1024, 2>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
@@ -612,17 +645,21 @@ __device__ __forceinline__ uint32_t key_bin(unsigned long long key) {
   return static_cast<uint32_t>(key >> 52);
 }
 
-// Threshold of a 256-thread block's histogram.  Lane i owns the 16 bins
-// [4080 - 16 i, 4095 - 16 i], scanned from the top; returns (t, count(bins >= t)) in every
-// thread, (0, total) when the block holds fewer than k keys.
+// Threshold of an NT-thread block's histogram.  Thread i owns the kTopkBins / NT bins
+// just below bin 4095 - i * (kTopkBins / NT), scanned from the top; returns
+// (t, count(bins >= t)) in every thread, (0, total) when the block holds fewer than k
+// keys.  sm_w holds NT / 64 wave totals.
+template <int NT = 256>
 __device__ __forceinline__ int2 hist_threshold(const uint32_t* hist, uint32_t k, uint32_t* sm_w,
                                                int* sm_res) {
+  constexpr int PER = kTopkBins / NT;
+  constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int top = kTopkBins - 1 - 16 * tid;
-  uint32_t c[16];
+  const int top = kTopkBins - 1 - PER * tid;
+  uint32_t c[PER];
   uint32_t s = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < PER; ++j) {
     c[j] = hist[top - j];
     s += c[j];
   }
@@ -636,7 +673,7 @@ __device__ __forceinline__ int2 hist_threshold(const uint32_t* hist, uint32_t k,
   __syncthreads();
   uint32_t before = inc - s, total = 0;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < NW; ++w) {
     if (w < wave) before += sm_w[w];
     total += sm_w[w];
   }
@@ -644,7 +681,7 @@ __device__ __forceinline__ int2 hist_threshold(const uint32_t* hist, uint32_t k,
   if (before < k && before + s >= k) {
     uint32_t acc = before;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < PER; ++j) {
       if (acc + c[j] >= k) {
         sm_res[0] = top - j;
         sm_res[1] = static_cast<int>(acc + c[j]);
@@ -658,10 +695,10 @@ __device__ __forceinline__ int2 hist_threshold(const uint32_t* hist, uint32_t k,
 }
 
 // Rank the nc distinct candidate keys in LDS; key of rank r < k goes to emit(r, key).
-template <typename Emit>
+template <int NT = 256, typename Emit>
 __device__ __forceinline__ void rank_candidates(const unsigned long long* cand, int nc, int k,
                                                 Emit emit) {
-  for (int i = threadIdx.x; i < nc; i += 256) {
+  for (int i = threadIdx.x; i < nc; i += NT) {
     const unsigned long long kc = cand[i];
     int r = 0;
 #pragma unroll 8
@@ -921,10 +958,15 @@ int32_t topk_nchunk(int64_t vocab) {
 //      partials in split order (one wave, lanes over splits: lsg_merge_kernel's
 //      arithmetic), gathers the row's K candidate tokens and writes
 //      U[a, b*K+j] = R[a, b] + lp (fp32, the method's cumulative reward);
-//   3. the LAST row to finish (one more counter) folds the welfare of every candidate
-//      over the agents in agent order in fp64 (welfare_kernel's fold, non-finite
-//      skipped) and, when B*K <= kFusedSort, sorts the (value desc, index asc) keys in
-//      LDS (topk_kernel's keys).
+//   3. MIN / MAX welfare is order-free, so each row finisher also folds its K
+//      utilities into a per-candidate key with one device-scope atomicMax (ordered
+//      float keys; MIN stores inverted keys), and the LAST row to finish (one more
+//      counter) only reads the C keys back.  SUM / SUMLOG (order matters in fp64) are
+//      folded by the last row over the agents in agent order (welfare_kernel's fold,
+//      non-finite skipped).  When B*K <= kFusedSort the last row then sorts the
+//      (value desc, index asc) keys in LDS (topk_kernel's keys).
+//   The candidate ids and their logits are loaded before the stream starts, so the
+//   gather costs no memory round trip after the row's lse is known.
 // Bit-identical to cs_logsoftmax_gather + cs_welfare_reduce + cs_segmented_topk.
 // Hand-offs use sc1 stores / loads and arrival counters (no fences, see st_sc1).
 // Nobody waits on anybody, so the launch cannot stall; the last arrivers reset the
@@ -952,9 +994,35 @@ __device__ __forceinline__ uint32_t arrive(uint32_t* cnt) {
   return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Phase timestamps of cs_beam_step's last workgroup (diagnostics build only:
+// hipcc -DCS_TRACE_BEAM, tools/beam_trace.py); compiled out of the library.
+#ifdef CS_TRACE_BEAM
+__device__ unsigned long long g_trace_start = ~0ull;
+#define CS_TSTAMP(v) const unsigned long long v = wall_clock64()
+#else
+#define CS_TSTAMP(v)
+#endif
+
 constexpr int kFusedSort = 1024;      // candidates sorted inside the launch
+constexpr int kSelectMax = 256;       // n_order up to this: threshold selection, no full sort
 constexpr int kBeamMaxRows = 65536;   // A * B (one arrival counter per row)
-constexpr size_t kBeamCounterBytes = 64 + sizeof(uint32_t) * kBeamMaxRows;
+constexpr int kBeamMaxCand = 16384;   // B * K (one welfare key per candidate)
+// workspace: [done counter | pad to 64 B][row counters][welfare keys][row partials]
+constexpr size_t kBeamRowCntOff = 64;
+constexpr size_t kBeamKeyOff = kBeamRowCntOff + sizeof(uint32_t) * kBeamMaxRows;
+constexpr size_t kBeamCounterBytes = kBeamKeyOff + sizeof(uint32_t) * kBeamMaxCand;
+
+// Welfare key of one utility for the atomic MIN / MAX fold: 0 = no finite value yet (the
+// zeroed workspace state); order_key of a finite float is >= 0x00800000, so MAX keeps
+// order_key(u) and MIN keeps ~order_key(u) (the largest inverted key is the minimum).
+__device__ __forceinline__ uint32_t welfare_key(float u, bool is_min) {
+  const uint32_t k = order_key(u);
+  return is_min ? ~k : k;
+}
+__device__ __forceinline__ float welfare_from_key(uint32_t k, bool is_min) {
+  if (k == 0u) return __builtin_nanf("");
+  return key_to_float(is_min ? ~k : k);
+}
 
 __device__ __forceinline__ void welfare_fold(double& acc, bool& any, float u, int kind,
                                              double eps) {
@@ -1007,20 +1075,90 @@ __device__ __forceinline__ void fold_candidates(uint32_t* U, int32_t A, int32_t 
   }
 }
 
+// Descending bitonic sort of n2 (a power of two <= KPT * BLOCK) distinct keys held in
+// registers: element i = r * BLOCK + tid lives in kv[r] of thread tid.  Exchanges at
+// stride < 64 go through wave shuffles (no barrier), at stride >= BLOCK between the
+// thread's own registers, and only the strides in between through LDS, double-buffered
+// so that each such pass costs one barrier.  For n2 = 1024 on 1024 threads: 10 LDS
+// passes of the 55 instead of 55 barrier-separated LDS passes.
+__device__ __forceinline__ unsigned long long bitonic_pick(unsigned long long a,
+                                                           unsigned long long b, int i, int stride,
+                                                           int size) {
+  const bool keep_max = ((i & stride) == 0) == ((i & size) == 0);
+  return keep_max ? (a > b ? a : b) : (a < b ? a : b);
+}
+
+template <int BLOCK, int KPT>
+__device__ __forceinline__ void bitonic_desc_regs(unsigned long long (&kv)[KPT], int n2,
+                                                  unsigned long long* buf0,
+                                                  unsigned long long* buf1) {
+  const int tid = threadIdx.x;
+  bool flip = false;
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= BLOCK) {
+        const int rs = stride / BLOCK;
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+          if ((r & rs) == 0 && (r | rs) < KPT) {
+            const int i = r * BLOCK + tid;
+            if (i < n2) {
+              const unsigned long long a = kv[r], b = kv[r | rs];
+              const bool desc = (i & size) == 0;
+              if ((a < b) == desc) {
+                kv[r] = b;
+                kv[r | rs] = a;
+              }
+            }
+          }
+        }
+      } else if (stride >= 64) {
+        unsigned long long* buf = flip ? buf1 : buf0;
+        flip = !flip;
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+          const int i = r * BLOCK + tid;
+          if (i < n2) buf[i] = kv[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+          const int i = r * BLOCK + tid;
+          if (i < n2) kv[r] = bitonic_pick(kv[r], buf[i ^ stride], i, stride, size);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+          const int i = r * BLOCK + tid;
+          const unsigned long long b = __shfl_xor(kv[r], stride, 64);
+          if (i < n2) kv[r] = bitonic_pick(kv[r], b, i, stride, size);
+        }
+      }
+    }
+  }
+}
+
 template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
-__global__ __launch_bounds__(BLOCK) void beam_step_kernel(
+__global__ __launch_bounds__(BLOCK, 2) void beam_step_kernel(
     const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nsplit,
     int64_t split_len, int32_t A, int32_t B, int32_t K, const int32_t* __restrict__ tgt,
     const float* __restrict__ R, float cap, float inv_cap, int kind, double eps,
     unsigned long long* __restrict__ part, uint32_t* __restrict__ row_cnt,
-    uint32_t* __restrict__ done_cnt, float* __restrict__ U, float* __restrict__ W,
-    int32_t n_order, int32_t n2, int32_t* __restrict__ out_order, float* __restrict__ out_val) {
+    uint32_t* __restrict__ done_cnt, uint32_t* __restrict__ wkey, float* __restrict__ U,
+    float* __restrict__ W, int32_t n_order, int32_t n2, int32_t* __restrict__ out_order,
+    float* __restrict__ out_val) {
   __shared__ float sm_m[BLOCK / 64];
   __shared__ float sm_s[BLOCK / 64];
   __shared__ float sm_lse;
   __shared__ int sm_last;
-  __shared__ __attribute__((aligned(16))) unsigned long long keys[kFusedSort];
+  // keys2 directly after keys: the selection path uses the pair as one 16 KB histogram
+  __shared__ __attribute__((aligned(16))) unsigned long long keys[2 * kFusedSort];
+  unsigned long long* keys2 = keys + kFusedSort;
+  __shared__ __attribute__((aligned(16))) unsigned long long sel_cand[kTopkCand];
   __shared__ float sm_w[kFusedSort];
+  __shared__ uint32_t sm_tw[BLOCK / 64];
+  __shared__ int sm_res[2];
+  __shared__ uint32_t sm_n;
   const int tid = threadIdx.x;
   const int32_t rows = A * B;
   const int32_t C = B * K;
@@ -1033,14 +1171,23 @@ __global__ __launch_bounds__(BLOCK) void beam_step_kernel(
   const int64_t v0 = static_cast<int64_t>(split) * split_len;
   const int64_t v1 = min(vocab, v0 + split_len);
   uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
-  // the candidate ids are read now (not used before the row finish), so the finisher's
-  // logit gather does not wait on a dependent id load
+  CS_TSTAMP(t0);
+#ifdef CS_TRACE_BEAM
+  if (threadIdx.x == 0) atomicMin(&g_trace_start, t0);
+#endif
+  const bool order_free = kind == CS_WELFARE_MIN || kind == CS_WELFARE_MAX;
+  const bool is_min = kind == CS_WELFARE_MIN;
+  // the candidate ids and their logits are read now (used only at the row finish), so
+  // the finisher's gather costs no memory round trip after the lse is known
   const int32_t t_pre = (tid < K) ? tgt[bm * K + tid] : -1;
+  const bool ok = t_pre >= 0 && t_pre < vocab;
+  const float xg = ok ? load_one<DT>(rp, t_pre) : 0.0f;
 
   // 1. stream
   const float2 ms =
       block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
 
+  CS_TSTAMP(t1);
   // 2. row finish by the row's last arriver
   if (nsplit > 1) {
     if (tid == 0) {
@@ -1068,10 +1215,6 @@ __global__ __launch_bounds__(BLOCK) void beam_step_kernel(
     sm_lse = ms.x + logf(ms.y);
   }
   {
-    // gather (issued before the barrier that publishes the lse)
-    float xg = 0.0f;
-    const bool ok = t_pre >= 0 && t_pre < vocab;
-    if (ok) xg = load_one<DT>(rp, t_pre);
     __syncthreads();
     const float r0 = R[row];
     const float lse = sm_lse;
@@ -1088,10 +1231,15 @@ __global__ __launch_bounds__(BLOCK) void beam_step_kernel(
         if (CAP) x = softcap_fn(x, cap, inv_cap);
         lp = x - lse;
       }
-      st_sc1(Uw + static_cast<int64_t>(ag) * C + bm * K + j, __float_as_uint(r0 + lp));
+      const float u = r0 + lp;
+      st_sc1(Uw + static_cast<int64_t>(ag) * C + bm * K + j, __float_as_uint(u));
+      if (order_free && __builtin_isfinite(u))
+        __hip_atomic_fetch_max(wkey + bm * K + j, welfare_key(u, is_min), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
+  CS_TSTAMP(t2);
   // 3. welfare + order by the last row
   wait_stores();
   __syncthreads();
@@ -1099,47 +1247,95 @@ __global__ __launch_bounds__(BLOCK) void beam_step_kernel(
   __syncthreads();
   if (!sm_last) return;  // block-uniform
   if (tid == 0) *done_cnt = 0u;
+  CS_TSTAMP(t3);
   const bool sort_here = n_order > 0 && n2 <= kFusedSort;
-  if (C <= BLOCK) {
-    double acc[1];
-    bool any[1];
-    fold_candidates<1, 64>(Uw, A, C, tid, BLOCK, kind, eps, acc, any);
-    if (tid < C) {
-      const float w = any[0] ? static_cast<float>(acc[0]) : __builtin_nanf("");
-      W[tid] = w;
-      if (sort_here) sm_w[tid] = w;
+  if (order_free) {
+    for (int32_t c = tid; c < C; c += BLOCK) {
+      const float w = welfare_from_key(ld_sc1(wkey + c), is_min);
+      wkey[c] = 0u;  // leave the workspace zeroed for the next call
+      W[c] = w;
+      if (sort_here) sm_w[c] = w;
     }
   } else {
-    for (int32_t c0 = tid; c0 < C; c0 += 4 * BLOCK) {
-      double acc[4];
-      bool any[4];
-      fold_candidates<4, 16>(Uw, A, C, c0, BLOCK, kind, eps, acc, any);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int32_t c = c0 + q * BLOCK;
-        if (c < C) {
-          const float w = any[q] ? static_cast<float>(acc[q]) : __builtin_nanf("");
-          W[c] = w;
-          if (sort_here) sm_w[c] = w;
-        }
-      }
+    for (int32_t c = tid; c < C; c += BLOCK) {
+      double acc[1];
+      bool any[1];
+      fold_candidates<1, 16>(Uw, A, C, c, BLOCK, kind, eps, acc, any);
+      const float w = any[0] ? static_cast<float>(acc[0]) : __builtin_nanf("");
+      W[c] = w;
+      if (sort_here) sm_w[c] = w;
     }
   }
+  CS_TSTAMP(t4);
   if (!sort_here) return;  // block-uniform
   __syncthreads();
-  for (int32_t c = tid; c < n2; c += BLOCK)
-    keys[c] = c < C ? (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
-                          static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c))
-                    : 0ull;
-  __syncthreads();
-  // bitonic sort in LDS: log2(n2)(log2(n2)+1)/2 barrier-separated passes, n2/2 compare-
-  // exchanges each (keys are distinct: the index is in the low word)
-  bitonic_desc(keys, n2, tid, BLOCK);
-  for (int32_t r = tid; r < n_order; r += BLOCK) {
-    const int32_t c = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(keys[r] & 0xffffffffull));
-    out_order[r] = c;
-    if (out_val) out_val[r] = sm_w[c];
+  if (n_order <= kSelectMax) {
+    // the n_order best by histogram threshold + rank counting (as vocab_topk): the
+    // candidates' (value, ~index) keys are distinct, so the order is the full sort's
+    uint32_t* hist = reinterpret_cast<uint32_t*>(keys);      // keys + keys2: 16 KB
+    unsigned long long* cand = sel_cand;
+    for (int i = tid; i < kTopkBins; i += BLOCK) hist[i] = 0u;
+    if (tid == 0) sm_n = 0u;
+    __syncthreads();
+    unsigned long long kc[kFusedSort / BLOCK];
+#pragma unroll
+    for (int r = 0; r < kFusedSort / BLOCK; ++r) {
+      const int32_t c = r * BLOCK + tid;
+      kc[r] = 0ull;
+      if (c < C) {
+        kc[r] = (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
+                static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c));
+        atomicAdd(&hist[key_bin(kc[r])], 1u);
+      }
+    }
+    __syncthreads();
+    const int2 th = hist_threshold<BLOCK>(hist, static_cast<uint32_t>(n_order), sm_tw, sm_res);
+    if (th.y <= kTopkCand) {  // block-uniform
+#pragma unroll
+      for (int r = 0; r < kFusedSort / BLOCK; ++r)
+        if (kc[r] && key_bin(kc[r]) >= static_cast<uint32_t>(th.x)) cand[atomicAdd(&sm_n, 1u)] = kc[r];
+      __syncthreads();
+      rank_candidates<BLOCK>(cand, static_cast<int>(sm_n), n_order,
+                             [&](int r, unsigned long long key) {
+                               const int32_t c = static_cast<int32_t>(
+                                   0xffffffffu - static_cast<uint32_t>(key & 0xffffffffull));
+                               out_order[r] = c;
+                               if (out_val) out_val[r] = sm_w[c];
+                             });
+      return;
+    }
+    __syncthreads();  // the fallback sort below reuses keys / keys2
   }
+  constexpr int KPT = kFusedSort / BLOCK;
+  unsigned long long kv[KPT];
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    const int32_t c = r * BLOCK + tid;
+    kv[r] = c < C ? (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
+                        static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c))
+                  : 0ull;
+  }
+  bitonic_desc_regs<BLOCK, KPT>(kv, n2, keys, keys2);
+  CS_TSTAMP(t5);
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    const int32_t i = r * BLOCK + tid;
+    if (i < n_order) {
+      const int32_t c = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(kv[r] & 0xffffffffull));
+      out_order[i] = c;
+      if (out_val) out_val[i] = sm_w[c];
+    }
+  }
+#ifdef CS_TRACE_BEAM
+  __syncthreads();
+  CS_TSTAMP(t6);
+  if (tid == 0) {
+    const unsigned long long g0 = g_trace_start;
+    printf("TRACE grid_start->wg_start %llu stream %llu rowfinish %llu lastwait %llu welfare %llu sort %llu out %llu (x10ns)\n",
+           t0 - g0, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5);
+    g_trace_start = ~0ull;
+  }
+#endif
 }
 
 }  // namespace
@@ -1316,7 +1512,8 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
   if (rows * plan.nsplit > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_beam_step: grid too large");
   char* wsb = static_cast<char*>(workspace);
   auto* done_cnt = reinterpret_cast<uint32_t*>(wsb);
-  auto* row_cnt = reinterpret_cast<uint32_t*>(wsb + 64);
+  auto* row_cnt = reinterpret_cast<uint32_t*>(wsb + kBeamRowCntOff);
+  auto* wkey = reinterpret_cast<uint32_t*>(wsb + kBeamKeyOff);
   auto* part = reinterpret_cast<unsigned long long*>(wsb + kBeamCounterBytes);
   const int64_t ld_bytes = ld * elt_size(dtype);
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1334,13 +1531,13 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
       hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 256, 8>), grid, dim3(256), 0, st, lg, \
                          vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,          \
                          rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
-                         part, row_cnt, done_cnt, out_U, out_W, n_order, n2, out_order,           \
+                         part, row_cnt, done_cnt, wkey, out_U, out_W, n_order, n2, out_order,     \
                          out_order_val);                                                          \
     else                                                                                          \
       hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 1024, 2>), grid, dim3(1024), 0, st,   \
                          lg, vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,      \
                          rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
-                         part, row_cnt, done_cnt, out_U, out_W, n_order, n2, out_order,           \
+                         part, row_cnt, done_cnt, wkey, out_U, out_W, n_order, n2, out_order,     \
                          out_order_val);                                                          \
   } while (0)
   if (dtype == CS_F32) {

@@ -226,6 +226,7 @@ BEAM_CASES = [
     (torch.bfloat16, 64, 40, 3, 4099, 0.0, "sum"),      # single-pass rows (A*B >= 2048)
     (torch.float16, 5, 3, 7, 5003, 0.0, "sumlog"),      # odd vocab
     (torch.bfloat16, 3, 1, 1, 777, 0.0, "max"),         # first step: one beam, one token
+    (torch.bfloat16, 4, 16, 64, 3001, 0.0, "min"),      # B*K = 1024: largest in-launch sort
 ]
 
 
@@ -254,6 +255,12 @@ def test_beam_step_matches_oracle_and_unfused_path(ops, orc, dev, dtype, A, B, K
     assert torch.equal(torch.nan_to_num(W, nan=7.0), torch.nan_to_num(W2, nan=7.0))
     assert torch.equal(order, o2) and torch.equal(torch.nan_to_num(oval, nan=7.0),
                                                   torch.nan_to_num(v2, nan=7.0))
+    # partial orders (threshold-selection path): the first n of the full order
+    for n in sorted({1, B, min(C, 256), min(C, 257)}):
+        _, Wn, on, vn = ops.beam_step(lg, tg, Rg, kind, n_order=n, softcap=softcap)
+        assert torch.equal(on, order[:n]), f"n_order={n}"
+        assert torch.equal(torch.nan_to_num(vn, nan=7.0), torch.nan_to_num(oval[:n], nan=7.0))
+        assert torch.equal(torch.nan_to_num(Wn, nan=7.0), torch.nan_to_num(W, nan=7.0))
 
     # 2) the CPU oracle: per-agent log-probs within 1e-3, order bit-exact given the scores
     host, bf16 = _host_logits(logits)
@@ -280,3 +287,20 @@ def test_beam_step_sort_skipped_for_sharded_runs(ops, dev):
     assert order is None and U.shape == (A, B * K) and torch.isfinite(W).all()
     with pytest.raises(ops.CSError):
         ops.beam_step(x, t, torch.zeros(A, B + 1, device=dev), "min")
+
+
+def test_beam_step_partial_order_with_ties_and_nan(ops, dev):
+    """Every candidate ties (constant rows, equal rewards) except a few NaN slots: the
+    threshold-selection order must still be index order with NaN last."""
+    A, B, K, V = 3, 8, 16, 2048
+    x = torch.zeros(A * B, V, device=dev, dtype=torch.bfloat16)
+    t = torch.randint(0, V, (B, K), device=dev, dtype=torch.int32)
+    t[2, 5] = -1
+    t[0, 0] = V + 3
+    R = torch.zeros(A, B, device=dev)
+    U, W, full, _ = ops.beam_step(x, t, R, "min")
+    for n in (1, 7, 64, B * K):
+        _, _, part, _ = ops.beam_step(x, t, R, "min", n_order=n)
+        assert torch.equal(part, full[:n])
+    ref = [c for c in range(B * K) if c not in (0, 2 * K + 5)] + [0, 2 * K + 5]
+    assert full.cpu().tolist() == ref

@@ -47,6 +47,7 @@ def main():
         r["lsg_k0_us"] = timed(lambda: ops.logsoftmax_gather(x, None, softcap=cap, workspace=ws, want_lse=True))
         r["lsg_kK_us"] = timed(lambda: ops.logsoftmax_gather(x, t.repeat(A, 1), softcap=cap, workspace=ws))
         r["beam_sort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", softcap=cap, workspace=wb))
+        r["beam_topB_us"] = timed(lambda: ops.beam_step(x, t, R, "min", n_order=B, softcap=cap, workspace=wb))
         r["beam_nosort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", n_order=0, softcap=cap, workspace=wb))
         r["vocab_topk_us"] = timed(lambda: ops.vocab_topk(ref, K, softcap=cap, workspace=ws))
         r["bytes"] = A * B * V * x.element_size()
