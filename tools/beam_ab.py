@@ -50,6 +50,13 @@ def main():
         r["beam_topB_us"] = timed(lambda: ops.beam_step(x, t, R, "min", n_order=B, softcap=cap, workspace=wb))
         r["beam_nosort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", n_order=0, softcap=cap, workspace=wb))
         r["vocab_topk_us"] = timed(lambda: ops.vocab_topk(ref, K, softcap=cap, workspace=ws))
+        wp = ops.Workspace()
+
+        def serial():
+            ids, _ = ops.vocab_topk(ref, K, softcap=cap, workspace=wp)
+            return ops.beam_step(x, ids, R, "min", n_order=B, softcap=cap, workspace=wb)
+
+        r["step_us"] = timed(serial)   # proposer + fused scoring step, top-B kept
         r["bytes"] = A * B * V * x.element_size()
         r["ideal_us"] = r["bytes"] / 8e12 * 1e6
         print(json.dumps(r), flush=True)
