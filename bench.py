@@ -227,19 +227,24 @@ def run_beam(name, world, rank, dev, steps, warmup):
     g = torch.Generator(device=dev).manual_seed(4321 + rank)
     ref = (torch.randn(B, V, generator=g, device=dev) * 3.0).to(dt)
     ag = (torch.randn(A_loc * B, V, generator=g, device=dev) * 3.0).to(dt)
-    R = torch.zeros(A_loc, B, dtype=torch.float32, device=dev)
+    # cumulative rewards, ping-pong: step i reads Rs[i % 2] and the launch writes the kept
+    # beams' rewards into Rs[(i + 1) % 2] (cs_beam_step out_kept)
+    Rs = [torch.zeros(A_loc, B, dtype=torch.float32, device=dev) for _ in range(2)]
+    R = Rs[0]
     ws_p, ws_b = ops.Workspace(), ops.Workspace(zeroed=True)
     sharded = world > 1
 
-    def score():
+    def score(i=0):
         ids, _ = ops.vocab_topk(ref, K, softcap=cap, workspace=ws_p)
         if A_loc == 0:   # more ranks than agents: this rank only proposes
             return (torch.empty(0, C, device=dev),
                     torch.full((C,), float("inf"), device=dev), None)
         # keep = the B best candidates: the launch selects them (threshold + rank, no
-        # full sort); sharded runs all-reduce W first and select afterwards
-        U, W, order, _ = ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else B,
-                                       softcap=cap, workspace=ws_b)
+        # full sort) and writes their rewards; sharded runs all-reduce W first and
+        # select afterwards
+        U, W, order, _ = ops.beam_step(ag, ids, Rs[i % 2], "min", n_order=0 if sharded else B,
+                                       softcap=cap, workspace=ws_b,
+                                       kept_out=None if sharded else Rs[(i + 1) % 2])
         return U, W, order
 
     def keep(U, order):
@@ -253,22 +258,23 @@ def run_beam(name, world, rank, dev, steps, warmup):
     s = torch.cuda.Stream(device=dev)
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        for _ in range(3):   # warm the workspaces / allocator before capture
-            U, W, order = score()
-            if not sharded:
-                keep(U, order)
+        for i in range(4):   # warm the workspaces / allocator before capture
+            U, W, order = score(i)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     with torch.cuda.graph(g1):
-        U, W, order = score()
-        if not sharded:
-            keep(U, order)
+        if not sharded:      # two decode steps per replay (the reward buffers ping-pong)
+            score(0)
+            U, W, order = score(1)
         else:
+            U, W, order = score()
             Wx = torch.where(torch.isnan(W), torch.full_like(W, float("inf")), W)
     if sharded:
         with torch.cuda.graph(g2):
             select(U, Wx)
+    per_replay = 1 if sharded else 2
+    steps = max(per_replay, steps - steps % per_replay)
 
     def step():
         g1.replay()
@@ -276,14 +282,14 @@ def run_beam(name, world, rank, dev, steps, warmup):
             torch.distributed.all_reduce(Wx, op=torch.distributed.ReduceOp.MIN)
             g2.replay()
 
-    for _ in range(warmup):
+    for _ in range(max(1, warmup // per_replay)):
         step()
     torch.cuda.synchronize()
     if sharded:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(steps // per_replay):
         step()
     torch.cuda.synchronize()
     if sharded:
@@ -304,8 +310,8 @@ def run_beam(name, world, rank, dev, steps, warmup):
     for e0, e1 in ev:
         e0.record(st)
         if A_loc:
-            ops.beam_step(ag, ids, R, "min", n_order=0 if sharded else B, softcap=cap,
-                          workspace=ws_b)
+            ops.beam_step(ag, ids, Rs[0], "min", n_order=0 if sharded else B, softcap=cap,
+                          workspace=ws_b, kept_out=None if sharded else Rs[1])
         e1.record(st)
     torch.cuda.synchronize()
     k_ms = max(float(np.median([a.elapsed_time(b) for a, b in ev])), 1e-6)
@@ -317,7 +323,7 @@ def run_beam(name, world, rank, dev, steps, warmup):
             "decode_steps_per_s": 1000.0 / ms, "ms_per_step": ms,
             "scorings_per_s": A * C / (ms * 1e-3), "steps": steps,
             "timing": "hipGraph replay" + (" + eager RCCL all-reduce" if sharded else ""),
-            "roofline": {"bound": "hbm", "kernel": "cs_beam_step (lsg_stream_kernel + beam_tail_kernel)",
+            "roofline": {"bound": "hbm", "kernel": "cs_beam_step (beam_step_kernel: vocab stream + gather + welfare + top-B)",
                          "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
                          "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},

@@ -83,7 +83,7 @@ def load():
     L.cs_beam_step_workspace_size.argtypes = [i64, i64]
     L.cs_beam_step_workspace_size.restype = ctypes.c_size_t
     L.cs_beam_step.argtypes = [vp, ctypes.c_int, i32, i32, i64, i64, vp, i32, vp, f32, ctypes.c_int,
-                               f32, vp, vp, i32, vp, vp, vp, ctypes.c_size_t, vp]
+                               f32, vp, vp, i32, vp, vp, vp, vp, ctypes.c_size_t, vp]
     L.cs_beam_step.restype = ctypes.c_int
     _lib = L
     return L

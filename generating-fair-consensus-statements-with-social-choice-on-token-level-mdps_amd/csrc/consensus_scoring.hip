@@ -707,6 +707,48 @@ __device__ __forceinline__ void rank_candidates(const unsigned long long* cand, 
   }
 }
 
+// Radix select over 12-bit digits from the top of the 64-bit keys: the first digit is
+// hist_threshold's bin; while the keys that can still be among the k largest (every key
+// of a higher bin, plus the threshold bin) number more than `limit`, the threshold bin is
+// split on the next 12 bits.  Returns (shift, prefix, count): the keys with
+// (key >> shift) >= prefix are the k largest plus the other keys of the last threshold
+// bin, `count` of them.  The last digit sits at shift 4, where a bin holds at most 16
+// distinct keys, so count <= k + 15 there.  Clustered values (e.g. beam rewards that
+// share one exponent) refine instead of ranking hundreds of candidates.
+// for_each(f) calls f(key) for each present key of the calling thread's share.
+struct RadixCut {
+  int shift;
+  unsigned long long prefix;
+  uint32_t count;
+};
+
+template <int NT, typename ForEach>
+__device__ __forceinline__ RadixCut radix_select(ForEach for_each, uint32_t k, uint32_t limit,
+                                                 uint32_t* hist, uint32_t* sm_w, int* sm_res) {
+  int shift = 52;
+  unsigned long long prefix = 0ull;
+  uint32_t above = 0;
+  for (;;) {
+    for (int i = threadIdx.x; i < kTopkBins; i += NT) hist[i] = 0u;
+    __syncthreads();
+    const int sh = shift;
+    const unsigned long long pf = prefix;
+    for_each([&](unsigned long long key) {
+      if (sh == 52 || (key >> (sh + 12)) == pf)
+        atomicAdd(&hist[static_cast<uint32_t>(key >> sh) & (kTopkBins - 1)], 1u);
+    });
+    __syncthreads();
+    const int2 th = hist_threshold<NT>(hist, k - above, sm_w, sm_res);
+    const uint32_t in_bin = hist[th.x];
+    prefix = (prefix << 12) | static_cast<unsigned long long>(th.x);
+    const uint32_t count = above + static_cast<uint32_t>(th.y);
+    if (count <= limit || shift < 12) return RadixCut{shift, prefix, count};
+    above = count - in_bin;
+    shift -= 12;
+    __syncthreads();  // every thread has read hist before the next level clears it
+  }
+}
+
 // One (row, 4096-element chunk) per workgroup: the chunk's k largest composite keys
 // (order key, ~token id), descending, zero-padded when the chunk holds fewer than k.
 template <int DT, bool CAP>
@@ -739,25 +781,26 @@ __global__ __launch_bounds__(256) void vocab_topk_chunk_kernel(
                static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + i));
     }
   }
-  for (int i = tid; i < kTopkBins; i += 256) hist[i] = 0u;
   if (tid == 0) sm_n = 0u;
-  __syncthreads();
+  const RadixCut cut = radix_select<256>(
+      [&](auto f) {
 #pragma unroll
-  for (int j = 0; j < kTopkPer; ++j)
-    if (key[j]) atomicAdd(&hist[key_bin(key[j])], 1u);
-  __syncthreads();
-  const int2 th = hist_threshold(hist, static_cast<uint32_t>(k), sm_w, sm_res);
+        for (int j = 0; j < kTopkPer; ++j)
+          if (key[j]) f(key[j]);
+      },
+      static_cast<uint32_t>(k), static_cast<uint32_t>(2 * k + 64), hist, sm_w, sm_res);
   unsigned long long* out = part + (row * nchunk + chunk) * static_cast<int64_t>(k);
-  if (th.y <= kTopkCand) {  // block-uniform
+  if (cut.count <= kTopkCand) {  // block-uniform (always, unless > 1024 keys tie exactly)
 #pragma unroll
     for (int j = 0; j < kTopkPer; ++j)
-      if (key[j] && key_bin(key[j]) >= static_cast<uint32_t>(th.x)) cand[atomicAdd(&sm_n, 1u)] = key[j];
+      if (key[j] && (key[j] >> cut.shift) >= cut.prefix) cand[atomicAdd(&sm_n, 1u)] = key[j];
     __syncthreads();
     const int nc = static_cast<int>(sm_n);
     rank_candidates(cand, nc, k, [&](int r, unsigned long long kc) { out[r] = kc; });
     for (int r = nc + tid; r < k; r += 256) out[r] = 0ull;
     return;
   }
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < kTopkPer; ++j) lds[tid + 256 * j] = key[j];
   __syncthreads();
@@ -785,19 +828,19 @@ __global__ __launch_bounds__(256) void vocab_topk_merge_kernel(
   const int tid = threadIdx.x;
   const int64_t row = blockIdx.x;
   const unsigned long long* pr = part + row * nkeys;
-  for (int i = tid; i < kTopkBins; i += 256) hist[i] = 0u;
   if (tid == 0) sm_n = 0u;
-  __syncthreads();
-  for (int i = tid; i < nkeys; i += 256) {
-    const unsigned long long c = pr[i];
-    if (c) atomicAdd(&hist[key_bin(c)], 1u);
-  }
-  __syncthreads();
-  const int2 th = hist_threshold(hist, static_cast<uint32_t>(k), sm_w, sm_res);
-  if (th.y <= kTopkCand) {  // block-uniform
+  const RadixCut cut = radix_select<256>(
+      [&](auto f) {
+        for (int i = tid; i < nkeys; i += 256) {
+          const unsigned long long c = pr[i];
+          if (c) f(c);
+        }
+      },
+      static_cast<uint32_t>(k), static_cast<uint32_t>(2 * k + 64), hist, sm_w, sm_res);
+  if (cut.count <= kTopkCand) {  // block-uniform
     for (int i = tid; i < nkeys; i += 256) {
       const unsigned long long c = pr[i];
-      if (c && key_bin(c) >= static_cast<uint32_t>(th.x)) cand[atomicAdd(&sm_n, 1u)] = c;
+      if (c && (c >> cut.shift) >= cut.prefix) cand[atomicAdd(&sm_n, 1u)] = c;
     }
     __syncthreads();
     const int nc = static_cast<int>(sm_n);
@@ -806,6 +849,7 @@ __global__ __launch_bounds__(256) void vocab_topk_merge_kernel(
     for (int r = nc + tid; r < k; r += 256) emit_token(out_ids, out_vals, row * k + r, 0ull);
     return;
   }
+  __syncthreads();
   for (int i = tid; i < n2; i += 256) mk[i] = (i < nkeys) ? pr[i] : 0ull;
   __syncthreads();
   bitonic_desc(mk, n2, tid, 256);
@@ -1075,6 +1119,20 @@ __device__ __forceinline__ void fold_candidates(uint32_t* U, int32_t A, int32_t 
   }
 }
 
+// The kept beams' cumulative rewards: out_kept[a][r] = U[a][ord[r]] (ord in LDS), all
+// A * n_order loads spread over the block so they are in flight together (U was written
+// by other workgroups: sc1 loads).
+template <int BLOCK>
+__device__ __forceinline__ void keep_columns(uint32_t* U, float* out_kept, const int32_t* ord,
+                                             int32_t A, int32_t C, int32_t n_order) {
+  const int32_t n = A * n_order;
+  for (int32_t i = threadIdx.x; i < n; i += BLOCK) {
+    const int32_t a = i / n_order;
+    const int32_t r = i - a * n_order;
+    out_kept[i] = __uint_as_float(ld_sc1(U + static_cast<int64_t>(a) * C + ord[r]));
+  }
+}
+
 // Descending bitonic sort of n2 (a power of two <= KPT * BLOCK) distinct keys held in
 // registers: element i = r * BLOCK + tid lives in kv[r] of thread tid.  Exchanges at
 // stride < 64 go through wave shuffles (no barrier), at stride >= BLOCK between the
@@ -1146,7 +1204,7 @@ __global__ __launch_bounds__(BLOCK, 2) void beam_step_kernel(
     unsigned long long* __restrict__ part, uint32_t* __restrict__ row_cnt,
     uint32_t* __restrict__ done_cnt, uint32_t* __restrict__ wkey, float* __restrict__ U,
     float* __restrict__ W, int32_t n_order, int32_t n2, int32_t* __restrict__ out_order,
-    float* __restrict__ out_val) {
+    float* __restrict__ out_val, float* __restrict__ out_kept) {
   __shared__ float sm_m[BLOCK / 64];
   __shared__ float sm_s[BLOCK / 64];
   __shared__ float sm_lse;
@@ -1156,6 +1214,7 @@ __global__ __launch_bounds__(BLOCK, 2) void beam_step_kernel(
   unsigned long long* keys2 = keys + kFusedSort;
   __shared__ __attribute__((aligned(16))) unsigned long long sel_cand[kTopkCand];
   __shared__ float sm_w[kFusedSort];
+  __shared__ int32_t sm_ord[kFusedSort];
   __shared__ uint32_t sm_tw[BLOCK / 64];
   __shared__ int sm_res[2];
   __shared__ uint32_t sm_n;
@@ -1274,26 +1333,26 @@ __global__ __launch_bounds__(BLOCK, 2) void beam_step_kernel(
     // candidates' (value, ~index) keys are distinct, so the order is the full sort's
     uint32_t* hist = reinterpret_cast<uint32_t*>(keys);      // keys + keys2: 16 KB
     unsigned long long* cand = sel_cand;
-    for (int i = tid; i < kTopkBins; i += BLOCK) hist[i] = 0u;
     if (tid == 0) sm_n = 0u;
-    __syncthreads();
     unsigned long long kc[kFusedSort / BLOCK];
 #pragma unroll
     for (int r = 0; r < kFusedSort / BLOCK; ++r) {
       const int32_t c = r * BLOCK + tid;
-      kc[r] = 0ull;
-      if (c < C) {
-        kc[r] = (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
-                static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c));
-        atomicAdd(&hist[key_bin(kc[r])], 1u);
-      }
+      kc[r] = c < C ? (static_cast<unsigned long long>(order_key(sm_w[c])) << 32) |
+                          static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c))
+                    : 0ull;
     }
-    __syncthreads();
-    const int2 th = hist_threshold<BLOCK>(hist, static_cast<uint32_t>(n_order), sm_tw, sm_res);
-    if (th.y <= kTopkCand) {  // block-uniform
+    const RadixCut cut = radix_select<BLOCK>(
+        [&](auto f) {
+#pragma unroll
+          for (int r = 0; r < kFusedSort / BLOCK; ++r)
+            if (kc[r]) f(kc[r]);
+        },
+        static_cast<uint32_t>(n_order), static_cast<uint32_t>(n_order + 64), hist, sm_tw, sm_res);
+    if (cut.count <= kTopkCand) {  // block-uniform
 #pragma unroll
       for (int r = 0; r < kFusedSort / BLOCK; ++r)
-        if (kc[r] && key_bin(kc[r]) >= static_cast<uint32_t>(th.x)) cand[atomicAdd(&sm_n, 1u)] = kc[r];
+        if (kc[r] && (kc[r] >> cut.shift) >= cut.prefix) cand[atomicAdd(&sm_n, 1u)] = kc[r];
       __syncthreads();
       rank_candidates<BLOCK>(cand, static_cast<int>(sm_n), n_order,
                              [&](int r, unsigned long long key) {
@@ -1301,7 +1360,12 @@ __global__ __launch_bounds__(BLOCK, 2) void beam_step_kernel(
                                    0xffffffffu - static_cast<uint32_t>(key & 0xffffffffull));
                                out_order[r] = c;
                                if (out_val) out_val[r] = sm_w[c];
+                               sm_ord[r] = c;
                              });
+      if (out_kept) {
+        __syncthreads();
+        keep_columns<BLOCK>(Uw, out_kept, sm_ord, A, C, n_order);
+      }
       return;
     }
     __syncthreads();  // the fallback sort below reuses keys / keys2
@@ -1324,7 +1388,12 @@ __global__ __launch_bounds__(BLOCK, 2) void beam_step_kernel(
       const int32_t c = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(kv[r] & 0xffffffffull));
       out_order[i] = c;
       if (out_val) out_val[i] = sm_w[c];
+      sm_ord[i] = c;
     }
+  }
+  if (out_kept) {
+    __syncthreads();
+    keep_columns<BLOCK>(Uw, out_kept, sm_ord, A, C, n_order);
   }
 #ifdef CS_TRACE_BEAM
   __syncthreads();
@@ -1482,7 +1551,7 @@ size_t cs_beam_step_workspace_size(int64_t rows, int64_t vocab) {
 int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vocab, int64_t ld,
                  const int32_t* targets, int32_t K, const float* rewards_in, float softcap,
                  int welfare_kind, float eps, float* out_U, float* out_W, int32_t n_order,
-                 int32_t* out_order, float* out_order_val, void* workspace,
+                 int32_t* out_order, float* out_order_val, float* out_kept, void* workspace,
                  size_t workspace_bytes, cs_stream_t stream) {
   if (dtype != CS_F32 && dtype != CS_BF16 && dtype != CS_F16)
     return fail(CS_ERR_INVALID, "cs_beam_step: unknown dtype");
@@ -1493,6 +1562,8 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
   if (C > 16384) return fail(CS_ERR_INVALID, "cs_beam_step: B*K exceeds 16384");
   if (rows > kBeamMaxRows) return fail(CS_ERR_INVALID, "cs_beam_step: A*B exceeds 65536");
   if (n_order < 0 || n_order > C) return fail(CS_ERR_INVALID, "cs_beam_step: need 0 <= n_order <= B*K");
+  if (out_kept && (n_order == 0 || C > kFusedSort))
+    return fail(CS_ERR_INVALID, "cs_beam_step: out_kept needs n_order > 0 and B*K <= 1024");
   if (welfare_kind < CS_WELFARE_MIN || welfare_kind > CS_WELFARE_MAX)
     return fail(CS_ERR_INVALID, "cs_beam_step: unknown welfare kind");
   if (!(softcap >= 0.0f) || std::isinf(softcap))
@@ -1532,13 +1603,13 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
                          vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,          \
                          rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
                          part, row_cnt, done_cnt, wkey, out_U, out_W, n_order, n2, out_order,     \
-                         out_order_val);                                                          \
+                         out_order_val, out_kept);                                                \
     else                                                                                          \
       hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 1024, 2>), grid, dim3(1024), 0, st,   \
                          lg, vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,      \
                          rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
                          part, row_cnt, done_cnt, wkey, out_U, out_W, n_order, n2, out_order,     \
-                         out_order_val);                                                          \
+                         out_order_val, out_kept);                                                \
   } while (0)
   if (dtype == CS_F32) {
     if (fixed) CS_BEAM_LAUNCH(CS_F32, true, true);

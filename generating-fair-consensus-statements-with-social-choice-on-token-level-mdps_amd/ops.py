@@ -201,7 +201,8 @@ def topk(W: torch.Tensor, k: int, *, with_values: bool = True):
 
 def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor, kind="min", *,
               n_order: Optional[int] = None, vocab: Optional[int] = None, softcap: float = 0.0,
-              eps: float = 1e-9, workspace: Optional[Workspace] = None):
+              eps: float = 1e-9, workspace: Optional[Workspace] = None,
+              kept_out: Optional[torch.Tensor] = None):
     """One beam-search scoring step after the LM head, fused into one launch.
 
     logits  [A*B, ld] agent rows (row a*B + b = agent a, beam b);
@@ -209,7 +210,10 @@ def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor
     rewards [A, B] float32 cumulative per-agent rewards of the beams.
     Returns (U [A, B*K], W [B*K], order [n_order] int32, order_val [n_order]) with
     U = rewards + log p(token), W = welfare over agents, order = stable descending
-    (n_order defaults to B*K; 0 skips the sort and returns (U, W, None, None)).
+    (n_order defaults to B*K; 0 skips the sort and returns (U, W, None, None); up to 256
+    the launch selects the n_order best without sorting the rest).
+    kept_out [A, n_order] float32 (optional) receives U[:, order]: the cumulative rewards
+    of the kept beams when the first n_order ranks are kept (B*K <= 1024).
 
     Restates beam_search.py:495-560 (per-candidate agent log-probs :335-404,
     cumulative rewards :534-536, stable sort by min over agents :558-560).
@@ -242,10 +246,16 @@ def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor
     if not workspace.zeroed:
         raise CSError("beam_step needs a Workspace(zeroed=True) of its own (arrival counters)")
     ws = workspace.get(nbytes, dev)
+    if kept_out is not None:
+        if (kept_out.dtype != torch.float32 or not kept_out.is_contiguous()
+                or tuple(kept_out.shape) != (A, n_order)):
+            raise CSError(f"kept_out must be a contiguous float32 [{A}, {n_order}] tensor")
+        _require_cuda(kept_out)
     rc = L.cs_beam_step(logits.data_ptr(), _DTYPE[logits.dtype], A, B, vocab, ld,
                         targets.data_ptr(), K, rewards.data_ptr(), float(softcap), int(kind),
                         float(eps), U.data_ptr(), W.data_ptr(), n_order,
                         order.data_ptr() if n_order else None, oval.data_ptr() if n_order else None,
+                        kept_out.data_ptr() if kept_out is not None else None,
                         ws.data_ptr() if ws is not None else None,
                         ws.numel() if ws is not None else 0, _stream())
     _lib.check(rc, "cs_beam_step")

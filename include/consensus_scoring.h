@@ -152,6 +152,11 @@ int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld
  *     out_W[c]     = welfare_kind over a of out_U[a*C+c]         (as cs_welfare_reduce, SKIP)
  *     out_order[r] = index of rank r by (W desc, index asc), NaN last, r < n_order
  *                    (as cs_segmented_topk); out_order_val (nullable) = W at that index.
+ *     out_kept[a*n_order + r] (nullable) = out_U[a*C + out_order[r]]: the cumulative
+ *                    rewards of the kept beams when the first n_order ranks are kept
+ *                    (needs n_order > 0 and B*K <= 1024).
+ * n_order <= 256 selects the n_order best (radix-select threshold + rank counting, the
+ * exact stable order) without sorting the rest.
  * Bit-identical to cs_logsoftmax_gather + cs_welfare_reduce + cs_segmented_topk on the
  * same inputs.  n_order = 0 skips the sort (agent-sharded runs all-reduce out_W
  * first, then call cs_segmented_topk).  B*K <= 16384 (a second launch sorts when
@@ -169,7 +174,7 @@ size_t cs_beam_step_workspace_size(int64_t rows, int64_t vocab);
 int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vocab, int64_t ld,
                  const int32_t* targets, int32_t K, const float* rewards_in, float softcap,
                  int welfare_kind, float eps, float* out_U, float* out_W, int32_t n_order,
-                 int32_t* out_order, float* out_order_val, void* workspace,
+                 int32_t* out_order, float* out_order_val, float* out_kept, void* workspace,
                  size_t workspace_bytes, cs_stream_t stream);
 
 /*

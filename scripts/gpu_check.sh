@@ -17,9 +17,9 @@ run_prof() {
 }
 run_pmc() {
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -f csv -- \
-     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/pmc_fetch.log" 2>&1) && \
+     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --beam "" > "$OUT/pmc_fetch.log" 2>&1) && \
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -f csv -- \
-     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/pmc_write.log" 2>&1)
+     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --beam "" > "$OUT/pmc_write.log" 2>&1)
 }
 case "$STEP" in
   tests) run_tests ;;

@@ -66,7 +66,7 @@ def _vt(logits, k, *, vocab=None, softcap=0.0, workspace=None):
 
 
 def _bs(logits, targets, rewards, kind="min", *, n_order=None, vocab=None, softcap=0.0,
-        eps=1e-9, workspace=None):
+        eps=1e-9, workspace=None, kept_out=None):
     A, B = rewards.shape
     K = targets.shape[1]
     tok, _ = _lsg(logits, targets.repeat(A, 1), vocab=vocab, softcap=softcap)
@@ -76,6 +76,8 @@ def _bs(logits, targets, rewards, kind="min", *, n_order=None, vocab=None, softc
     if n == 0:
         return U, W, None, None
     order, val = _tk(W, n)
+    if kept_out is not None:
+        kept_out.copy_(U[:, order.long()])
     return U, W, order.to(torch.int32), val
 
 

@@ -257,8 +257,12 @@ def test_beam_step_matches_oracle_and_unfused_path(ops, orc, dev, dtype, A, B, K
                                                   torch.nan_to_num(v2, nan=7.0))
     # partial orders (threshold-selection path): the first n of the full order
     for n in sorted({1, B, min(C, 256), min(C, 257)}):
-        _, Wn, on, vn = ops.beam_step(lg, tg, Rg, kind, n_order=n, softcap=softcap)
+        kept = torch.empty(A, n, device=dev) if C <= 1024 else None
+        _, Wn, on, vn = ops.beam_step(lg, tg, Rg, kind, n_order=n, softcap=softcap, kept_out=kept)
         assert torch.equal(on, order[:n]), f"n_order={n}"
+        if kept is not None:
+            assert torch.equal(torch.nan_to_num(kept, nan=7.0),
+                               torch.nan_to_num(U[:, on.long()], nan=7.0))
         assert torch.equal(torch.nan_to_num(vn, nan=7.0), torch.nan_to_num(oval[:n], nan=7.0))
         assert torch.equal(torch.nan_to_num(Wn, nan=7.0), torch.nan_to_num(W, nan=7.0))
 
@@ -304,3 +308,29 @@ def test_beam_step_partial_order_with_ties_and_nan(ops, dev):
         assert torch.equal(part, full[:n])
     ref = [c for c in range(B * K) if c not in (0, 2 * K + 5)] + [0, 2 * K + 5]
     assert full.cpu().tolist() == ref
+
+
+@pytest.mark.parametrize("offset", [-1000.0, -3.0e6])
+def test_beam_step_partial_order_clustered_rewards(ops, dev, offset):
+    """Cumulative rewards far from zero put every welfare value in one exponent bin: the
+    selection refines digit by digit and must still return the exact stable order."""
+    A, B, K, V = 8, 16, 50, 4099
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(A * B, V, generator=g, device=dev) * 3.0
+    t = torch.randint(0, V, (B, K), generator=g, device=dev, dtype=torch.int32)
+    R = offset - torch.rand(A, B, generator=g, device=dev)
+    _, W, full, _ = ops.beam_step(x, t, R, "min")
+    o2, _ = ops.topk(W, B * K)
+    assert torch.equal(full, o2)
+    for n in (1, B, 100, 256):
+        _, _, part, _ = ops.beam_step(x, t, R, "min", n_order=n)
+        assert torch.equal(part, full[:n]), n
+
+
+def test_vocab_topk_clustered_values(ops, orc, dev):
+    """Logits that share one exponent (the histogram's first digit) and exact ties."""
+    g = torch.Generator().manual_seed(9)
+    x = 1000.0 + torch.randint(0, 50, (4, 30000), generator=g).float() / 64.0
+    ids, vals = ops.vocab_topk(x.to(dev), 64)
+    o_ids, o_vals = orc.vocab_topk(x.double().numpy(), 64)
+    assert np.array_equal(ids.cpu().numpy(), o_ids)
