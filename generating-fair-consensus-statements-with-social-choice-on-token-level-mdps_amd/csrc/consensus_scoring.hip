@@ -768,6 +768,9 @@ __global__ __launch_bounds__(256) void vocab_topk_chunk_kernel(
   const char* rp = logits + row * ld_bytes;
   const int64_t v0 = static_cast<int64_t>(chunk) * kTopkChunk;
   const int n = static_cast<int>(min(static_cast<int64_t>(kTopkChunk), vocab - v0));
+#ifdef CS_TRACE_TOPK
+  const unsigned long long q0 = wall_clock64();
+#endif
   unsigned long long key[kTopkPer];
 #pragma unroll
   for (int j = 0; j < kTopkPer; ++j) {
@@ -782,6 +785,10 @@ __global__ __launch_bounds__(256) void vocab_topk_chunk_kernel(
     }
   }
   if (tid == 0) sm_n = 0u;
+#ifdef CS_TRACE_TOPK
+  __syncthreads();
+  const unsigned long long q1 = wall_clock64();
+#endif
   const RadixCut cut = radix_select<256>(
       [&](auto f) {
 #pragma unroll
@@ -789,6 +796,9 @@ __global__ __launch_bounds__(256) void vocab_topk_chunk_kernel(
           if (key[j]) f(key[j]);
       },
       static_cast<uint32_t>(k), static_cast<uint32_t>(2 * k + 64), hist, sm_w, sm_res);
+#ifdef CS_TRACE_TOPK
+  const unsigned long long q2 = wall_clock64();
+#endif
   unsigned long long* out = part + (row * nchunk + chunk) * static_cast<int64_t>(k);
   if (cut.count <= kTopkCand) {  // block-uniform (always, unless > 1024 keys tie exactly)
 #pragma unroll
@@ -798,6 +808,12 @@ __global__ __launch_bounds__(256) void vocab_topk_chunk_kernel(
     const int nc = static_cast<int>(sm_n);
     rank_candidates(cand, nc, k, [&](int r, unsigned long long kc) { out[r] = kc; });
     for (int r = nc + tid; r < k; r += 256) out[r] = 0ull;
+#ifdef CS_TRACE_TOPK
+    __syncthreads();
+    if (tid == 0 && blockIdx.x % 97 == 0)
+      printf("TOPK chunk %d load %llu select %llu rank %llu nc %d levels %d (x10ns)\n", (int)blockIdx.x,
+             q1 - q0, q2 - q1, wall_clock64() - q2, nc, (52 - cut.shift) / 12 + 1);
+#endif
     return;
   }
   __syncthreads();

@@ -218,6 +218,41 @@ def test_c2_full_size_sampled_rows(ops, orc, dev):
     torch.cuda.empty_cache()
 
 
+def test_c4_full_size_lookahead_nash(ops, orc, dev):
+    """BASELINE C4 at full size: R = 256 paths x depth 4 x A = 32 agents = 32,768 rows x
+    128,256 bf16 (8.4 GB).  Sampled rows vs the oracle; the full pipeline (mean of each
+    path's 4 log-probs -> U [32, 256] -> Nash welfare -> argmax) vs the oracle's folds on
+    the kernel's own token log-probs (size-independent: exact fold order and tie-break)."""
+    A, R, D, V = 32, 256, 4, 128_256
+    rows = A * R * D
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = torch.empty(rows, V, dtype=torch.bfloat16, device=dev)
+    for r0 in range(0, rows, 4096):
+        x[r0:r0 + 4096] = (torch.randn(min(4096, rows - r0), V, generator=g, device=dev) * 3)
+    t = torch.randint(0, V, (rows, 1), generator=g, device=dev, dtype=torch.int32)
+    tok, _ = ops.logsoftmax_gather(x, t)
+    pick = torch.tensor([0, 3, 4, 16_383, 16_384, rows - 1], device=dev)
+    o_tok, _ = orc.logsoftmax_gather(_bits(x[pick]), t[pick].cpu().numpy(), bf16=True)
+    assert np.max(np.abs(tok[pick].cpu().numpy().reshape(-1) - o_tok.reshape(-1))) < LP_TOL
+    del x
+    torch.cuda.empty_cache()
+    offs = torch.arange(0, rows + 1, D, dtype=torch.int32, device=dev)
+    seg = ops.segment_reduce(tok, offs)
+    U = (seg["sum_lp"] / seg["count"].float()).view(A, R)
+    # Nash welfare of log-prob utilities needs positive utilities: exp(mean lp) as in the
+    # evaluator's avg-prob welfare (evaluation.py:337-349)
+    P = torch.exp(U).contiguous()
+    W = ops.welfare(P, "sumlog")
+    best, _ = ops.topk(W, 1)
+    h = tok.cpu().numpy().reshape(-1)
+    o_seg = orc.segment_reduce(h, offs.cpu().numpy())
+    o_U = (o_seg["sum_lp"] / o_seg["count"]).reshape(A, R)
+    assert np.max(np.abs(U.cpu().numpy() - o_U)) < LP_TOL
+    o_W = orc.welfare(P.cpu().double().numpy(), orc.SUMLOG, eps=1e-9)
+    assert np.max(np.abs(W.cpu().numpy() - o_W)) < 1e-3 * A
+    assert int(best.item()) == int(orc.topk(W.cpu().double().numpy(), 1)[0, 0])
+
+
 BEAM_CASES = [
     # dtype, A, B, K, vocab, softcap, kind          shape exercised
     (torch.float32, 4, 4, 10, 128256, 0.0, "min"),     # C1 (fp32 Llama-3.2-1B vocab)
