@@ -24,7 +24,8 @@ EXPORTED = (
     "cs_version", "cs_last_error", "cs_workspace_size", "cs_logsoftmax_gather",
     "cs_segment_reduce", "cs_welfare_reduce", "cs_segmented_topk", "cs_vocab_topk_workspace_size",
     "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
-    "cs_beam_step_workspace_size", "cs_beam_step",
+    "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
+    "cs_beam_decode_step",
 )
 
 
@@ -85,6 +86,12 @@ def load():
     L.cs_beam_step.argtypes = [vp, ctypes.c_int, i32, i32, i64, i64, vp, i32, vp, f32, ctypes.c_int,
                                f32, vp, vp, i32, vp, vp, vp, vp, ctypes.c_size_t, vp]
     L.cs_beam_step.restype = ctypes.c_int
+    L.cs_beam_decode_workspace_size.argtypes = [i32, i32, i64, i32]
+    L.cs_beam_decode_workspace_size.restype = ctypes.c_size_t
+    L.cs_beam_decode_step.argtypes = [vp, i64, vp, i64, ctypes.c_int, i32, i32, i64, i32, f32, vp,
+                                      ctypes.c_int, f32, vp, vp, vp, i32, vp, vp, vp, vp,
+                                      ctypes.c_size_t, vp]
+    L.cs_beam_decode_step.restype = ctypes.c_int
     _lib = L
     return L
 

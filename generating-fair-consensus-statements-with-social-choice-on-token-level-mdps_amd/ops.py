@@ -64,6 +64,7 @@ class Workspace:
 
 _default_ws: dict = {}
 _beam_ws: dict = {}
+_decode_ws: dict = {}
 
 
 def workspace_size(rows: int, vocab: int, k: int = 1) -> int:
@@ -262,6 +263,66 @@ def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor
     if n_order == 0:
         return U, W, None, None
     return U, W, order, oval
+
+
+def beam_decode_step(ref_logits: torch.Tensor, logits: torch.Tensor, rewards: torch.Tensor,
+                     k: int, kind="min", *, n_order: Optional[int] = None,
+                     vocab: Optional[int] = None, softcap: float = 0.0, eps: float = 1e-9,
+                     workspace: Optional[Workspace] = None,
+                     kept_out: Optional[torch.Tensor] = None):
+    """Proposer + scoring of one beam decode step in ONE launch (cs_beam_decode_step).
+
+    ref_logits [B, ld_ref] reference-policy rows; logits [A*B, ld] agent rows (row a*B+b);
+    rewards [A, B] float32.  Returns (ids [B, k] int32, U [A, B*k], W [B*k], order, order_val)
+    — identical to ``ids, _ = vocab_topk(ref_logits, k)`` followed by
+    ``beam_step(logits, ids, rewards, ...)``.  Restates beam_search.py:439-560.
+    """
+    L = _lib.load()
+    rows, ld, vocab = _logits_args(logits, vocab)
+    B_ref, ld_ref, _ = _logits_args(ref_logits, vocab)
+    if rewards.dim() != 2 or rewards.dtype != torch.float32:
+        raise CSError("rewards must be [A, B] float32")
+    if ref_logits.dtype != logits.dtype:
+        raise CSError("ref_logits and logits must share a dtype")
+    rewards = rewards.contiguous()
+    A, B = rewards.shape
+    if B_ref != B or rows != A * B:
+        raise CSError(f"shape mismatch: ref rows {B_ref}, agent rows {rows}, rewards {tuple(rewards.shape)}")
+    _require_cuda(ref_logits, logits, rewards)
+    if isinstance(kind, str):
+        kind = WELFARE[kind]
+    k = int(k)
+    C = B * k
+    n_order = C if n_order is None else int(n_order)
+    dev = logits.device
+    ids = torch.empty((B, k), dtype=torch.int32, device=dev)
+    U = torch.empty((A, C), dtype=torch.float32, device=dev)
+    W = torch.empty(C, dtype=torch.float32, device=dev)
+    order = torch.empty(max(n_order, 0), dtype=torch.int32, device=dev)
+    oval = torch.empty(max(n_order, 0), dtype=torch.float32, device=dev)
+    nbytes = int(L.cs_beam_decode_workspace_size(A, B, vocab, k))
+    if workspace is None:
+        workspace = _decode_ws.setdefault(dev, Workspace(zeroed=True))
+    if not workspace.zeroed:
+        raise CSError("beam_decode_step needs a Workspace(zeroed=True) of its own (arrival counters)")
+    ws = workspace.get(nbytes, dev)
+    if kept_out is not None:
+        if (kept_out.dtype != torch.float32 or not kept_out.is_contiguous()
+                or tuple(kept_out.shape) != (A, n_order)):
+            raise CSError(f"kept_out must be a contiguous float32 [{A}, {n_order}] tensor")
+        _require_cuda(kept_out)
+    rc = L.cs_beam_decode_step(ref_logits.data_ptr(), ld_ref, logits.data_ptr(), ld,
+                               _DTYPE[logits.dtype], A, B, vocab, k, float(softcap),
+                               rewards.data_ptr(), int(kind), float(eps), ids.data_ptr(),
+                               U.data_ptr(), W.data_ptr(), n_order,
+                               order.data_ptr() if n_order else None,
+                               oval.data_ptr() if n_order else None,
+                               kept_out.data_ptr() if kept_out is not None else None,
+                               ws.data_ptr(), ws.numel(), _stream())
+    _lib.check(rc, "cs_beam_decode_step")
+    if n_order == 0:
+        return ids, U, W, None, None
+    return ids, U, W, order, oval
 
 
 def _logits_args(logits: torch.Tensor, vocab: Optional[int]):

@@ -178,6 +178,31 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
                  size_t workspace_bytes, cs_stream_t stream);
 
 /*
+ * cs_beam_decode_step — one whole beam-search decode step after the LM head in ONE
+ * launch: cs_vocab_topk on the B reference-policy rows (ref_logits [B][ld_ref]) proposes
+ * K candidate tokens per beam (out_ids [B][K], value desc / id asc), and cs_beam_step
+ * scores them under the agent rows (logits [A*B][ld]) — out_U, out_W, out_order,
+ * out_order_val, out_kept exactly as cs_beam_step with targets = out_ids.  The proposer
+ * workgroups run beside the agent-row stream; per beam the last of its A + 1 arrivals
+ * gathers the beam's candidates.  Bit-identical to cs_vocab_topk + cs_beam_step.
+ * Limits: K <= min(256, vocab), B*K <= 16384, A*B <= 65536, B <= 4096.
+ *
+ * WORKSPACE: cs_beam_decode_workspace_size() bytes, zero-filled before the first call,
+ * used by one stream at a time, left zeroed by every call (graph-replayable).
+ *
+ * Replaces: the reference's per-step loop of beam_search.py:439-560 — unique-token
+ *   sampling per beam (:199-333), per (beam, token, agent) scoring (:335-404, 495-538),
+ *   cumulative rewards and the stable sort by min over agents (:534-560).
+ */
+size_t cs_beam_decode_workspace_size(int32_t A, int32_t B, int64_t vocab, int32_t K);
+int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logits, int64_t ld,
+                        int dtype, int32_t A, int32_t B, int64_t vocab, int32_t K, float softcap,
+                        const float* rewards_in, int welfare_kind, float eps, int32_t* out_ids,
+                        float* out_U, float* out_W, int32_t n_order, int32_t* out_order,
+                        float* out_order_val, float* out_kept, void* workspace,
+                        size_t workspace_bytes, cs_stream_t stream);
+
+/*
  * cs_vocab_topk — deterministic candidate proposer: the k largest (soft-capped)
  * logits of every row, ordered by (value desc, token id asc).
  *

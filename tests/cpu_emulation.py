@@ -13,7 +13,7 @@ import oracle as orc
 
 PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
 NAMES = ("logsoftmax_gather", "segment_reduce", "welfare", "topk", "vocab_sample", "vocab_topk",
-         "beam_step")
+         "beam_step", "beam_decode_step")
 
 
 def _lsg(logits, targets, *, vocab=None, softcap=0.0, workspace=None, want_lse=False, **kw):
@@ -81,8 +81,17 @@ def _bs(logits, targets, rewards, kind="min", *, n_order=None, vocab=None, softc
     return U, W, order.to(torch.int32), val
 
 
+def _bd(ref_logits, logits, rewards, k, kind="min", *, n_order=None, vocab=None, softcap=0.0,
+        eps=1e-9, workspace=None, kept_out=None):
+    ids, _ = _vt(ref_logits, k, vocab=vocab, softcap=softcap)
+    ids = ids.to(torch.int32)
+    U, W, order, val = _bs(logits, ids, rewards, kind, n_order=n_order, vocab=vocab,
+                           softcap=softcap, eps=eps, kept_out=kept_out)
+    return ids, U, W, order, val
+
+
 _IMPL = {"logsoftmax_gather": _lsg, "segment_reduce": _seg, "welfare": _wel, "topk": _tk,
-         "vocab_sample": _vs, "vocab_topk": _vt, "beam_step": _bs}
+         "vocab_sample": _vs, "vocab_topk": _vt, "beam_step": _bs, "beam_decode_step": _bd}
 
 
 def install():

@@ -369,3 +369,35 @@ def test_vocab_topk_clustered_values(ops, orc, dev):
     ids, vals = ops.vocab_topk(x.to(dev), 64)
     o_ids, o_vals = orc.vocab_topk(x.double().numpy(), 64)
     assert np.array_equal(ids.cpu().numpy(), o_ids)
+
+
+@pytest.mark.parametrize("dtype,A,B,K,vocab,softcap,kind", [
+    (torch.float32, 4, 4, 10, 128256, 0.0, "min"),      # C1
+    (torch.bfloat16, 16, 16, 50, 256000, 30.0, "min"),  # C3
+    (torch.bfloat16, 64, 8, 32, 128256, 0.0, "min"),    # C5
+    (torch.bfloat16, 8, 3, 256, 70000, 0.0, "sum"),     # max K, split rows, fold path
+    (torch.float16, 5, 2, 7, 777, 0.0, "max"),          # one proposer chunk
+])
+def test_beam_decode_step_is_topk_plus_beam_step(ops, dev, dtype, A, B, K, vocab, softcap, kind):
+    """cs_beam_decode_step (proposer + scoring in one launch) is bit-identical to
+    cs_vocab_topk followed by cs_beam_step, for full and partial orders and kept rewards."""
+    g = torch.Generator(device=dev).manual_seed(A * 7 + B + K)
+    ref = (torch.randn(B, vocab, generator=g, device=dev) * 3.0).to(dtype)
+    ref[0, 11] = ref[0, 12] = ref[0].max()          # a tie at the top of beam 0
+    x = (torch.randn(A * B, vocab, generator=g, device=dev) * 3.0).to(dtype)
+    R = -torch.rand(A, B, generator=g, device=dev) * 30.0
+    ids, _ = ops.vocab_topk(ref, K, softcap=softcap)
+    U, W, o, v = ops.beam_step(x, ids, R, kind, softcap=softcap)
+    for rep in range(2):   # the workspace is reused (counters left at zero)
+        ids2, U2, W2, o2, v2 = ops.beam_decode_step(ref, x, R, K, kind, softcap=softcap)
+        assert torch.equal(ids, ids2)
+        assert torch.equal(torch.nan_to_num(U, nan=7.0), torch.nan_to_num(U2, nan=7.0))
+        assert torch.equal(torch.nan_to_num(W, nan=7.0), torch.nan_to_num(W2, nan=7.0))
+        assert torch.equal(o, o2)
+    n = min(B, B * K)
+    kept = torch.empty(A, n, device=dev) if B * K <= 1024 else None
+    _, _, _, on, _ = ops.beam_decode_step(ref, x, R, K, kind, n_order=n, softcap=softcap,
+                                          kept_out=kept)
+    assert torch.equal(on, o[:n])
+    if kept is not None:
+        assert torch.equal(kept, U[:, on.long()])

@@ -57,6 +57,18 @@ def main():
             return ops.beam_step(x, ids, R, "min", n_order=B, softcap=cap, workspace=wb)
 
         r["step_us"] = timed(serial)   # proposer + fused scoring step, top-B kept
+        wd = ops.Workspace(zeroed=True)
+        r["decode_us"] = timed(lambda: ops.beam_decode_step(ref, x, R, K, "min", n_order=B,
+                                                            softcap=cap, workspace=wd))
+        if "--sweep" in sys.argv:
+            for kp in (4, 16):
+                for rf in (0, 1):
+                    os.environ["CS_DECODE_KP"] = str(kp)
+                    os.environ["CS_DECODE_ROWS_FIRST"] = str(rf)
+                    r[f"decode_kp{kp}_rf{rf}_us"] = timed(lambda: ops.beam_decode_step(
+                        ref, x, R, K, "min", n_order=B, softcap=cap, workspace=wd))
+            os.environ.pop("CS_DECODE_KP")
+            os.environ.pop("CS_DECODE_ROWS_FIRST")
         r["bytes"] = A * B * V * x.element_size()
         r["ideal_us"] = r["bytes"] / 8e12 * 1e6
         print(json.dumps(r), flush=True)

@@ -17,7 +17,7 @@ OUT = os.path.join(REPO, "tools", "libcs_trace.so")
 if "--build" in sys.argv:
     src = os.path.join(REPO, PKG, "csrc", "consensus_scoring.hip")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17",
-                           "-ffp-contract=off", "-DCS_TRACE_BEAM", "-DCS_TRACE_TOPK", "-shared", "-fPIC", "-I",
+                           "-ffp-contract=off", "-DCS_TRACE_DECODE", "-shared", "-fPIC", "-I",
                            os.path.join(REPO, "include"), "-o", OUT, src])
     sys.exit(0)
 
@@ -37,7 +37,7 @@ for name, (A, B, K, V, cap, dt) in {"c1": (4, 4, 10, 128256, 0.0, torch.float32)
         ops.beam_step(x, t, R, "min", softcap=cap, workspace=wb)
         torch.cuda.synchronize()
     ref = (torch.randn(B, V, generator=g, device=dev) * 3).to(dt)
-    for i in range(2):
-        ops.vocab_topk(ref, K, softcap=cap)
+    for i in range(3):
+        ops.beam_decode_step(ref, x, R, K, "min", n_order=B, softcap=cap)
         torch.cuda.synchronize()
     print(name, "done", flush=True)
