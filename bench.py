@@ -247,12 +247,11 @@ def run_beam(name, world, rank, dev, steps, warmup):
                                                      softcap=cap, workspace=ws_d,
                                                      kept_out=Rs[(i + 1) % 2])
             return U, W, order
-        # sharded: every rank proposes the same candidates; W is all-reduced before the
-        # selection
-        ids, _ = ops.vocab_topk(ref, K, softcap=cap, workspace=ws_p)
-        U, W, order, _ = ops.beam_step(ag, ids, Rs[i % 2], "min", n_order=0, softcap=cap,
-                                       workspace=ws_b)
-        return U, W, order
+        # sharded: every rank proposes the same candidates (same launch, no order); W is
+        # all-reduced before the selection
+        _, U, W, _, _ = ops.beam_decode_step(ref, ag, Rs[i % 2], K, "min", n_order=0,
+                                             softcap=cap, workspace=ws_d)
+        return U, W, None
 
     def keep(U, order):
         R.copy_(U.index_select(1, order[:B].long()))
@@ -308,34 +307,32 @@ def run_beam(name, world, rank, dev, steps, warmup):
         el = float(tt.item())
 
     # kernel-level timing (HIP events on the launch stream), eager: the one launch of a
-    # step at N = 1 (cs_beam_decode_step), cs_beam_step when sharded
+    # step (cs_beam_decode_step; no order when sharded)
     st = torch.cuda.current_stream()
     n_ev = 50
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(n_ev)]
-    ids, _ = ops.vocab_topk(ref, K, softcap=cap, workspace=ws_p)
     gpu_busy(st)   # the host enqueues every launch before the GPU reaches the first event
     for e0, e1 in ev:
         e0.record(st)
-        if A_loc and not sharded:
-            ops.beam_decode_step(ref, ag, Rs[0], K, "min", n_order=B, softcap=cap,
-                                 workspace=ws_d, kept_out=Rs[1])
-        elif A_loc:
-            ops.beam_step(ag, ids, Rs[0], "min", n_order=0, softcap=cap, workspace=ws_b)
+        if A_loc:
+            ops.beam_decode_step(ref, ag, Rs[0], K, "min", n_order=0 if sharded else B,
+                                 softcap=cap, workspace=ws_d,
+                                 kept_out=None if sharded else Rs[1])
         e1.record(st)
     torch.cuda.synchronize()
     k_ms = max(float(np.median([a.elapsed_time(b) for a, b in ev])), 1e-6)
     esz = torch.finfo(dt).bits // 8
-    alg = (A_loc * B + (0 if sharded else B)) * V * esz   # agent rows (+ proposer rows)
+    alg = (A_loc * B + B) * V * esz   # agent rows + proposer rows
     ms = el * 1000.0 / steps
     return {"workload": desc, "agents": A, "agents_per_gpu": A_loc, "beams": B, "top_k": K,
             "vocab": V, "dtype": str(dt).replace("torch.", ""),
             "decode_steps_per_s": 1000.0 / ms, "ms_per_step": ms,
             "scorings_per_s": A * C / (ms * 1e-3), "steps": steps,
             "timing": "hipGraph replay" + (" + eager RCCL all-reduce" if sharded else ""),
-            "roofline": {"bound": "hbm", "kernel": ("cs_beam_step (beam_step_kernel)" if sharded else
-                                    "cs_beam_decode_step (beam_decode_kernel: proposer + "
-                                    "vocab stream + gather + welfare + top-B)"),
+            "roofline": {"bound": "hbm", "kernel": ("cs_beam_decode_step (beam_decode_kernel: proposer + "
+                                    "vocab stream + gather + welfare" +
+                                    ("" if sharded else " + top-B") + ")"),
                          "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
                          "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
