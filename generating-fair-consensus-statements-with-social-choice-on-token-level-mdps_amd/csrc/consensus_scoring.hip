@@ -1054,6 +1054,13 @@ __device__ __forceinline__ uint32_t arrive(uint32_t* cnt) {
   return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Hand-off regions are padded so that every 128-byte line is read by ONE consumer
+// workgroup, after all of it is published: a line is never in an L2 (per XCD) before its
+// consumer's first read of it in the launch.
+__host__ __device__ constexpr int64_t pad_line(int64_t n, int64_t elt_bytes) {
+  return (n * elt_bytes + 127) / 128 * 128 / elt_bytes;
+}
+
 constexpr int kFusedSort = 1024;      // candidates sorted inside the launch
 constexpr int kSelectMax = 256;       // n_order up to this: threshold selection, no full sort
 constexpr int kBeamMaxRows = 65536;   // A * B (one arrival counter per row)
@@ -1240,7 +1247,7 @@ __device__ __forceinline__ void beam_tail(const BeamLds& L, uint32_t* Uw, uint32
   if (order_free) {
     for (int32_t c = tid; c < C; c += BLOCK) {
       const float w = welfare_from_key(ld_sc1(wkey + c), is_min);
-      wkey[c] = 0u;  // leave the workspace zeroed for the next call
+      st_sc1(wkey + c, 0u);  // leave the workspace zeroed for the next call
       W[c] = w;
       if (sort_here) sm_w[c] = w;
     }
@@ -1374,7 +1381,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   // 2. row finish by the row's last arriver
   if (nsplit > 1) {
     if (tid == 0) {
-      st_sc1(part + item, (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
+      st_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + split,
+             (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
                               __float_as_uint(ms.x));
       wait_stores();
       sm_last = arrive(&row_cnt[row]) == static_cast<uint32_t>(nsplit - 1);
@@ -1384,14 +1392,14 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
     if (tid < 64) {
       float m = -INFINITY, s = 0.0f;
       for (int j = tid; j < nsplit; j += 64) {
-        const unsigned long long p = ld_sc1(part + static_cast<int64_t>(row) * nsplit + j);
+        const unsigned long long p = ld_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + j);
         lse_merge(m, s, __uint_as_float(static_cast<uint32_t>(p)),
                   __uint_as_float(static_cast<uint32_t>(p >> 32)));
       }
       wave_lse_reduce(m, s);
       if (tid == 0) {
         sm_lse = m + logf(s);
-        row_cnt[row] = 0u;
+        st_sc1(row_cnt + row, 0u);
       }
     }
   } else if (tid == 0) {
@@ -1428,7 +1436,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   if (tid == 0) sm_last = arrive(done_cnt) == static_cast<uint32_t>(rows - 1);
   __syncthreads();
   if (!sm_last) return;  // block-uniform
-  if (tid == 0) *done_cnt = 0u;
+  if (tid == 0) st_sc1(done_cnt, 0u);
   beam_tail<BLOCK>(L, Uw, wkey, W, A, C, kind, eps, n_order, n2, out_order, out_val, out_kept);
 }
 
@@ -1481,7 +1489,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     unsigned long long* __restrict__ ppart, uint32_t* __restrict__ row_cnt,
     uint32_t* __restrict__ prop_cnt, uint32_t* __restrict__ beam_cnt,
     uint32_t* __restrict__ done_cnt, uint32_t* __restrict__ wkey, uint32_t* __restrict__ lse_ws,
-    int32_t* __restrict__ out_ids, float* __restrict__ U, float* __restrict__ W, int32_t n_order,
+    uint32_t* __restrict__ ids_ws, int32_t* __restrict__ out_ids, float* __restrict__ U, float* __restrict__ W, int32_t n_order,
     int32_t n2, int32_t* __restrict__ out_order, float* __restrict__ out_val,
     float* __restrict__ out_kept) {
   __shared__ float sm_m[BLOCK / 64];
@@ -1504,7 +1512,6 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   const bool is_min = kind == CS_WELFARE_MIN;
   const bool order_free = kind == CS_WELFARE_MIN || kind == CS_WELFARE_MAX;
   uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
-  uint32_t* ids_w = reinterpret_cast<uint32_t*>(out_ids);
   DEC_T(const unsigned long long q0 = wall_clock64(); if (tid == 0) atomicMin(&g_dec_t0, q0);)
   int32_t gb;  // the beam this block arrives at
 
@@ -1548,7 +1555,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
       if (key[j] && (key[j] >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = key[j];
     __syncthreads();
     const int32_t nkeys = nchunk_p * K;
-    unsigned long long* pr = ppart + static_cast<int64_t>(b) * nkeys;
+    unsigned long long* pr = ppart + static_cast<int64_t>(b) * pad_line(nkeys, 8);
     unsigned long long* out = pr + static_cast<int64_t>(chunk) * K;
     const int nc = static_cast<int>(sm_n);
     rank_candidates<BLOCK>(sel_cand, nc, K, [&](int r, unsigned long long kc) { st_sc1(out + r, kc); });
@@ -1561,7 +1568,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     }
     __syncthreads();
     if (!sm_last) return;  // block-uniform
-    if (tid == 0) prop_cnt[b] = 0u;
+    if (tid == 0) st_sc1(prop_cnt + b, 0u);
     // the beam's K best among the chunk winners -> its candidate ids
     const RadixCut mcut = radix_select<BLOCK>(
         [&](auto f) {
@@ -1578,9 +1585,14 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     __syncthreads();
     const int mc = static_cast<int>(sm_n);
     rank_candidates<BLOCK>(sel_cand, mc, K, [&](int r, unsigned long long c) {
-      st_sc1(ids_w + b * K + r, 0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull));
+      const uint32_t id = 0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull);
+      st_sc1(ids_ws + b * pad_line(K, 4) + r, id);
+      out_ids[b * K + r] = static_cast<int32_t>(id);
     });
-    for (int r = mc + tid; r < K; r += BLOCK) st_sc1(ids_w + b * K + r, 0xffffffffu);
+    for (int r = mc + tid; r < K; r += BLOCK) {
+      st_sc1(ids_ws + b * pad_line(K, 4) + r, 0xffffffffu);
+      out_ids[b * K + r] = -1;
+    }
     DEC_T(if (tid == 0 && b == 0) printf("DEC proposer merge done b0 at %llu (start %llu)\n", wall_clock64() - g_dec_t0, q0 - g_dec_t0);)
     gb = b;
   } else {
@@ -1595,7 +1607,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
         block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
     if (nsplit > 1) {
       if (tid == 0) {
-        st_sc1(part + item, (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
+        st_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + split,
+               (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
                                 __float_as_uint(ms.x));
         wait_stores();
         sm_last = arrive(&row_cnt[row]) == static_cast<uint32_t>(nsplit - 1);
@@ -1605,18 +1618,18 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
       if (tid < 64) {
         float m = -INFINITY, sum = 0.0f;
         for (int j = tid; j < nsplit; j += 64) {
-          const unsigned long long pv = ld_sc1(part + static_cast<int64_t>(row) * nsplit + j);
+          const unsigned long long pv = ld_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + j);
           lse_merge(m, sum, __uint_as_float(static_cast<uint32_t>(pv)),
                     __uint_as_float(static_cast<uint32_t>(pv >> 32)));
         }
         wave_lse_reduce(m, sum);
         if (tid == 0) {
-          st_sc1(lse_ws + row, __float_as_uint(m + logf(sum)));
-          row_cnt[row] = 0u;
+          st_sc1(lse_ws + (row % B) * pad_line(A, 4) + row / B, __float_as_uint(m + logf(sum)));
+          st_sc1(row_cnt + row, 0u);
         }
       }
     } else if (tid == 0) {
-      st_sc1(lse_ws + row, __float_as_uint(ms.x + logf(ms.y)));
+      st_sc1(lse_ws + (row % B) * pad_line(A, 4) + row / B, __float_as_uint(ms.x + logf(ms.y)));
     }
     gb = row % B;
     DEC_T(if (tid == 0 && (row == 0 || row == A * B - 1)) printf("DEC row %d stream start %llu done %llu\n", row, q0 - g_dec_t0, wall_clock64() - g_dec_t0);)
@@ -1628,13 +1641,13 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   if (tid == 0) sm_last = arrive(&beam_cnt[gb]) == static_cast<uint32_t>(A);
   __syncthreads();
   if (!sm_last) return;  // block-uniform
-  if (tid == 0) beam_cnt[gb] = 0u;
+  if (tid == 0) st_sc1(beam_cnt + gb, 0u);
   for (int32_t i = tid; i < A * K; i += BLOCK) {
     const int32_t a = i / K;
     const int32_t j = i - a * K;
     const int32_t row = a * B + gb;
-    const int32_t t = static_cast<int32_t>(ld_sc1(ids_w + gb * K + j));
-    const float lse = __uint_as_float(ld_sc1(lse_ws + row));
+    const int32_t t = static_cast<int32_t>(ld_sc1(ids_ws + gb * pad_line(K, 4) + j));
+    const float lse = __uint_as_float(ld_sc1(lse_ws + gb * pad_line(A, 4) + a));
     float lp = __builtin_nanf("");
     if (t >= 0 && t < vocab) {
       float x = load_one<DT>(logits + row * ld_bytes, t);
@@ -1652,7 +1665,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   if (tid == 0) sm_last = arrive(done_cnt) == static_cast<uint32_t>(B - 1);
   __syncthreads();
   if (!sm_last) return;  // block-uniform
-  if (tid == 0) *done_cnt = 0u;
+  if (tid == 0) st_sc1(done_cnt, 0u);
   DEC_T(const unsigned long long q8 = wall_clock64();)
   beam_tail<BLOCK>(L, Uw, wkey, W, A, C, kind, eps, n_order, n2, out_order, out_val, out_kept);
   DEC_T(if (tid == 0) { printf("DEC last gather+done at %llu, tail end %llu\n", q8 - g_dec_t0, wall_clock64() - g_dec_t0); g_dec_t0 = ~0ull; })
@@ -1796,7 +1809,7 @@ size_t cs_beam_step_workspace_size(int64_t rows, int64_t vocab) {
   const SplitPlan p = plan_split(rows, vocab, CS_BF16);
   const SplitPlan q = plan_split(rows, vocab, CS_F32);
   const int64_t ns = p.nsplit > q.nsplit ? p.nsplit : q.nsplit;
-  return kBeamCounterBytes + static_cast<size_t>(rows) * ns * sizeof(unsigned long long);
+  return kBeamCounterBytes + static_cast<size_t>(rows) * pad_line(ns, 8) * sizeof(unsigned long long);
 }
 
 int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vocab, int64_t ld,
@@ -1826,7 +1839,8 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
   if (reinterpret_cast<uintptr_t>(logits) % elt_size(dtype) != 0)
     return fail(CS_ERR_INVALID, "cs_beam_step: logits not element-aligned");
   const SplitPlan plan = plan_split(rows, vocab, dtype);
-  const size_t need = kBeamCounterBytes + static_cast<size_t>(rows) * plan.nsplit * sizeof(unsigned long long);
+  const size_t need = kBeamCounterBytes + static_cast<size_t>(rows) * pad_line(plan.nsplit, 8) *
+                                              sizeof(unsigned long long);
   if (!workspace || workspace_bytes < need)
     return fail(CS_ERR_WORKSPACE, "cs_beam_step: workspace smaller than cs_beam_step_workspace_size()");
   if (reinterpret_cast<uintptr_t>(workspace) % 8 != 0)
@@ -1891,7 +1905,7 @@ struct DecodeLayout {
   int32_t block;
   int32_t kp;
   int32_t nchunk_p;
-  size_t lse_off, ppart_off, part_off, total;
+  size_t lse_off, ids_off, ppart_off, part_off, total;
 };
 DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int dtype) {
   DecodeLayout d;
@@ -1902,9 +1916,12 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   const int64_t ch = static_cast<int64_t>(d.kp) * d.block;
   d.nchunk_p = static_cast<int32_t>((vocab + ch - 1) / ch);
   d.lse_off = kBeamCounterBytes + 2 * sizeof(uint32_t) * kBeamMaxBeams;
-  d.ppart_off = (d.lse_off + sizeof(uint32_t) * rows + 7) / 8 * 8;
-  d.part_off = d.ppart_off + sizeof(unsigned long long) * static_cast<size_t>(B) * d.nchunk_p * K;
-  d.total = d.part_off + sizeof(unsigned long long) * static_cast<size_t>(rows) * d.plan.nsplit;
+  d.ids_off = d.lse_off + sizeof(uint32_t) * static_cast<size_t>(B) * pad_line(A, 4);
+  d.ppart_off = d.ids_off + sizeof(uint32_t) * static_cast<size_t>(B) * pad_line(K, 4);
+  d.part_off = d.ppart_off + sizeof(unsigned long long) * static_cast<size_t>(B) *
+                                 pad_line(static_cast<int64_t>(d.nchunk_p) * K, 8);
+  d.total = d.part_off + sizeof(unsigned long long) * static_cast<size_t>(rows) *
+                             pad_line(d.plan.nsplit, 8);
   return d;
 }
 }  // namespace
@@ -1962,6 +1979,7 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
   auto* prop_cnt = reinterpret_cast<uint32_t*>(wsb + kBeamCounterBytes);
   auto* beam_cnt = prop_cnt + kBeamMaxBeams;
   auto* lse_ws = reinterpret_cast<uint32_t*>(wsb + d.lse_off);
+  auto* ids_ws = reinterpret_cast<uint32_t*>(wsb + d.ids_off);
   auto* ppart = reinterpret_cast<unsigned long long*>(wsb + d.ppart_off);
   auto* part = reinterpret_cast<unsigned long long*>(wsb + d.part_off);
   const int64_t esz = elt_size(dtype);
@@ -1979,7 +1997,7 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
                      st, rg, ld_ref * esz, d.nchunk_p, rows_first, lg, vocab, ld * esz,            \
                      d.plan.nsplit, d.plan.split_len, A, B, K, rewards_in, softcap, inv_cap,       \
                      welfare_kind, static_cast<double>(eps), part, ppart, row_cnt, prop_cnt,       \
-                     beam_cnt, done_cnt, wkey, lse_ws, out_ids, out_U, out_W, n_order, n2,         \
+                     beam_cnt, done_cnt, wkey, lse_ws, ids_ws, out_ids, out_U, out_W, n_order, n2, \
                      out_order, out_order_val, out_kept)
 #define CS_DECODE_LAUNCH(DTV, CAPV, FIXV)                                                          \
   do {                                                                                             \

@@ -401,3 +401,31 @@ def test_beam_decode_step_is_topk_plus_beam_step(ops, dev, dtype, A, B, K, vocab
     assert torch.equal(on, o[:n])
     if kept is not None:
         assert torch.equal(kept, U[:, on.long()])
+
+
+def test_fused_beam_launches_stress_shared_workspace(ops, dev):
+    """Hand-offs under repetition: 40 fused decode / beam launches of alternating shapes on
+    ONE workspace (counters must return to zero every call), each checked word for word
+    against the unfused kernels, with a large stream kernel queued in between so that the
+    launches start on a busy device."""
+    shapes = [(16, 16, 50, 64000, 30.0, torch.bfloat16), (64, 8, 32, 32000, 0.0, torch.bfloat16),
+              (4, 4, 10, 128256, 0.0, torch.float32)]
+    g = torch.Generator(device=dev).manual_seed(77)
+    data = []
+    for A, B, K, V, cap, dt in shapes:
+        ref = (torch.randn(B, V, generator=g, device=dev) * 3.0).to(dt)
+        x = (torch.randn(A * B, V, generator=g, device=dev) * 3.0).to(dt)
+        ids, _ = ops.vocab_topk(ref, K, softcap=cap)
+        data.append((A, B, K, cap, ref, x, ids))
+    busy = torch.randn(8192, 32000, device=dev, dtype=torch.bfloat16)
+    wd, wb = ops.Workspace(zeroed=True), ops.Workspace(zeroed=True)
+    for it in range(40):
+        A, B, K, cap, ref, x, ids = data[it % len(data)]
+        R = -torch.rand(A, B, generator=g, device=dev) * (1 + it)
+        ops.logsoftmax_gather(busy, None, want_lse=True)       # uneven load ahead
+        U, W, o, _ = ops.beam_step(x, ids, R, "min", softcap=cap, workspace=wb)
+        ids2, U2, W2, o2, _ = ops.beam_decode_step(ref, x, R, K, "min", softcap=cap,
+                                                   workspace=wd, n_order=B * K if it % 2 else B)
+        assert torch.equal(ids, ids2), it
+        assert torch.equal(U, U2) and torch.equal(W, W2), it
+        assert torch.equal(o[:o2.numel()], o2), it
