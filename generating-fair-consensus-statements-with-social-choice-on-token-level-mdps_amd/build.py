@@ -1,12 +1,18 @@
-"""In-tree build of the gfx950 HIP library (no JIT cache: the .so travels with the repo)."""
+"""In-tree build of the gfx950 HIP library (no JIT cache: the .so travels with the repo).
+
+Four translation units (csrc/*.hip, sharing csrc/cs_kernels.cuh) compile in parallel to
+objects, then link into libconsensus_scoring.so."""
 from __future__ import annotations
 
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
-SOURCES = [os.path.join(_HERE, "csrc", "consensus_scoring.hip")]
+_CSRC = os.path.join(_HERE, "csrc")
+SOURCES = [os.path.join(_CSRC, n) for n in ("stream.hip", "fold.hip", "proposer.hip", "beam.hip")]
+HEADERS = [os.path.join(_CSRC, "cs_kernels.cuh"), os.path.join(_REPO, "include", "consensus_scoring.h")]
 OUT = os.path.join(_HERE, "libconsensus_scoring.so")
 ARCH = os.environ.get("CS_OFFLOAD_ARCH", "gfx950")
 
@@ -15,23 +21,36 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + [os.path.join(_REPO, "include", "consensus_scoring.h")]
-    return any(os.path.getmtime(s) > t for s in deps)
+    return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
+
+
+def _flags():
+    # -ffp-contract=off: every FMA in the kernels is an explicit fmaf, so kernels that
+    # share a formula (lse, gather, soft-cap) round identically wherever they are inlined
+    return ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC",
+            "-I", os.path.join(_REPO, "include"), "-I", _CSRC]
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    # -ffp-contract=off: every FMA in the kernels is an explicit fmaf, so kernels that
-    # share a formula (lse, gather, soft-cap) round identically wherever they are inlined
-    cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-shared",
-           "-fPIC",
-           "-I", os.path.join(_REPO, "include"), "-o", OUT + ".tmp"] + SOURCES
+    objs = [OUT + "." + os.path.basename(s) + ".o" for s in SOURCES]
+    cmds = [[hipcc] + _flags() + ["-c", s, "-o", o] for s, o in zip(SOURCES, objs)]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        for c in cmds:
+            print(" ".join(c))
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(jobs) as ex:
+        for r in ex.map(lambda c: subprocess.run(c, check=True), cmds):
+            pass
+    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+    if verbose:
+        print(" ".join(link))
+    subprocess.run(link, check=True)
     os.replace(OUT + ".tmp", OUT)
+    for o in objs:
+        os.remove(o)
     return OUT
 
 

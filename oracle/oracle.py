@@ -163,7 +163,7 @@ _M64 = (1 << 64) - 1
 
 def cs_uniform(seed: int, v: np.ndarray) -> np.ndarray:
     """u(seed, v) in (0, 1): splitmix64 finaliser of (seed, v), top 23 bits + 0.5 over 2^23.
-    Exactly the device function cs_uniform in csrc/consensus_scoring.hip."""
+    Exactly the device function cs_uniform in csrc/proposer.hip."""
     with np.errstate(over="ignore"):
         x = (np.uint64(seed & _M64) * np.uint64(0x9E3779B97F4A7C15)
              + (np.asarray(v, dtype=np.uint64) + np.uint64(1)) * np.uint64(0xD1B54A32D192ED03))

@@ -15,10 +15,9 @@ PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-md
 OUT = os.path.join(REPO, "tools", "libcs_trace.so")
 
 if "--build" in sys.argv:
-    src = os.path.join(REPO, PKG, "csrc", "consensus_scoring.hip")
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17",
-                           "-ffp-contract=off", "-DCS_TRACE_DECODE", "-shared", "-fPIC", "-I",
-                           os.path.join(REPO, "include"), "-o", OUT, src])
+    bld = importlib.import_module(PKG + ".build")
+    subprocess.check_call(["/opt/rocm/bin/hipcc"] + bld._flags() +
+                          ["-DCS_TRACE_DECODE", "-DCS_TRACE_TOPK", "-shared", "-o", OUT] + bld.SOURCES)
     sys.exit(0)
 
 _lib = importlib.import_module(PKG + "._lib")
