@@ -45,7 +45,30 @@ CONFIGS = {
     "c4": (32, 256, 4, 128_256, "sumlog",
            "C4 finite_lookahead depth 4: R=256 paths x A=32 agents per GPU, "
            "Llama-3.1-8B vocab 128256 bf16 logits, Nash welfare"),
+    # the same C4 scorings with the paths' shared prefixes scored once (the method's
+    # engine.score_tree): a full 4-ary depth-4 tree has 4+16+64+256 = 340 nodes per
+    # agent instead of 256 x 4 path rows
+    "c4tree": (32, 256, 4, 128_256, "sumlog",
+               "C4 finite_lookahead depth 4, tree-shared rows: R=256 paths (4-ary, depth 4, "
+               "340 nodes) x A=32 agents per GPU, Llama-3.1-8B vocab 128256 bf16 logits, "
+               "Nash welfare"),
 }
+
+
+def tree_layout(bf, depth, A, dev):
+    """Full bf-ary tree of the given depth, nodes in level order: (nodes per agent, flat
+    row index [A * leaves * depth] of every path's nodes, agent-major, path-major)."""
+    levels = [bf ** (d + 1) for d in range(depth)]
+    start = [sum(levels[:d]) for d in range(depth)]
+    n_nodes = sum(levels)
+    leaves = levels[-1]
+    idx = []
+    for p in range(leaves):
+        for d in range(depth):
+            idx.append(start[d] + p // (bf ** (depth - 1 - d)))
+    per_agent = torch.as_tensor(idx, dtype=torch.long, device=dev)
+    flat = (torch.arange(A, device=dev)[:, None] * n_nodes + per_agent[None]).reshape(-1)
+    return n_nodes, flat
 
 
 # Beam-search decode steps (BASELINE configs C1, C3, C5).  Total agents are fixed per
@@ -360,8 +383,16 @@ def main():
     par = importlib.import_module(PKG_DIR + ".parallel")
 
     A, N, T, V, wkind, desc = CONFIGS[args.config]
-    rows = A * N * T
-    logits, tgt, offsets = make_inputs(A, N, T, V, 1234 + rank, dev)
+    tree = args.config.endswith("tree")
+    flat = None
+    if tree:   # rows = tree nodes; each path's log-probs are gathered from its nodes
+        n_nodes, flat = tree_layout(4, T, A, dev)
+        rows = A * n_nodes
+        logits, tgt, _ = make_inputs(A, n_nodes, 1, V, 1234 + rank, dev)
+        offsets = torch.arange(0, A * N * T + 1, T, dtype=torch.int32, device=dev)
+    else:
+        rows = A * N * T
+        logits, tgt, offsets = make_inputs(A, N, T, V, 1234 + rank, dev)
     ws = ops.Workspace()
     stream = torch.cuda.current_stream()
     shard = par.AgentShard(A * world, rank, world)   # A agents per GPU, round-robin
@@ -372,6 +403,8 @@ def main():
         tok, _ = ops.logsoftmax_gather(logits, tgt, workspace=ws)
         if ev is not None:
             ev[1].record(stream)
+        if flat is not None:
+            tok = tok.view(-1).index_select(0, flat)
         seg = ops.segment_reduce(tok, offsets)
         U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N)
         if wkind == "sumlog":
@@ -409,10 +442,10 @@ def main():
         alg_bytes = rows * V * 2 + rows * 4 * 2  # logits read once + targets in + lp out
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         cpu = None
-        if world == 1 and args.cpu_seconds > 0:
+        if world == 1 and args.cpu_seconds > 0 and not tree:
             cpu = cpu_baseline(A, N, T, V, wkind, args.cpu_seconds)
         e2e = None
-        if args.e2e and world == 1:
+        if args.e2e and world == 1 and not tree:
             del logits
             torch.cuda.empty_cache()
             e2e = end_to_end(A, N, T, V, wkind, dev)

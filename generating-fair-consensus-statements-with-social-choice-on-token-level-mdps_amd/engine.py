@@ -177,6 +177,53 @@ class ScoringEngine:
         out.copy_(tok.view(-1))
         del flat_h, flat_t
 
+    @torch.no_grad()
+    def score_tree(self, cache: PrefixCache, owner: Sequence[int], tokens: Sequence[int],
+                   parents: Sequence[int]) -> torch.Tensor:
+        """Log-probs of every node of ONE token tree under each owner's prefix.
+
+        tokens[i] is node i's token, parents[i] its parent node (< i) or -1 for a child of
+        the prefix.  Node i's log-prob is log p(tokens[i] | prefix, ancestors of i): every
+        node is scored once however many paths share it (a path's log-probs are its
+        nodes'), in one extend over all nodes with a tree attention mask (ancestors and
+        self), one logits row per node, cs_logsoftmax_gather.  Returns [len(owner), N]."""
+        dev = self.device
+        R, N = len(owner), len(tokens)
+        if N == 0:
+            return torch.empty(R, 0, dtype=torch.float32, device=dev)
+        depth = [0] * N
+        anc = torch.zeros(N, N, dtype=torch.bool)
+        for i, p in enumerate(parents):
+            if p >= i:
+                raise ValueError("parents must precede their children")
+            depth[i] = 0 if p < 0 else depth[p] + 1
+            if p >= 0:
+                anc[i] = anc[p]
+            anc[i, i] = True
+        own = torch.as_tensor(list(owner), dtype=torch.long, device=dev)
+        toks = torch.as_tensor(list(tokens), dtype=torch.long, device=dev)[None].expand(R, N)
+        last = cache.last_hidden[own]                                   # [R, d]
+        # only internal nodes (some node's parent) need a forward: their outputs predict
+        # their children; leaves are scored from their parent's row
+        internal = sorted({p for p in parents if p >= 0})
+        slot = {n: j + 1 for j, n in enumerate(internal)}               # 0 = the prefix
+        par_slot = torch.as_tensor([slot.get(p, 0) for p in parents], dtype=torch.long,
+                                   device=dev)
+        if internal:
+            ii = torch.as_tensor(internal, dtype=torch.long)
+            it = toks[:, ii.to(dev)]
+            pos = cache.lengths[own][:, None] + torch.as_tensor([depth[n] for n in internal],
+                                                                device=dev)[None]
+            ctx = [(k[own], v[own]) for k, v in cache.kv]
+            h, _ = self.model.extend(it, pos, ctx, cache.valid[own], cache.pos[own],
+                                     self_mask=anc[ii][:, ii].to(dev))
+            hpad = torch.cat([last[:, None, :], h], dim=1)
+            rows_h = hpad[:, par_slot]                                  # [R, N, d]
+        else:
+            rows_h = last[:, None, :].expand(R, N, last.shape[-1])
+        tgt = toks.reshape(R * N, 1).to(torch.int32)
+        return self.rows_logprobs(rows_h.reshape(R * N, -1), tgt).view(R, N)
+
     @staticmethod
     def offsets(conts: Sequence[Sequence[int]], device) -> torch.Tensor:
         off = [0]

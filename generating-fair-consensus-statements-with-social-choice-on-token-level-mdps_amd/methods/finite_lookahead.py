@@ -10,8 +10,12 @@ Per committed token (finite_lookahead.py:99-153):
      forward and one cs_vocab_sample launch (b draws per node row).
   2. For every (path, agent): mean of the last len(path) user-span log-probs of
      agent_user + statement + path (:490-520); best path = first max of the min over
-     agents (:527).  Here: all (agent, path) continuations in one batched scoring
-     pass, cs_segment_reduce, cs_welfare_reduce(MIN), cs_segmented_topk(k=1).
+     agents (:527).  Here: the paths form a token tree; every tree node is scored ONCE
+     per agent (engine.score_tree: one extend over the internal nodes with a tree
+     attention mask, one logits row per node, cs_logsoftmax_gather), each path's
+     log-probs are its nodes' (cs_segment_reduce over the path -> node lists), then
+     cs_welfare_reduce(MIN), cs_segmented_topk(k=1).  A depth-d, branching-b tree needs
+     b + ... + b^d rows per agent instead of d * b^d.
   3. Commit the best path's first token; stop on "DONE" / newline tokens (:141-144).
 
 Reference quirk kept: a one-token draw that hits an end-of-sequence token returns
@@ -122,10 +126,33 @@ class FiniteLookaheadGenerator(BaseGenerator):
                     for op in agent_opinions.values()]
         cache = engine.prefill(prefixes)
         A, R = len(prefixes), len(paths)
-        owner = [a for a in range(A) for _ in range(R)]
-        conts = [paths[p][1] for _ in range(A) for p in range(R)]
-        lp = engine.score(cache, owner, conts)
-        seg = ops.segment_reduce(lp, engine.offsets(conts, engine.device))
+        # the paths form a token tree: every node is scored once per agent (shared
+        # prefixes of the lookahead paths are not re-scored), then each path's log-probs
+        # are its nodes'
+        node_of, tokens, parents, path_nodes = {}, [], [], []
+        for _strs, ids in paths:
+            cur, lst = -1, []
+            for t in range(len(ids)):
+                key = tuple(ids[:t + 1])
+                if key not in node_of:
+                    node_of[key] = len(tokens)
+                    tokens.append(ids[t])
+                    parents.append(cur)
+                cur = node_of[key]
+                lst.append(cur)
+            path_nodes.append(lst)
+        dev = engine.device
+        node_lp = engine.score_tree(cache, list(range(A)), tokens, parents)   # [A, N]
+        flat = [n for lst in path_nodes for n in lst]
+        total = len(flat)
+        lp = node_lp[:, torch.as_tensor(flat, dtype=torch.long, device=dev)].contiguous()
+        offs = [0]
+        for a in range(A):
+            for lst in path_nodes:
+                offs.append(offs[-1] + len(lst))
+        seg = ops.segment_reduce(lp.reshape(-1), torch.as_tensor(offs, dtype=torch.int32,
+                                                                  device=dev))
+        assert offs[-1] == A * total
         sums = seg["sum_lp"].view(A, R).double()
         cnt = seg["count"].view(A, R).double()
         # empty path elements: the last len(path) span log-probs reach into the prefix

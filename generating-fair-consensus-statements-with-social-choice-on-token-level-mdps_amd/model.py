@@ -202,11 +202,13 @@ class Model:
             return p @ v
         return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=scale)
 
-    def _layer(self, i, h, pos, ctx_k, ctx_v, ctx_mask, ctx_pos, self_causal=True):
+    def _layer(self, i, h, pos, ctx_k, ctx_v, ctx_mask, ctx_pos, self_mask=None):
         """One decoder layer over new tokens h [B,T,d] at positions pos [B,T].
 
         ctx_k/ctx_v [B,Hkv,S,D] is the earlier context (prefix + history), visible
-        where ctx_mask [B,S] is True.  Returns (h, k_new, v_new)."""
+        where ctx_mask [B,S] is True.  The new tokens see each other causally, or through
+        self_mask [T,T] (True = attend; e.g. a token tree: ancestors and self).
+        Returns (h, k_new, v_new)."""
         c = self.cfg
         p = f"l{i}."
         B, T, _ = h.shape
@@ -216,7 +218,8 @@ class Model:
         v = (x @ self.w[p + "wv"].t()).view(B, T, c.n_kv_heads, c.head_dim).transpose(1, 2)
         q = self._rope(q, pos)
         k = self._rope(k, pos)
-        causal = torch.ones(T, T, dtype=torch.bool, device=h.device).tril()
+        causal = (torch.ones(T, T, dtype=torch.bool, device=h.device).tril()
+                  if self_mask is None else self_mask)
         if ctx_k is not None:
             K = torch.cat([ctx_k, k], dim=2)
             V = torch.cat([ctx_v, v], dim=2)
@@ -256,14 +259,15 @@ class Model:
 
     @torch.no_grad()
     def extend(self, tokens: torch.Tensor, pos: torch.Tensor, ctx_kv, ctx_mask: torch.Tensor,
-               ctx_pos: torch.Tensor):
+               ctx_pos: torch.Tensor, self_mask: torch.Tensor = None):
         """tokens [R, T], pos [R, T]; ctx_kv per layer (k, v) [R, Hkv, S, D] with
-        ctx_mask [R, S].  Returns (final-norm hidden [R, T, d], new kv per layer)."""
+        ctx_mask [R, S]; self_mask [T, T] (optional, default causal).  Returns
+        (final-norm hidden [R, T, d], new kv per layer)."""
         h = self._embed(tokens)
         new = []
         for i in range(self.cfg.n_layers):
             ck, cv = ctx_kv[i] if ctx_kv is not None else (None, None)
-            h, k, v = self._layer(i, h, pos, ck, cv, ctx_mask, ctx_pos)
+            h, k, v = self._layer(i, h, pos, ck, cv, ctx_mask, ctx_pos, self_mask)
             new.append((k, v))
         return self._rms(h, self.w["norm"]), new
 

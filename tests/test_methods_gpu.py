@@ -55,3 +55,33 @@ def test_beam_topk_proposer_runs(traces):
         traces["issue"], traces["agent_opinions"])
     assert s1 == s2 and isinstance(s1, str)
     assert all(len(st["candidates"]) <= 4 * 10 for st in gen.step_log)
+
+
+def test_score_tree_matches_per_path_scoring(traces):
+    """engine.score_tree (each token-tree node once, tree attention mask) gives the same
+    log-probs as scoring every root-to-node path as its own continuation."""
+    R = importlib.import_module(mp.PKG + ".runtime")
+    engine, tok = R.get_engine(traces["model_id"])
+    g = torch.Generator().manual_seed(3)
+    prefixes = [tok.encode("Issue: genes. Opinion " + str(a) + ":") for a in range(3)]
+    prefixes = [[tok.bos_id] + p for p in prefixes]
+    cache = engine.prefill(prefixes)
+    # a random tree: 3 roots, branching 2-3, depth 3
+    tokens, parents, paths = [], [], []
+    frontier = [(-1, [])]
+    for _ in range(3):
+        nxt = []
+        for p, path in frontier:
+            for _b in range(int(torch.randint(2, 4, (1,), generator=g))):
+                t = int(torch.randint(40, 200, (1,), generator=g))
+                tokens.append(t)
+                parents.append(p)
+                paths.append(path + [t])
+                nxt.append((len(tokens) - 1, path + [t]))
+        frontier = nxt
+    node_lp = engine.score_tree(cache, [0, 1, 2], tokens, parents)          # [3, N]
+    for a in range(3):
+        lp = engine.score(cache, [a] * len(paths), paths)
+        offs = engine.offsets(paths, engine.device)
+        last = lp[offs[1:].long() - 1]                                       # each path's last token
+        assert torch.max(torch.abs(last - node_lp[a])).item() < 1e-4
