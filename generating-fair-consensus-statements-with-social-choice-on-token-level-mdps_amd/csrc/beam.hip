@@ -453,22 +453,43 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
 // Proposer blocks come first in the grid, so they are dispatched first.  No block waits
 // on another (last-arriver hand-offs only), so the launch cannot stall.  Bit-identical to
 // cs_vocab_topk + cs_beam_step (same selection, same lse arithmetic, same U formula).
-// Proposer keys per lane: 16, unless that leaves fewer than 128 proposer workgroups
-// (few beams, e.g. C5's B = 8): then 4, so the proposer finishes under the agent-row
-// stream (tools/beam_ab.py, profiles/r01f_beam_ab.jsonl).  CS_DECODE_KP overrides.
+// Proposer keys per lane: the largest of 16 (256-thread blocks) or 8 (1024-thread blocks;
+// 16 would spill) that still gives >= 128 proposer workgroups, else 4 (few beams, e.g.
+// C5's B = 8), so the proposer finishes under the agent-row stream (tools/beam_ab.py
+// --sweep; profiles/r01f_beam_ab*.jsonl).  CS_DECODE_KP overrides (4, 8 or 16).
 int decode_kp(int32_t B, int64_t vocab, int32_t block, int32_t K) {
-  const char* e = getenv("CS_DECODE_KP");
-  if (e && (atoi(e) == 4 || atoi(e) == 16)) return atoi(e);
-  const int64_t n16 = B * ((vocab + 16LL * block - 1) / (16LL * block));
+  const int big = block >= 1024 ? 8 : 16;
+  if (const char* e = getenv("CS_DECODE_KP")) {
+    const int v = atoi(e);
+    if (v == 4 || v == big) return v;
+  }
+  const int64_t nbig = B * ((vocab + big * block - 1) / (big * static_cast<int64_t>(block)));
   const int64_t n4c = (vocab + 4LL * block - 1) / (4LL * block);
-  return (n16 < 128 && n4c * K <= 16384) ? 4 : 16;
+  return (nbig < 128 && n4c * K <= 16384) ? 4 : big;
 }
-int decode_rows_first() {  // tuning knob CS_DECODE_ROWS_FIRST
-  const char* e = getenv("CS_DECODE_ROWS_FIRST");
-  return (e && atoi(e) == 1) ? 1 : 0;
+// Grid order: the agent-row blocks first when they leave workgroup slots free for the
+// proposer (C3: 256 rows on 256 CUs x 2 slots), the proposer first when the rows alone
+// fill the chip (C5: 512 rows) — then the rows would starve the proposer to the end.
+// CS_DECODE_ROWS_FIRST=0/1 overrides.
+int decode_rows_first(int64_t row_blocks, int32_t block) {
+  if (const char* e = getenv("CS_DECODE_ROWS_FIRST")) return atoi(e) == 1 ? 1 : 0;
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n_cu = v;
+    else
+      n_cu = 256;
+  }
+  const int64_t slots = static_cast<int64_t>(n_cu) * (block >= 1024 ? 2 : 4);
+  return row_blocks < slots ? 1 : 0;
 }
 #ifdef CS_TRACE_DECODE
-__device__ unsigned long long g_dec_t0 = ~0ull;
+// slots: 0 first block start (min), 1 last proposer chunk start, 2 last proposer chunk
+// published, 3 last proposer merge done, 4 last row block start, 5 first row lse,
+// 6 last row lse, 7 last beam gather done, 8 tail start, 9 tail end (wall_clock64 ticks)
+__device__ unsigned long long g_dec_ts[16];
 #define DEC_T(...) __VA_ARGS__
 #else
 #define DEC_T(...)
@@ -478,6 +499,7 @@ constexpr int kBeamMaxBeams = 4096;
 template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL, int KP>
 __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kernel(
     const char* __restrict__ ref, int64_t ld_ref_bytes, int32_t nchunk_p, int32_t rows_first,
+    int32_t ref_vec,
     const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes, int32_t nsplit,
     int64_t split_len, int32_t A, int32_t B, int32_t K, const float* __restrict__ R, float cap,
     float inv_cap, int kind, double eps, unsigned long long* __restrict__ part,
@@ -507,7 +529,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   const bool is_min = kind == CS_WELFARE_MIN;
   const bool order_free = kind == CS_WELFARE_MIN || kind == CS_WELFARE_MAX;
   uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
-  DEC_T(const unsigned long long q0 = wall_clock64(); if (tid == 0) atomicMin(&g_dec_t0, q0);)
+  DEC_T(const unsigned long long q0 = wall_clock64(); if (tid == 0) atomicMin(&g_dec_ts[0], q0);)
   int32_t gb;  // the beam this block arrives at
 
   const int32_t n_rowblk = static_cast<int32_t>(gridDim.x) - n_prop;
@@ -518,36 +540,67 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
                                   : static_cast<int32_t>(blockIdx.x) - n_prop;
   if (pblk >= 0 && pblk < n_prop) {
     // ---- proposer chunk ----
+    // the proposer's short latency chain goes first when it shares a CU with a streaming
+    // row block (instruction issue priority; the stream is bandwidth-bound, not issue-bound)
+    __builtin_amdgcn_s_setprio(2);
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[1], q0);)
     constexpr int CH = KP * BLOCK;
     const int32_t b = pblk / nchunk_p;
     const int32_t chunk = pblk - b * nchunk_p;
     const char* rp = ref + b * ld_ref_bytes;
     const int64_t v0 = static_cast<int64_t>(chunk) * CH;
     const int n = static_cast<int>(min(static_cast<int64_t>(CH), vocab - v0));
-    unsigned long long key[KP];
+    // 32-bit order keys in registers (the token id is implied by (j, lane)): half the
+    // registers of 64-bit composite keys, so the 1024-thread variant does not spill
+    uint32_t okey[KP];
+    constexpr int EPV = Elt<DT>::kPerVec;
+    const bool vec = KP % EPV == 0 && ref_vec && n == CH;
+    if (vec) {
+      // whole 16-byte-aligned chunk: KP / EPV non-temporal 16-byte loads per lane, all in
+      // flight at once (element (j / EPV * BLOCK + tid) * EPV + j % EPV in okey[j])
+      const u32x4* vp = reinterpret_cast<const u32x4*>(rp + v0 * Elt<DT>::kSize);
+      u32x4 q[KP / EPV > 0 ? KP / EPV : 1];
 #pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      const int i = tid + BLOCK * j;
-      float x = 0.0f;
-      if (i < n) x = load_one<DT>(rp, v0 + i);
-      key[j] = 0ull;
-      if (i < n) {
-        if (CAP) x = softcap_fn(x, cap, inv_cap);
-        key[j] = (static_cast<unsigned long long>(order_key(x)) << 32) |
-                 static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + i));
+      for (int j = 0; j < KP / EPV; ++j) q[j] = __builtin_nontemporal_load(vp + j * BLOCK + tid);
+#pragma unroll
+      for (int j = 0; j < KP / EPV; ++j) {
+        float v[EPV];
+        unpack_vec<DT>(q[j], v);
+#pragma unroll
+        for (int e = 0; e < EPV; ++e)
+          okey[j * EPV + e] = order_key(CAP ? softcap_fn(v[e], cap, inv_cap) : v[e]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        const int i = tid + BLOCK * j;
+        float x = 0.0f;
+        if (i < n) x = load_one<DT>(rp, v0 + i);
+        okey[j] = order_key(CAP ? softcap_fn(x, cap, inv_cap) : x);
       }
     }
+    auto local = [&](int j) -> int {   // element of okey[j] within the chunk
+      return vec ? (j / EPV * BLOCK + tid) * EPV + j % EPV : tid + BLOCK * j;
+    };
+    auto key_of = [&](int j) -> unsigned long long {
+      return (static_cast<unsigned long long>(okey[j]) << 32) |
+             static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + local(j)));
+    };
     if (tid == 0) sm_n = 0u;
     const RadixCut cut = radix_select<BLOCK>(
         [&](auto f) {
 #pragma unroll
           for (int j = 0; j < KP; ++j)
-            if (key[j]) f(key[j]);
+            if (local(j) < n) f(key_of(j));
         },
         static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
 #pragma unroll
-    for (int j = 0; j < KP; ++j)
-      if (key[j] && (key[j] >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = key[j];
+    for (int j = 0; j < KP; ++j) {
+      if (local(j) < n) {
+        const unsigned long long kj = key_of(j);
+        if ((kj >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = kj;
+      }
+    }
     __syncthreads();
     const int32_t nkeys = nchunk_p * K;
     unsigned long long* pr = ppart + static_cast<int64_t>(b) * pad_line(nkeys, 8);
@@ -557,6 +610,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     for (int r = nc + tid; r < K; r += BLOCK) st_sc1(out + r, 0ull);
     wait_stores();
     __syncthreads();
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[2], wall_clock64());)
     if (tid == 0) {
       sm_last = arrive(&prop_cnt[b]) == static_cast<uint32_t>(nchunk_p - 1);
       sm_n = 0u;
@@ -588,7 +642,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
       st_sc1(ids_ws + b * pad_line(K, 4) + r, 0xffffffffu);
       out_ids[b * K + r] = -1;
     }
-    DEC_T(if (tid == 0 && b == 0) printf("DEC proposer merge done b0 at %llu (start %llu)\n", wall_clock64() - g_dec_t0, q0 - g_dec_t0);)
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[3], wall_clock64());)
     gb = b;
   } else {
     // ---- agent row stream ----
@@ -627,7 +681,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
       st_sc1(lse_ws + (row % B) * pad_line(A, 4) + row / B, __float_as_uint(ms.x + logf(ms.y)));
     }
     gb = row % B;
-    DEC_T(if (tid == 0 && (row == 0 || row == A * B - 1)) printf("DEC row %d stream start %llu done %llu\n", row, q0 - g_dec_t0, wall_clock64() - g_dec_t0);)
+    DEC_T(if (tid == 0) { const unsigned long long q = wall_clock64(); atomicMax(&g_dec_ts[4], q0);
+                          atomicMin(&g_dec_ts[5], q); atomicMax(&g_dec_ts[6], q); })
   }
 
   // ---- arrival at beam gb (A agent rows + its proposer); the last one gathers ----
@@ -657,13 +712,14 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   }
   wait_stores();
   __syncthreads();
+  DEC_T(if (tid == 0) atomicMax(&g_dec_ts[7], wall_clock64());)
   if (tid == 0) sm_last = arrive(done_cnt) == static_cast<uint32_t>(B - 1);
   __syncthreads();
   if (!sm_last) return;  // block-uniform
   if (tid == 0) st_sc1(done_cnt, 0u);
-  DEC_T(const unsigned long long q8 = wall_clock64();)
+  DEC_T(if (tid == 0) g_dec_ts[8] = wall_clock64();)
   beam_tail<BLOCK>(L, Uw, wkey, W, A, C, kind, eps, n_order, n2, out_order, out_val, out_kept);
-  DEC_T(if (tid == 0) { printf("DEC last gather+done at %llu, tail end %llu\n", q8 - g_dec_t0, wall_clock64() - g_dec_t0); g_dec_t0 = ~0ull; })
+  DEC_T(if (tid == 0) g_dec_ts[9] = wall_clock64();)
 }
 
 }  // namespace
@@ -792,6 +848,17 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
 }
 }  // namespace
 
+#ifdef CS_TRACE_DECODE
+// diagnostics build only: copy the phase timestamps of the last launch and reset them
+int cs_trace_read(unsigned long long* out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_ts), sizeof(g_dec_ts));
+  unsigned long long init[16];
+  for (int i = 0; i < 16; ++i) init[i] = (i == 0 || i == 5) ? ~0ull : 0ull;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dec_ts), init, sizeof(init));
+  return 0;
+}
+#endif
+
 size_t cs_beam_decode_workspace_size(int32_t A, int32_t B, int64_t vocab, int32_t K) {
   if (A <= 0 || B <= 0 || vocab <= 0 || K <= 0) return 0;
   const DecodeLayout p = decode_layout(A, B, vocab, K, CS_BF16);
@@ -857,10 +924,13 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
   while (n2 < C) n2 <<= 1;
   const char* rg = static_cast<const char*>(ref_logits);
   const char* lg = static_cast<const char*>(logits);
-  const int32_t rows_first = decode_rows_first();
+  const int32_t rows_first = decode_rows_first(rows * d.plan.nsplit, d.block);
+  // 16-byte vector loads in the proposer when every reference row starts 16-B aligned
+  const int32_t ref_vec = (reinterpret_cast<uintptr_t>(ref_logits) % 16 == 0 &&
+                           (ld_ref * esz) % 16 == 0) ? 1 : 0;
 #define CS_DECODE_GO(DTV, CAPV, FIXV, BL, UN, KPV)                                                 \
   hipLaunchKernelGGL((beam_decode_kernel<DTV, CAPV, FIXV, BL, UN, KPV>), dim3(grid), dim3(BL), 0,  \
-                     st, rg, ld_ref * esz, d.nchunk_p, rows_first, lg, vocab, ld * esz,            \
+                     st, rg, ld_ref * esz, d.nchunk_p, rows_first, ref_vec, lg, vocab, ld * esz,   \
                      d.plan.nsplit, d.plan.split_len, A, B, K, rewards_in, softcap, inv_cap,       \
                      welfare_kind, static_cast<double>(eps), part, ppart, row_cnt, prop_cnt,       \
                      beam_cnt, done_cnt, wkey, lse_ws, ids_ws, out_ids, out_U, out_W, n_order, n2, \
@@ -872,7 +942,7 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
       else CS_DECODE_GO(DTV, CAPV, FIXV, 256, 8, 16);                                             \
     } else {                                                                                       \
       if (d.kp == 4) CS_DECODE_GO(DTV, CAPV, FIXV, 1024, 2, 4);                                   \
-      else CS_DECODE_GO(DTV, CAPV, FIXV, 1024, 2, 16);                                            \
+      else CS_DECODE_GO(DTV, CAPV, FIXV, 1024, 2, 8);                                             \
     }                                                                                              \
   } while (0)
   if (dtype == CS_F32) {
