@@ -339,12 +339,19 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   __shared__ float sm_s[BLOCK / 64];
   __shared__ float sm_lse;
   __shared__ int sm_last;
-  // keys2 directly after keys: the selection path uses the pair as one 16 KB histogram
-  __shared__ __attribute__((aligned(16))) unsigned long long keys[2 * kFusedSort];
+  // one LDS pool: the bf16 soft-cap table while a row streams, the proposer's and the
+  // tail's buffers otherwise (keys2 directly after keys: the selection path uses the pair
+  // as one 16 KB histogram)
+  constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
+  constexpr int kPoolTail = 2 * kFusedSort + kTopkCand + kFusedSort;  // u64 words
+  constexpr int kPool = TAB && kCapTab / 2 > kPoolTail ? kCapTab / 2 : kPoolTail;
+  __shared__ __attribute__((aligned(16))) unsigned long long pool[kPool];
+  unsigned long long* keys = pool;
   unsigned long long* keys2 = keys + kFusedSort;
-  __shared__ __attribute__((aligned(16))) unsigned long long sel_cand[kTopkCand];
-  __shared__ float sm_w[kFusedSort];
-  __shared__ int32_t sm_ord[kFusedSort];
+  unsigned long long* sel_cand = pool + 2 * kFusedSort;
+  float* sm_w = reinterpret_cast<float*>(sel_cand + kTopkCand);
+  int32_t* sm_ord = reinterpret_cast<int32_t*>(sm_w + kFusedSort);
+  float* ctab = reinterpret_cast<float*>(pool);
   __shared__ uint32_t sm_tw[BLOCK / 64];
   __shared__ int sm_res[2];
   __shared__ uint32_t sm_n;
@@ -370,8 +377,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   const float xg = ok ? load_one<DT>(rp, t_pre) : 0.0f;
 
   // 1. stream
-  const float2 ms =
-      block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
+  if constexpr (TAB) {
+    build_cap_table<BLOCK>(ctab, cap, inv_cap);
+    __syncthreads();
+  }
+  const float2 ms = block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap,
+                                                                     sm_m, sm_s, ctab);
 
   // 2. row finish by the row's last arriver
   if (nsplit > 1) {
@@ -513,11 +524,19 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   __shared__ float sm_s[BLOCK / 64];
   __shared__ float sm_lse;
   __shared__ int sm_last;
-  __shared__ __attribute__((aligned(16))) unsigned long long keys[2 * kFusedSort];
+  // one LDS pool: the bf16 soft-cap table while a row streams, the proposer's and the
+  // tail's buffers otherwise (keys2 directly after keys: the selection path uses the pair
+  // as one 16 KB histogram)
+  constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
+  constexpr int kPoolTail = 2 * kFusedSort + kTopkCand + kFusedSort;  // u64 words
+  constexpr int kPool = TAB && kCapTab / 2 > kPoolTail ? kCapTab / 2 : kPoolTail;
+  __shared__ __attribute__((aligned(16))) unsigned long long pool[kPool];
+  unsigned long long* keys = pool;
   unsigned long long* keys2 = keys + kFusedSort;
-  __shared__ __attribute__((aligned(16))) unsigned long long sel_cand[kTopkCand];
-  __shared__ float sm_w[kFusedSort];
-  __shared__ int32_t sm_ord[kFusedSort];
+  unsigned long long* sel_cand = pool + 2 * kFusedSort;
+  float* sm_w = reinterpret_cast<float*>(sel_cand + kTopkCand);
+  int32_t* sm_ord = reinterpret_cast<int32_t*>(sm_w + kFusedSort);
+  float* ctab = reinterpret_cast<float*>(pool);
   __shared__ uint32_t sm_tw[BLOCK / 64];
   __shared__ int sm_res[2];
   __shared__ uint32_t sm_n;
@@ -652,8 +671,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     const char* rp = logits + row * ld_bytes;
     const int64_t v0 = static_cast<int64_t>(split) * split_len;
     const int64_t v1 = min(vocab, v0 + split_len);
-    const float2 ms =
-        block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
+    if constexpr (TAB) {
+      build_cap_table<BLOCK>(ctab, cap, inv_cap);
+      __syncthreads();
+    }
+    const float2 ms = block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(
+        rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s, ctab);
     if (nsplit > 1) {
       if (tid == 0) {
         st_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + split,

@@ -131,6 +131,41 @@ __device__ __forceinline__ float softcap_exp(float x, float cap, float inv_cap) 
   return __builtin_amdgcn_exp2f(fmaf((-2.0f * kLog2e) * cap, softcap_rcp(x, inv_cap), kLog2e * cap));
 }
 
+// bf16 soft-cap table.  A bf16 logit takes 2^16 values, so exp(cap * tanh(x / cap)) --
+// three transcendentals per element in the fixed-offset sum (softcap_exp) -- becomes one
+// LDS lookup.  Only magnitude bits in [kCapLo, kCapHi] need entries of their own: below
+// 2^-24 the value is that of x = 0 (exp2 of |arg| < 6e-9 rounds to 1), from 512 up it is
+// saturated (x' = +-cap exactly in fp32).  Every entry is softcap_exp of its exact bf16
+// value, so the sums are the transcendental path's sums.  NaN (magnitude > 0x7f80) is
+// tracked beside the sum, since the clamp would map it to the saturated entry.
+constexpr uint32_t kCapLo = 102u << 7;
+constexpr uint32_t kCapHi = (136u << 7) | 127u;
+constexpr int kCapSpan = static_cast<int>(kCapHi - kCapLo + 1);  // 4480 entries per sign
+constexpr int kCapTab = 2 * kCapSpan;                             // 35,840 B of LDS
+
+template <int DT, bool CAP, bool FIXED>
+struct CapTable {
+  static constexpr bool kOn = DT == CS_BF16 && CAP && FIXED;
+};
+
+template <int BLOCK>
+__device__ __forceinline__ void build_cap_table(float* tab, float cap, float inv_cap) {
+  for (int i = threadIdx.x; i < kCapTab; i += BLOCK) {
+    const uint32_t neg = i >= kCapSpan ? 1u : 0u;
+    const uint32_t c = static_cast<uint32_t>(i) - neg * kCapSpan;
+    const uint32_t u = c < 128u ? 0u : kCapLo + c;  // the lowest bin stands for +-0
+    tab[i] = softcap_exp(__uint_as_float(((neg << 15) | u) << 16), cap, inv_cap);
+  }
+}
+
+// exp(softcap(x)) of one bf16 bit pattern b (low 16 bits of the argument)
+__device__ __forceinline__ float cap_lookup(const float* tab, uint32_t u, uint32_t neg,
+                                            uint32_t& nanmax) {
+  nanmax = max(nanmax, u);
+  const uint32_t c = min(max(u, kCapLo), kCapHi) - kCapLo;
+  return tab[c + neg * kCapSpan];
+}
+
 // ---------------------------------------------------------------------------
 // online log-sum-exp state
 // ---------------------------------------------------------------------------
@@ -216,6 +251,24 @@ __device__ __forceinline__ void gather_targets(const char* row, int64_t vocab, f
   }
 }
 
+// NQ 16-byte vectors of bf16 through the soft-cap table, summed in element order
+// (element 2i = low half of dword i), as accum_elems sums softcap_exp.
+template <int NQ>
+__device__ __forceinline__ void cap_accum(float& s, uint32_t& nanmax, const u32x4* q,
+                                          const float* __restrict__ tab) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t w = q[u][i];
+      acc += cap_lookup(tab, w & 0x7fffu, (w >> 15) & 1u, nanmax);
+      acc += cap_lookup(tab, (w >> 16) & 0x7fffu, w >> 31, nanmax);
+    }
+  }
+  s += acc;
+}
+
 // ---------------------------------------------------------------------------
 // streaming kernel: one workgroup per (row, split) work item
 // ---------------------------------------------------------------------------
@@ -228,12 +281,15 @@ __device__ __forceinline__ void gather_targets(const char* row, int64_t vocab, f
 template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
 __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp, int64_t v0,
                                                     int64_t n, float cap, float inv_cap,
-                                                    float* sm_m, float* sm_s) {
+                                                    float* sm_m, float* sm_s,
+                                                    const float* __restrict__ ctab = nullptr) {
   constexpr int ESZ = Elt<DT>::kSize;
   constexpr int EPV = Elt<DT>::kPerVec;
   constexpr int NW = BLOCK / 64;
+  constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
   const int tid = threadIdx.x;
   float m = FIXED ? 0.0f : -INFINITY, s = 0.0f;
+  uint32_t nanmax = 0u;
 
   const uintptr_t a0 = reinterpret_cast<uintptr_t>(rp + v0 * ESZ);
   int64_t head = static_cast<int64_t>(((16u - (a0 & 15u)) & 15u) / ESZ);
@@ -251,7 +307,10 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
       have = true;
     }
     if (have) {
-      if constexpr (CAP && FIXED) {
+      if constexpr (TAB) {
+        const uint32_t b = __float_as_uint(x) >> 16;
+        s += cap_lookup(ctab, b & 0x7fffu, b >> 15, nanmax);
+      } else if constexpr (CAP && FIXED) {
         s += softcap_exp(x, cap, inv_cap);
       } else {
         if (CAP) x = softcap_fn(x, cap, inv_cap);
@@ -267,17 +326,26 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
     u32x4 q[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * BLOCK);
-    float v[UNROLL * EPV];
+    if constexpr (TAB) {
+      cap_accum<UNROLL>(s, nanmax, q, ctab);
+    } else {
+      float v[UNROLL * EPV];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
-    accum_elems<UNROLL * EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
+      for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
+      accum_elems<UNROLL * EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
+    }
   }
   for (; i < nvec; i += BLOCK) {
     const u32x4 q = __builtin_nontemporal_load(vp + i);
-    float v[EPV];
-    unpack_vec<DT>(q, v);
-    accum_elems<EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
+    if constexpr (TAB) {
+      cap_accum<1>(s, nanmax, &q, ctab);
+    } else {
+      float v[EPV];
+      unpack_vec<DT>(q, v);
+      accum_elems<EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
+    }
   }
+  if (TAB && nanmax > 0x7f80u) s = __builtin_nanf("");
 
   wave_lse_reduce(m, s);
   const int wave = tid >> 6;

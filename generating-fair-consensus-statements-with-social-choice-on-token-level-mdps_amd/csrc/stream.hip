@@ -5,7 +5,7 @@ namespace {
 
 // Work items (row, split) are walked grid-stride so a capped grid also works.
 template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
-__global__ __launch_bounds__(BLOCK) void lsg_stream_kernel(
+__global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 1) void lsg_stream_kernel(
     const char* __restrict__ logits, int64_t n_items, int64_t vocab, int64_t ld_bytes,
     int32_t nsplit, int64_t split_len, const int32_t* __restrict__ tgt, int32_t k, float cap,
     float inv_cap, float* __restrict__ out_tok, float* __restrict__ out_lse,
@@ -13,7 +13,13 @@ __global__ __launch_bounds__(BLOCK) void lsg_stream_kernel(
   __shared__ float sm_m[BLOCK / 64];
   __shared__ float sm_s[BLOCK / 64];
   __shared__ float sm_lse;
+  constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
+  __shared__ float ctab[TAB ? kCapTab : 1];
   const int tid = threadIdx.x;
+  if constexpr (TAB) {
+    build_cap_table<BLOCK>(ctab, cap, inv_cap);
+    __syncthreads();
+  }
 
   for (int64_t bid = blockIdx.x; bid < n_items; bid += gridDim.x) {
     const int64_t row = bid / nsplit;
@@ -22,7 +28,8 @@ __global__ __launch_bounds__(BLOCK) void lsg_stream_kernel(
     const int64_t v0 = static_cast<int64_t>(split) * split_len;
     const int64_t v1 = min(vocab, v0 + split_len);
     const float2 ms =
-        block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s);
+        block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s,
+                                                         ctab);
     if (tid == 0) {
       if (nsplit > 1) {
         part[bid] = ms;

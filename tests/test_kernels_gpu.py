@@ -39,6 +39,8 @@ CASES = [
     (torch.float32, 1, 7, 0, 7, 0.0),                 # tiny row, k = vocab
     (torch.bfloat16, 4096, 4096, 0, 1, 0.0),          # single pass, many rows
     (torch.float32, 2049, 515, 0, 3, 5.0),            # single pass, soft-cap, scalar tail
+    (torch.bfloat16, 300, 256000, 1, 4, 30.0),        # single pass, soft-cap table, misaligned
+    (torch.bfloat16, 7, 77, 0, 3, 50.0),              # tiny rows through the soft-cap table
 ]
 
 
@@ -56,6 +58,43 @@ def test_logsoftmax_gather_matches_oracle(ops, orc, dev, dtype, rows, vocab, ld_
     assert np.max(np.abs(tok.cpu().numpy() - o_tok)) < LP_TOL
     assert np.max(np.abs(lse.cpu().numpy() - o_lse)) < LP_TOL
     del logits
+
+
+@pytest.mark.parametrize("cap", [30.0, 50.0, 2.5])
+def test_bf16_softcap_table_covers_every_bit_pattern(ops, orc, dev, cap):
+    """bf16 + soft-cap looks exp(cap*tanh(x/cap)) up in an LDS table (magnitudes clamped at
+    2^-24 and 512).  Rows hold every non-NaN bf16 bit pattern (+-0, subnormals, +-inf, the
+    largest finite values) in order and shuffled, rows of one pattern class, and a NaN row:
+    lse and gathered targets against the fp64 oracle and the fp32 (transcendental) path."""
+    bits = np.arange(65536, dtype=np.uint32)
+    fin = bits[(bits & 0x7FFF) <= 0x7F80].astype(np.uint16)        # 65,282 patterns
+    rng = np.random.default_rng(int(cap * 10))
+    V = fin.size
+    tiny = fin[(fin & 0x7FFF) < (104 << 7)]
+    huge = fin[(fin & 0x7FFF) >= (135 << 7)]
+    rows = [fin, rng.permutation(fin), np.resize(rng.permutation(tiny), V),
+            np.resize(rng.permutation(huge), V), rng.permutation(fin)]
+    rows[4][12345] = 0x7FC1                                         # a NaN
+    host = np.ascontiguousarray(np.stack(rows))
+    x = torch.from_numpy(host.view(np.int16)).view(torch.bfloat16)
+    tgt = torch.from_numpy(rng.integers(0, V, size=(len(rows), 6), dtype=np.int32))
+    tgt[0, :3] = torch.tensor([0, V // 2, V - 1], dtype=torch.int32)
+    tok, lse = ops.logsoftmax_gather(x.to(dev), tgt.to(dev), softcap=cap, want_lse=True)
+    o_tok, o_lse = orc.logsoftmax_gather(host, tgt.numpy(), softcap=cap, bf16=True)
+    lse, tok = lse.cpu().numpy(), tok.cpu().numpy()
+    assert np.isnan(lse[4]) and np.all(np.isnan(tok[4])) and np.isnan(o_lse[4])
+    assert np.max(np.abs(lse[:4] - o_lse[:4])) < LP_TOL
+    assert np.max(np.abs(tok[:4] - o_tok[:4])) < LP_TOL
+    f_tok, f_lse = ops.logsoftmax_gather(x.float().to(dev), tgt.to(dev), softcap=cap, want_lse=True)
+    assert np.max(np.abs(lse[:4] - f_lse.cpu().numpy()[:4])) < 2e-5
+    # misaligned rows (odd element offset) exercise the table's scalar head / tail
+    xs = x.to(dev)[:4, 1:]
+    t2 = torch.clamp(tgt[:4].to(dev) - 1, min=0)
+    m_tok, m_lse = ops.logsoftmax_gather(xs, t2, softcap=cap, want_lse=True)
+    o2_tok, o2_lse = orc.logsoftmax_gather(np.ascontiguousarray(host[:4, 1:]), t2.cpu().numpy(),
+                                           softcap=cap, bf16=True)
+    assert np.max(np.abs(m_lse.cpu().numpy() - o2_lse)) < LP_TOL
+    assert np.max(np.abs(m_tok.cpu().numpy() - o2_tok)) < LP_TOL
 
 
 def test_out_of_range_targets_are_nan_and_masked_vocab(ops, orc, dev):

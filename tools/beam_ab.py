@@ -11,6 +11,11 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+if "--lib" in sys.argv:   # A/B another build of the library: --lib path/to/lib.so
+    _lib = importlib.import_module(PKG + "._lib")
+    _lib.LIB_NAME = os.path.relpath(os.path.abspath(sys.argv[sys.argv.index("--lib") + 1]),
+                                    os.path.join(REPO, PKG))
 ops = importlib.import_module(
     "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd.ops")
 import bench  # noqa: E402
@@ -43,7 +48,9 @@ def main():
         t = torch.randint(0, V, (B, K), generator=g, device=dev, dtype=torch.int32)
         R = torch.zeros(A, B, device=dev)
         ws, wb = ops.Workspace(), ops.Workspace(zeroed=True)
-        r = {"config": name}
+        if "--only" in sys.argv and name not in sys.argv[sys.argv.index("--only") + 1].split(","):
+            continue
+        r = {"config": name, "lib": "alt" if "--lib" in sys.argv else "tree"}
         r["lsg_k0_us"] = timed(lambda: ops.logsoftmax_gather(x, None, softcap=cap, workspace=ws, want_lse=True))
         r["lsg_kK_us"] = timed(lambda: ops.logsoftmax_gather(x, t.repeat(A, 1), softcap=cap, workspace=ws))
         r["beam_sort_us"] = timed(lambda: ops.beam_step(x, t, R, "min", softcap=cap, workspace=wb))
