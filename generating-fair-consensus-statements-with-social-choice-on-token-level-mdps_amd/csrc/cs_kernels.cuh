@@ -251,22 +251,27 @@ __device__ __forceinline__ void gather_targets(const char* row, int64_t vocab, f
   }
 }
 
-// NQ 16-byte vectors of bf16 through the soft-cap table, summed in element order
-// (element 2i = low half of dword i), as accum_elems sums softcap_exp.
+// NQ 16-byte vectors of bf16 through the soft-cap table.  All 8 * NQ lookups are issued
+// before the first add, and the sum is a fixed tree (four chains, element e in chain
+// e % 4), so the LDS latency is paid once per batch, not once per element.  Every kernel
+// sums through this one function, so their results stay bit-identical to each other.
 template <int NQ>
 __device__ __forceinline__ void cap_accum(float& s, uint32_t& nanmax, const u32x4* q,
                                           const float* __restrict__ tab) {
-  float acc = 0.0f;
+  float t[8 * NQ];
 #pragma unroll
   for (int u = 0; u < NQ; ++u) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint32_t w = q[u][i];
-      acc += cap_lookup(tab, w & 0x7fffu, (w >> 15) & 1u, nanmax);
-      acc += cap_lookup(tab, (w >> 16) & 0x7fffu, w >> 31, nanmax);
+      t[u * 8 + 2 * i] = cap_lookup(tab, w & 0x7fffu, (w >> 15) & 1u, nanmax);
+      t[u * 8 + 2 * i + 1] = cap_lookup(tab, (w >> 16) & 0x7fffu, w >> 31, nanmax);
     }
   }
-  s += acc;
+  float a[4] = {t[0], t[1], t[2], t[3]};
+#pragma unroll
+  for (int e = 4; e < 8 * NQ; ++e) a[e & 3] += t[e];
+  s += (a[0] + a[1]) + (a[2] + a[3]);
 }
 
 // ---------------------------------------------------------------------------
