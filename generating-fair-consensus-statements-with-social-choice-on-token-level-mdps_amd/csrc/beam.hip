@@ -606,6 +606,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
              static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + local(j)));
     };
     if (tid == 0) sm_n = 0u;
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[10], wall_clock64());)
     const RadixCut cut = radix_select<BLOCK>(
         [&](auto f) {
 #pragma unroll
@@ -613,6 +614,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
             if (local(j) < n) f(key_of(j));
         },
         static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[11], wall_clock64());)
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
       if (local(j) < n) {
@@ -629,7 +631,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     for (int r = nc + tid; r < K; r += BLOCK) st_sc1(out + r, 0ull);
     wait_stores();
     __syncthreads();
-    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[2], wall_clock64());)
+    DEC_T(if (tid == 0) { const unsigned long long q = wall_clock64(); atomicMax(&g_dec_ts[2], q);
+                          atomicMin(&g_dec_ts[12], q); })
     if (tid == 0) {
       sm_last = arrive(&prop_cnt[b]) == static_cast<uint32_t>(nchunk_p - 1);
       sm_n = 0u;
@@ -876,7 +879,7 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
 int cs_trace_read(unsigned long long* out) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_ts), sizeof(g_dec_ts));
   unsigned long long init[16];
-  for (int i = 0; i < 16; ++i) init[i] = (i == 0 || i == 5) ? ~0ull : 0ull;
+  for (int i = 0; i < 16; ++i) init[i] = (i == 0 || i == 5 || i == 12) ? ~0ull : 0ull;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dec_ts), init, sizeof(init));
   return 0;
 }

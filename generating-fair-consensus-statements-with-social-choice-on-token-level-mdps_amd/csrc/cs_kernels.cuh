@@ -428,7 +428,7 @@ struct SplitPlan {
 };
 
 inline int64_t target_wgs() {
-  const char* e = getenv("CS_TARGET_WGS");  // tuning knob (tools/beam_ab.py); default 2048
+  const char* e = getenv("CS_TARGET_WGS");  // tuning knob (tools/beam_ab.py, split_sweep.py)
   const int64_t v = e ? atoll(e) : 0;
   return v > 0 ? v : kTargetWgs;
 }

@@ -79,6 +79,16 @@ def main():
                         pass
             os.environ.pop("CS_DECODE_KP")
             os.environ.pop("CS_DECODE_ROWS_FIRST")
+        if "--twsweep" in sys.argv:   # split-V target grid (block shape) x grid order
+            for tw in (512, 1024, 2048):
+                for rf in (0, 1):
+                    os.environ["CS_TARGET_WGS"] = str(tw)
+                    os.environ["CS_DECODE_ROWS_FIRST"] = str(rf)
+                    wt = ops.Workspace(zeroed=True)
+                    r[f"decode_tw{tw}_rf{rf}_us"] = timed(lambda: ops.beam_decode_step(
+                        ref, x, R, K, "min", n_order=B, softcap=cap, workspace=wt))
+            os.environ.pop("CS_TARGET_WGS")
+            os.environ.pop("CS_DECODE_ROWS_FIRST")
         r["bytes"] = A * B * V * x.element_size()
         r["ideal_us"] = r["bytes"] / 8e12 * 1e6
         print(json.dumps(r), flush=True)

@@ -30,7 +30,7 @@ L = _lib.load()
 L.cs_trace_read.argtypes = [ctypes.c_void_p]
 NAMES = ["start", "last_prop_chunk_start", "last_prop_chunk_published", "last_prop_merge_done",
          "last_row_start", "first_row_lse", "last_row_lse", "last_gather_done", "tail_start",
-         "tail_end"]
+         "tail_end", "last_prop_keys_ready", "last_prop_cut_done", "first_prop_chunk_published"]
 dev = torch.device("cuda:0")
 buf = (ctypes.c_ulonglong * 16)()
 for name, (A, B, K, V, cap, dt) in {"c1": (4, 4, 10, 128256, 0.0, torch.float32),
