@@ -305,10 +305,18 @@ def run_beam(name, world, rank, dev, steps, warmup):
     per_replay = 1 if sharded else 2
     steps = max(per_replay, steps - steps % per_replay)
 
-    def step():
+    coll_ev = []
+
+    def step(timed=False):
         g1.replay()
         if sharded:
+            if timed:
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record()
             torch.distributed.all_reduce(Wx, op=torch.distributed.ReduceOp.MIN)
+            if timed:
+                e[1].record()
+                coll_ev.append(e)
             g2.replay()
 
     for _ in range(max(1, warmup // per_replay)):
@@ -319,11 +327,12 @@ def run_beam(name, world, rank, dev, steps, warmup):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps // per_replay):
-        step()
+        step(timed=True)
     torch.cuda.synchronize()
     if sharded:
         torch.distributed.barrier()
     el = time.perf_counter() - t0
+    coll_ms = float(np.mean([a.elapsed_time(b) for a, b in coll_ev])) if coll_ev else None
     if sharded:
         tt = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -359,6 +368,8 @@ def run_beam(name, world, rank, dev, steps, warmup):
                          "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
                          "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "collective": {"op": "all_reduce(MIN) of W" if sharded else "none (1 GPU)",
+                           "bytes": C * 4 if sharded else 0, "ms_per_step": coll_ms},
             "step_bytes": (A_loc * B + B) * V * esz,
             "step_frac_of_hbm": (A_loc * B + B) * V * esz / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
@@ -410,14 +421,18 @@ def main():
         if wkind == "sumlog":
             U = torch.exp(U)  # Nash over geometric-mean token probability
         # agents sharded over ranks: MIN all-reduce (egalitarian) or gather + ordered fold
+        if ev is not None:
+            ev[2].record(stream)
         W = par.combine_welfare(U, wkind, shard, eps=1e-30)
+        if ev is not None:
+            ev[3].record(stream)
         idx, _ = ops.topk(W, 1)
         return idx
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
               for _ in range(args.steps)]
     if world > 1:
         torch.distributed.barrier()
@@ -433,7 +448,9 @@ def main():
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    # the welfare exchange (RCCL MIN all-reduce, or all-gather + ordered fold) broken out
+    coll_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in events]))
     ms_per_step = elapsed * 1000.0 / args.steps
 
     line = None
@@ -472,6 +489,11 @@ def main():
                          "kernel": "lsg_stream_kernel (cs_logsoftmax_gather)",
                          "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "collective": {"op": ("all_reduce(MIN) of W" if wkind == "min" else
+                                  "all_gather of [A_local, C] + ordered fold") if world > 1
+                           else "none (1 GPU: local fold)",
+                           "bytes": N * 4 if wkind == "min" else A * world * N * 4,
+                           "ms_per_step": coll_ms},
         }
         if e2e is not None:
             line["end_to_end"] = e2e
