@@ -550,6 +550,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
   DEC_T(const unsigned long long q0 = wall_clock64(); if (tid == 0) atomicMin(&g_dec_ts[0], q0);)
   int32_t gb;  // the beam this block arrives at
+  bool ids_in_lds = false;  // this block merged beam gb's proposer: its ids are in LDS
 
   const int32_t n_rowblk = static_cast<int32_t>(gridDim.x) - n_prop;
   // block role: proposer blocks first in the grid, or after the row blocks
@@ -640,30 +641,52 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     __syncthreads();
     if (!sm_last) return;  // block-uniform
     if (tid == 0) st_sc1(prop_cnt + b, 0u);
-    // the beam's K best among the chunk winners -> its candidate ids
-    const RadixCut mcut = radix_select<BLOCK>(
-        [&](auto f) {
-          for (int i = tid; i < nkeys; i += BLOCK) {
-            const unsigned long long c = ld_sc1(pr + i);
-            if (c) f(c);
-          }
-        },
-        static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
-    for (int i = tid; i < nkeys; i += BLOCK) {
-      const unsigned long long c = ld_sc1(pr + i);
-      if (c && (c >> mcut.shift) >= mcut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = c;
+    // the beam's K best among the chunk winners -> its candidate ids.  The winners are
+    // read once (all loads in flight together) into registers when they fit, not again
+    // per radix level and for the collection.
+    constexpr int MR = 4;
+    unsigned long long mk[MR];
+    const bool cached = nkeys <= MR * BLOCK;
+    if (cached) {
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        const int i = tid + r * BLOCK;
+        mk[r] = i < nkeys ? ld_sc1(pr + i) : 0ull;
+      }
     }
+    auto each_key = [&](auto f) {
+      if (cached) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+          if (mk[r]) f(mk[r]);
+      } else {
+        for (int i = tid; i < nkeys; i += BLOCK) {
+          const unsigned long long c = ld_sc1(pr + i);
+          if (c) f(c);
+        }
+      }
+    };
+    const RadixCut mcut = radix_select<BLOCK>(
+        each_key, static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+    each_key([&](unsigned long long c) {
+      if ((c >> mcut.shift) >= mcut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = c;
+    });
     __syncthreads();
     const int mc = static_cast<int>(sm_n);
+    // the ids also stay in LDS: when this block gathers the beam it reads them there
+    uint32_t* sm_ids = reinterpret_cast<uint32_t*>(sm_ord);
     rank_candidates<BLOCK>(sel_cand, mc, K, [&](int r, unsigned long long c) {
       const uint32_t id = 0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull);
       st_sc1(ids_ws + b * pad_line(K, 4) + r, id);
+      sm_ids[r] = id;
       out_ids[b * K + r] = static_cast<int32_t>(id);
     });
     for (int r = mc + tid; r < K; r += BLOCK) {
       st_sc1(ids_ws + b * pad_line(K, 4) + r, 0xffffffffu);
+      sm_ids[r] = 0xffffffffu;
       out_ids[b * K + r] = -1;
     }
+    ids_in_lds = true;
     DEC_T(if (tid == 0) atomicMax(&g_dec_ts[3], wall_clock64());)
     gb = b;
   } else {
@@ -722,7 +745,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     const int32_t a = i / K;
     const int32_t j = i - a * K;
     const int32_t row = a * B + gb;
-    const int32_t t = static_cast<int32_t>(ld_sc1(ids_ws + gb * pad_line(K, 4) + j));
+    const int32_t t = static_cast<int32_t>(ids_in_lds ? reinterpret_cast<const uint32_t*>(sm_ord)[j]
+                                                      : ld_sc1(ids_ws + gb * pad_line(K, 4) + j));
     const float lse = __uint_as_float(ld_sc1(lse_ws + gb * pad_line(A, 4) + a));
     float lp = __builtin_nanf("");
     if (t >= 0 && t < vocab) {
