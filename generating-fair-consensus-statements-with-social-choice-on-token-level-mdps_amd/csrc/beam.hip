@@ -608,22 +608,47 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     };
     if (tid == 0) sm_n = 0u;
     DEC_T(if (tid == 0) atomicMax(&g_dec_ts[10], wall_clock64());)
-    const RadixCut cut = radix_select<BLOCK>(
-        [&](auto f) {
+    bool have = false;   // candidates collected (block-uniform)
+    // (256-thread variants only: in the 1024-thread ones the extra code's registers slow
+    // the agent-row stream more than the bound saves; profiles/r01h_decode_wave_bound.jsonl)
+    if (BLOCK <= 256 && K <= kWaveBoundMaxK) {
+      uint32_t lm = 0u;
 #pragma unroll
-          for (int j = 0; j < KP; ++j)
-            if (local(j) < n) f(key_of(j));
-        },
-        static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
-    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[11], wall_clock64());)
+      for (int j = 0; j < KP; ++j)
+        if (local(j) < n) lm = max(lm, okey[j]);
+      const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
 #pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      if (local(j) < n) {
-        const unsigned long long kj = key_of(j);
-        if ((kj >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = kj;
+      for (int j = 0; j < KP; ++j) {
+        if (local(j) < n && okey[j] >= t) {
+          const uint32_t at = atomicAdd(&sm_n, 1u);
+          if (at < kTopkCand) sel_cand[at] = key_of(j);
+        }
+      }
+      __syncthreads();
+      have = sm_n <= static_cast<uint32_t>(kTopkCand);
+      if (!have) {   // massive ties at the bound: the radix path below
+        __syncthreads();
+        if (tid == 0) sm_n = 0u;
       }
     }
-    __syncthreads();
+    if (!have) {
+      const RadixCut cut = radix_select<BLOCK>(
+          [&](auto f) {
+#pragma unroll
+            for (int j = 0; j < KP; ++j)
+              if (local(j) < n) f(key_of(j));
+          },
+          static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        if (local(j) < n) {
+          const unsigned long long kj = key_of(j);
+          if ((kj >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = kj;
+        }
+      }
+      __syncthreads();
+    }
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[11], wall_clock64());)
     const int32_t nkeys = nchunk_p * K;
     unsigned long long* pr = ppart + static_cast<int64_t>(b) * pad_line(nkeys, 8);
     unsigned long long* out = pr + static_cast<int64_t>(chunk) * K;
@@ -666,12 +691,34 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
         }
       }
     };
-    const RadixCut mcut = radix_select<BLOCK>(
-        each_key, static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
-    each_key([&](unsigned long long c) {
-      if ((c >> mcut.shift) >= mcut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = c;
-    });
-    __syncthreads();
+    bool mhave = false;
+    if (BLOCK <= 256 && K <= kWaveBoundMaxK && cached) {
+      uint32_t lm = 0u;
+#pragma unroll
+      for (int r = 0; r < MR; ++r) lm = max(lm, static_cast<uint32_t>(mk[r] >> 32));
+      const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        if (mk[r] && static_cast<uint32_t>(mk[r] >> 32) >= t) {
+          const uint32_t at = atomicAdd(&sm_n, 1u);
+          if (at < kTopkCand) sel_cand[at] = mk[r];
+        }
+      }
+      __syncthreads();
+      mhave = sm_n <= static_cast<uint32_t>(kTopkCand);
+      if (!mhave) {
+        __syncthreads();
+        if (tid == 0) sm_n = 0u;
+      }
+    }
+    if (!mhave) {
+      const RadixCut mcut = radix_select<BLOCK>(
+          each_key, static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+      each_key([&](unsigned long long c) {
+        if ((c >> mcut.shift) >= mcut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = c;
+      });
+      __syncthreads();
+    }
     const int mc = static_cast<int>(sm_n);
     // the ids also stay in LDS: when this block gathers the beam it reads them there
     uint32_t* sm_ids = reinterpret_cast<uint32_t*>(sm_ord);

@@ -611,4 +611,34 @@ __device__ __forceinline__ RadixCut radix_select(ForEach for_each, uint32_t k, u
   }
 }
 
+// Lower bound on the k-th largest of a block's 32-bit order keys, for small k: each lane
+// passes its largest key; per wave the k-th largest of those 64 (a wave64 bitonic sort in
+// registers) -- at least k of the wave's keys are >= it, so every key among the block's k
+// largest is >= the largest such bound over the waves.  With k of a few dozen or less
+// only about k..2k keys pass it, so collecting them and rank-counting replaces the
+// histogram passes of radix_select (no LDS atomics on hot bins, two barriers).
+// sm_t holds BLOCK / 64 words.  Returns 0 (every key passes) when a wave has < k keys.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t wave_bound(uint32_t lane_max, int k, uint32_t* sm_t) {
+  const int lane = threadIdx.x & 63;
+  uint32_t v = lane_max;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint32_t o = __shfl_xor(v, stride, 64);
+      const bool keep_max = ((lane & stride) == 0) == ((lane & size) == 0);
+      v = keep_max ? max(v, o) : min(v, o);
+    }
+  }
+  const uint32_t t = __shfl(v, k - 1, 64);
+  if (lane == 0) sm_t[threadIdx.x >> 6] = t;
+  __syncthreads();
+  uint32_t b = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / 64; ++w) b = max(b, sm_t[w]);
+  return b;
+}
+constexpr int kWaveBoundMaxK = 16;   // larger k: radix_select (the bound passes too many)
+
 }  // namespace

@@ -442,6 +442,40 @@ def test_beam_decode_step_is_topk_plus_beam_step(ops, dev, dtype, A, B, K, vocab
         assert torch.equal(kept, U[:, on.long()])
 
 
+@pytest.mark.parametrize("case", ["constant", "masked", "nan", "chunk_ties", "random"])
+@pytest.mark.parametrize("K", [1, 10, 16])
+def test_beam_decode_proposer_edge_rows(ops, orc, dev, case, K):
+    """Small K takes the decode proposer's wave-bound selection (lane maxima -> per-wave
+    k-th -> block bound -> rank the few keys above it), with the radix path as fallback
+    for massive ties: constant rows, masked (-inf) rows with fewer finite values than K,
+    NaN rows and ties straddling chunk boundaries give the oracle's ids and cs_vocab_topk's
+    ids (radix path) exactly."""
+    g = torch.Generator().manual_seed(17 + K)
+    B, V, A = 3, 20000, 2
+    ref = torch.randn(B, V, generator=g) * 3.0
+    if case == "constant":
+        ref[:] = 1.25
+        ref[1, 5000:9000] = 0.0
+    elif case == "masked":
+        ref[:, 6:] = float("-inf")
+        ref[2] = float("-inf")
+    elif case == "nan":
+        ref[0, ::3] = float("nan")
+        ref[1, :] = float("nan")
+        ref[1, 17] = 2.0
+    elif case == "chunk_ties":
+        ref[:] = -5.0
+        for c in (4095, 4096, 8191, 8192, 12287, 19999, 1023, 1024, 2047):
+            ref[:, c] = 7.0
+    x = torch.randn(A * B, V, generator=g) * 3.0
+    R = torch.zeros(A, B)
+    ids, *_ = ops.beam_decode_step(ref.to(dev), x.to(dev), R.to(dev), K, "min")
+    o_ids, _ = orc.vocab_topk(ref.double().numpy(), K)
+    t_ids, _ = ops.vocab_topk(ref.to(dev), K)
+    assert np.array_equal(ids.cpu().numpy(), o_ids)
+    assert torch.equal(ids, t_ids)
+
+
 def test_fused_beam_launches_stress_shared_workspace(ops, dev):
     """Hand-offs under repetition: 40 fused decode / beam launches of alternating shapes on
     ONE workspace (counters must return to zero every call), each checked word for word
