@@ -272,6 +272,40 @@ __device__ __forceinline__ void beam_tail(const BeamLds& L, uint32_t* Uw, uint32
                           static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(c))
                     : 0ull;
     }
+    auto emit = [&](int r, unsigned long long key) {
+      const int32_t c = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(key & 0xffffffffull));
+      out_order[r] = c;
+      if (out_val) out_val[r] = sm_w[c];
+      sm_ord[r] = c;
+    };
+    if (BLOCK <= 256 && n_order <= kWaveBoundMaxK) {
+      // few kept beams (256-thread blocks): the wave bound instead of histogram passes
+      __syncthreads();   // sm_n = 0 is visible before any append
+      uint32_t lm = 0u;
+#pragma unroll
+      for (int r = 0; r < kFusedSort / BLOCK; ++r)
+        if (kc[r]) lm = max(lm, static_cast<uint32_t>(kc[r] >> 32));
+      const uint32_t t = wave_bound<BLOCK>(lm, n_order, sm_tw);
+#pragma unroll
+      for (int r = 0; r < kFusedSort / BLOCK; ++r) {
+        if (kc[r] && static_cast<uint32_t>(kc[r] >> 32) >= t) {
+          const uint32_t at = atomicAdd(&sm_n, 1u);
+          if (at < kTopkCand) cand[at] = kc[r];
+        }
+      }
+      __syncthreads();
+      const uint32_t nc = sm_n;
+      if (nc <= static_cast<uint32_t>(kTopkCand)) {  // block-uniform
+        rank_candidates<BLOCK>(cand, static_cast<int>(nc), n_order, emit);
+        if (out_kept) {
+          __syncthreads();
+          keep_columns<BLOCK>(Uw, out_kept, sm_ord, A, C, n_order);
+        }
+        return;
+      }
+      __syncthreads();
+      if (tid == 0) sm_n = 0u;
+    }
     const RadixCut cut = radix_select<BLOCK>(
         [&](auto f) {
 #pragma unroll
@@ -284,14 +318,7 @@ __device__ __forceinline__ void beam_tail(const BeamLds& L, uint32_t* Uw, uint32
       for (int r = 0; r < kFusedSort / BLOCK; ++r)
         if (kc[r] && (kc[r] >> cut.shift) >= cut.prefix) cand[atomicAdd(&sm_n, 1u)] = kc[r];
       __syncthreads();
-      rank_candidates<BLOCK>(cand, static_cast<int>(sm_n), n_order,
-                             [&](int r, unsigned long long key) {
-                               const int32_t c = static_cast<int32_t>(
-                                   0xffffffffu - static_cast<uint32_t>(key & 0xffffffffull));
-                               out_order[r] = c;
-                               if (out_val) out_val[r] = sm_w[c];
-                               sm_ord[r] = c;
-                             });
+      rank_candidates<BLOCK>(cand, static_cast<int>(sm_n), n_order, emit);
       if (out_kept) {
         __syncthreads();
         keep_columns<BLOCK>(Uw, out_kept, sm_ord, A, C, n_order);
