@@ -379,7 +379,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   float* sm_w = reinterpret_cast<float*>(sel_cand + kTopkCand);
   int32_t* sm_ord = reinterpret_cast<int32_t*>(sm_w + kFusedSort);
   float* ctab = reinterpret_cast<float*>(pool);
-  __shared__ uint32_t sm_tw[BLOCK / 64];
+  __shared__ uint32_t sm_tw[2 * BLOCK / 64];
   __shared__ int sm_res[2];
   __shared__ uint32_t sm_n;
   const BeamLds L{keys, keys2, sel_cand, sm_w, sm_ord, sm_tw, sm_res, &sm_n};
@@ -473,6 +473,22 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   beam_tail<BLOCK>(L, Uw, wkey, W, A, C, kind, eps, n_order, n2, out_order, out_val, out_kept);
 }
 
+// wave-bound selection in the decode proposer (chunk and merge): every block shape
+// (CS_WB_ALL=1) or the 256-thread blocks with K <= 16 only (CS_WB_ALL=0)
+#ifndef CS_WB_ALL
+#define CS_WB_ALL 0
+#endif
+#define CS_WB_ON(BL, KK) \
+  (CS_WB_ALL ? wave_bound_ok<BL>(KK) : ((BL) <= 256 && (KK) <= kWaveBoundMaxK))
+#ifndef CS_PROP_PRIO
+#define CS_PROP_PRIO 2   // instruction-issue priority of the proposer waves
+#endif
+#ifndef CS_DECODE_KP1024
+#define CS_DECODE_KP1024 8   // proposer keys per lane in the 1024-thread blocks (4 or this)
+#endif
+#ifndef CS_DECODE_UN1024
+#define CS_DECODE_UN1024 2   // 16-byte vectors in flight per lane in the 1024-thread rows
+#endif
 // ---------------------------------------------------------------------------
 // beam decode step: proposer + scoring in ONE launch
 // ---------------------------------------------------------------------------
@@ -496,7 +512,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
 // C5's B = 8), so the proposer finishes under the agent-row stream (tools/beam_ab.py
 // --sweep; profiles/r01f_beam_ab*.jsonl).  CS_DECODE_KP overrides (4, 8 or 16).
 int decode_kp(int32_t B, int64_t vocab, int32_t block, int32_t K) {
-  const int big = block >= 1024 ? 8 : 16;
+  const int big = block >= 1024 ? CS_DECODE_KP1024 : 16;
   if (const char* e = getenv("CS_DECODE_KP")) {
     const int v = atoi(e);
     if (v == 4 || v == big) return v;
@@ -564,7 +580,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   float* sm_w = reinterpret_cast<float*>(sel_cand + kTopkCand);
   int32_t* sm_ord = reinterpret_cast<int32_t*>(sm_w + kFusedSort);
   float* ctab = reinterpret_cast<float*>(pool);
-  __shared__ uint32_t sm_tw[BLOCK / 64];
+  __shared__ uint32_t sm_tw[2 * BLOCK / 64];
   __shared__ int sm_res[2];
   __shared__ uint32_t sm_n;
   const BeamLds L{keys, keys2, sel_cand, sm_w, sm_ord, sm_tw, sm_res, &sm_n};
@@ -589,7 +605,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     // ---- proposer chunk ----
     // the proposer's short latency chain goes first when it shares a CU with a streaming
     // row block (instruction issue priority; the stream is bandwidth-bound, not issue-bound)
-    __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(CS_PROP_PRIO);
     DEC_T(if (tid == 0) atomicMax(&g_dec_ts[1], q0);)
     constexpr int CH = KP * BLOCK;
     const int32_t b = pblk / nchunk_p;
@@ -638,7 +654,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     bool have = false;   // candidates collected (block-uniform)
     // (256-thread variants only: in the 1024-thread ones the extra code's registers slow
     // the agent-row stream more than the bound saves; profiles/r01h_decode_wave_bound.jsonl)
-    if (BLOCK <= 256 && K <= kWaveBoundMaxK) {
+    if (CS_WB_ON(BLOCK, K)) {
       uint32_t lm = 0u;
 #pragma unroll
       for (int j = 0; j < KP; ++j)
@@ -719,7 +735,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
       }
     };
     bool mhave = false;
-    if (BLOCK <= 256 && K <= kWaveBoundMaxK && cached) {
+    if (CS_WB_ON(BLOCK, K) && cached) {
       uint32_t lm = 0u;
 #pragma unroll
       for (int r = 0; r < MR; ++r) lm = max(lm, static_cast<uint32_t>(mk[r] >> 32));
@@ -1065,8 +1081,8 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
       if (d.kp == 4) CS_DECODE_GO(DTV, CAPV, FIXV, 256, 8, 4);                                    \
       else CS_DECODE_GO(DTV, CAPV, FIXV, 256, 8, 16);                                             \
     } else {                                                                                       \
-      if (d.kp == 4) CS_DECODE_GO(DTV, CAPV, FIXV, 1024, 2, 4);                                   \
-      else CS_DECODE_GO(DTV, CAPV, FIXV, 1024, 2, 8);                                             \
+      if (d.kp == 4) CS_DECODE_GO(DTV, CAPV, FIXV, 1024, CS_DECODE_UN1024, 4);                    \
+      else CS_DECODE_GO(DTV, CAPV, FIXV, 1024, CS_DECODE_UN1024, CS_DECODE_KP1024);               \
     }                                                                                              \
   } while (0)
   if (dtype == CS_F32) {

@@ -611,15 +611,22 @@ __device__ __forceinline__ RadixCut radix_select(ForEach for_each, uint32_t k, u
   }
 }
 
-// Lower bound on the k-th largest of a block's 32-bit order keys, for small k: each lane
-// passes its largest key; per wave the k-th largest of those 64 (a wave64 bitonic sort in
-// registers) -- at least k of the wave's keys are >= it, so every key among the block's k
-// largest is >= the largest such bound over the waves.  With k of a few dozen or less
-// only about k..2k keys pass it, so collecting them and rank-counting replaces the
-// histogram passes of radix_select (no LDS atomics on hot bins, two barriers).
-// sm_t holds BLOCK / 64 words.  Returns 0 (every key passes) when a wave has < k keys.
+// Lower bound on the k-th largest of a block's 32-bit order keys: each lane passes its
+// largest key and every wave sorts those 64 (a wave64 bitonic sort in registers).  Two
+// bounds come out of that sort, both valid, and the larger is returned:
+//   * (k <= 64) the largest over the waves of each wave's k-th largest lane maximum: at
+//     least k keys of that wave are >= it;
+//   * the smallest over the NW = BLOCK / 64 waves of each wave's ceil(k / NW)-th largest
+//     lane maximum: every wave holds ceil(k / NW) keys >= it, NW * ceil(k / NW) >= k.
+// The first is tight for small k, the second for k of tens to hundreds spread over many
+// waves (a C3 proposer chunk, k = 50 of 8,192 keys in 16 waves, passes ~100 keys).  Every
+// key among the block's k largest is >= the bound, so collecting those and rank-counting
+// replaces the histogram passes of radix_select (no LDS atomics on hot bins, two
+// barriers).  sm_t holds 2 * BLOCK / 64 words.  Returns 0 (every key passes) when a wave
+// has too few keys.
 template <int BLOCK>
 __device__ __forceinline__ uint32_t wave_bound(uint32_t lane_max, int k, uint32_t* sm_t) {
+  constexpr int NW = BLOCK / 64;
   const int lane = threadIdx.x & 63;
   uint32_t v = lane_max;
 #pragma unroll
@@ -631,14 +638,24 @@ __device__ __forceinline__ uint32_t wave_bound(uint32_t lane_max, int k, uint32_
       v = keep_max ? max(v, o) : min(v, o);
     }
   }
-  const uint32_t t = __shfl(v, k - 1, 64);
-  if (lane == 0) sm_t[threadIdx.x >> 6] = t;
+  const uint32_t t1 = k <= 64 ? __shfl(v, k - 1, 64) : 0u;
+  const uint32_t t2 = __shfl(v, (k + NW - 1) / NW - 1, 64);
+  if (lane == 0) {
+    sm_t[threadIdx.x >> 6] = t1;
+    sm_t[NW + (threadIdx.x >> 6)] = t2;
+  }
   __syncthreads();
-  uint32_t b = 0;
+  uint32_t b1 = 0u, b2 = 0xffffffffu;
 #pragma unroll
-  for (int w = 0; w < BLOCK / 64; ++w) b = max(b, sm_t[w]);
-  return b;
+  for (int w = 0; w < NW; ++w) {
+    b1 = max(b1, sm_t[w]);
+    b2 = min(b2, sm_t[NW + w]);
+  }
+  return max(b1, b2);
 }
+// the bound needs ceil(k / NW) <= 64
+template <int BLOCK>
+__host__ __device__ constexpr bool wave_bound_ok(int k) { return k <= 64 * (BLOCK / 64); }
 constexpr int kWaveBoundMaxK = 16;   // larger k: radix_select (the bound passes too many)
 
 }  // namespace
