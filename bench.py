@@ -116,7 +116,7 @@ def init_dist(n_gpus, backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or os.environ.get("CS_BENCH_FORCE_SHARDED") == "1":
         if backend == "gloo":   # rehearsal: every rank on the one visible GPU
             torch.cuda.set_device(0)
             torch.distributed.init_process_group("gloo")
@@ -227,7 +227,7 @@ def gpu_busy(stream, ms=20.0):
                 a = a @ a.T * 1e-3
 
 
-def run_beam(name, world, rank, dev, steps, warmup):
+def run_beam(name, world, rank, dev, steps, warmup, comm=None):
     """Beam-search decode steps on resident logits (BASELINE C1 / C3 / C5).
 
     One decode step, per rank:
@@ -238,8 +238,9 @@ def run_beam(name, world, rank, dev, steps, warmup):
     (the reference's walk over the sorted candidates, beam_search.py:562-600, keeps the
     first beam_width; synthetic candidates have no duplicates / EOS, so the B best are
     exactly what it keeps, and the launch selects just those)
-    At N = 1 the whole step is one captured hipGraph; with agents sharded, the per-rank
-    parts are two graphs around the eager all-reduce.
+    At N = 1 two whole steps are one captured hipGraph; with agents sharded a step is the
+    all-reduce (one ncclAllReduce on the stream through parallel.RcclComm) followed by
+    one graph holding this step's selection (cs_beam_select) and the next step's scoring.
     """
     ops = importlib.import_module(PKG_DIR + ".ops")
     par = importlib.import_module(PKG_DIR + ".parallel")
@@ -255,70 +256,74 @@ def run_beam(name, world, rank, dev, steps, warmup):
     Rs = [torch.zeros(A_loc, B, dtype=torch.float32, device=dev) for _ in range(2)]
     R = Rs[0]
     ws_p, ws_b, ws_d = ops.Workspace(), ops.Workspace(zeroed=True), ops.Workspace(zeroed=True)
-    sharded = world > 1
+    sharded = world > 1 or os.environ.get("CS_BENCH_FORCE_SHARDED") == "1"   # (diagnostics: the sharded step on one rank)
+
+    # sharded: persistent U / W buffers so that one captured graph can run the select of
+    # step i and the scoring of step i + 1 back to back; W is all-reduced in place
+    U_buf = torch.empty(A_loc, C, dtype=torch.float32, device=dev)
+    Wx = torch.full((C,), float("inf"), dtype=torch.float32, device=dev)
 
     def score(i=0):
-        if A_loc == 0:   # more ranks than agents: this rank only proposes
+        if A_loc == 0:   # more ranks than agents: this rank only proposes (W stays +inf)
             ops.vocab_topk(ref, K, softcap=cap, workspace=ws_p)
-            return (torch.empty(0, C, device=dev),
-                    torch.full((C,), float("inf"), device=dev), None)
+            return
         if not sharded:
             # propose + score + keep the B best in ONE launch (cs_beam_decode_step): the
             # proposer runs beside the agent-row stream; the launch selects the B best
             # (radix select, no full sort) and writes their cumulative rewards
-            _, U, W, order, _ = ops.beam_decode_step(ref, ag, Rs[i % 2], K, "min", n_order=B,
-                                                     softcap=cap, workspace=ws_d,
-                                                     kept_out=Rs[(i + 1) % 2])
-            return U, W, order
-        # sharded: every rank proposes the same candidates (same launch, no order); W is
-        # all-reduced before the selection
-        _, U, W, _, _ = ops.beam_decode_step(ref, ag, Rs[i % 2], K, "min", n_order=0,
-                                             softcap=cap, workspace=ws_d)
-        return U, W, None
+            ops.beam_decode_step(ref, ag, Rs[i % 2], K, "min", n_order=B, softcap=cap,
+                                 workspace=ws_d, kept_out=Rs[(i + 1) % 2])
+            return
+        # sharded: every rank proposes the same candidates (same launch, no order); a
+        # column with no usable utility on this rank must not win the MIN all-reduce
+        ops.beam_decode_step(ref, ag, R, K, "min", n_order=0, softcap=cap, workspace=ws_d,
+                             out_U=U_buf, out_W=Wx)
+        Wx.nan_to_num_(nan=float("inf"), posinf=float("inf"), neginf=float("-inf"))
 
-    def keep(U, order):
-        R.copy_(U.index_select(1, order[:B].long()))
-
-    def select(U, W):
-        W = torch.where(torch.isinf(W) & (W > 0), torch.full_like(W, float("nan")), W)
-        order, _ = ops.topk(W, B)
-        keep(U, order)
+    def select():
+        # one launch: +inf -> NaN, stable top-B, the kept beams' rewards (cs_beam_select)
+        ops.beam_select(Wx, B, U=U_buf, unfill="min", kept_out=R)
 
     s = torch.cuda.Stream(device=dev)
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         for i in range(4):   # warm the workspaces / allocator before capture
-            U, W, order = score(i)
+            score(i)
+            if sharded:
+                select()
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     with torch.cuda.graph(g1):
         if not sharded:      # two decode steps per replay (the reward buffers ping-pong)
             score(0)
-            U, W, order = score(1)
-        else:
-            U, W, order = score()
-            Wx = torch.where(torch.isnan(W), torch.full_like(W, float("inf")), W)
+            score(1)
+        else:                # prologue: the first step's scoring
+            score()
     if sharded:
-        with torch.cuda.graph(g2):
-            select(U, Wx)
+        with torch.cuda.graph(g2):   # select of step i, scoring of step i + 1
+            select()
+            score()
     per_replay = 1 if sharded else 2
     steps = max(per_replay, steps - steps % per_replay)
 
-    coll_ev = []
-
-    def step(timed=False):
-        g1.replay()
-        if sharded:
-            if timed:
-                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                e[0].record()
+    def all_reduce_min():
+        # the direct RCCL communicator (parallel.RcclComm: one ncclAllReduce on the stream,
+        # a few us of host time) when there is one, else the ProcessGroup call
+        if comm is not None:
+            comm.all_reduce(Wx, comm.MIN)
+        else:
             torch.distributed.all_reduce(Wx, op=torch.distributed.ReduceOp.MIN)
-            if timed:
-                e[1].record()
-                coll_ev.append(e)
-            g2.replay()
 
+    def step():
+        if sharded:          # one step = the exchange + select + the next scoring
+            all_reduce_min()
+            g2.replay()
+        else:
+            g1.replay()
+
+    if sharded:
+        g1.replay()
     for _ in range(max(1, warmup // per_replay)):
         step()
     torch.cuda.synchronize()
@@ -327,12 +332,33 @@ def run_beam(name, world, rank, dev, steps, warmup):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps // per_replay):
-        step(timed=True)
+        step()
     torch.cuda.synchronize()
     if sharded:
         torch.distributed.barrier()
     el = time.perf_counter() - t0
-    coll_ms = float(np.mean([a.elapsed_time(b) for a, b in coll_ev])) if coll_ev else None
+    coll_ms, split_us = None, None
+    if sharded:   # the exchange alone, HIP events around it (outside the timed steps)
+        coll_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(20)]
+        for e0, e1 in coll_ev:
+            e0.record()
+            all_reduce_min()
+            e1.record()
+        torch.cuda.synchronize()
+        coll_ms = float(np.median([a.elapsed_time(b) for a, b in coll_ev]))
+        # GPU-side split of a sharded step (queue kept full, so host gaps do not count)
+        parts = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(20)]
+        gpu_busy(torch.cuda.current_stream())
+        for e in parts:
+            e[0].record()
+            all_reduce_min()
+            e[1].record()
+            g2.replay()
+            e[2].record()
+        torch.cuda.synchronize()
+        split_us = {n: float(np.median([e[i].elapsed_time(e[i + 1]) for e in parts])) * 1e3
+                    for i, n in enumerate(("all_reduce", "select_and_next_scoring_graph"))}
     if sharded:
         tt = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -368,8 +394,11 @@ def run_beam(name, world, rank, dev, steps, warmup):
                          "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
                          "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
-            "collective": {"op": "all_reduce(MIN) of W" if sharded else "none (1 GPU)",
+            "collective": {"op": ("all_reduce(MIN) of W" + (" (direct RCCL communicator)" if comm
+                                                             else " (ProcessGroup)")
+                                  if sharded else "none (1 GPU)"),
                            "bytes": C * 4 if sharded else 0, "ms_per_step": coll_ms},
+            "gpu_split_us": split_us,
             "step_bytes": (A_loc * B + B) * V * esz,
             "step_frac_of_hbm": (A_loc * B + B) * V * esz / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
@@ -498,8 +527,18 @@ def main():
         if e2e is not None:
             line["end_to_end"] = e2e
     beam = {}
-    for name in [b for b in args.beam.split(",") if b]:
-        beam[name] = run_beam(name, world, rank, dev, args.beam_steps, 20)
+    beams = [b for b in args.beam.split(",") if b]
+    comm = None
+    if beams and torch.distributed.is_initialized() and args.backend == "nccl":
+        try:
+            comm = par.RcclComm()
+        except Exception as e:   # every rank fails alike (library / symbol): ProcessGroup path
+            print(f"bench: direct RCCL communicator unavailable ({e}); using the ProcessGroup",
+                  file=sys.stderr, flush=True)
+    for name in beams:
+        beam[name] = run_beam(name, world, rank, dev, args.beam_steps, 20, comm)
+    if comm is not None:
+        comm.close()
     if rank == 0:
         if beam:
             line["beam"] = beam

@@ -25,7 +25,7 @@ EXPORTED = (
     "cs_segment_reduce", "cs_welfare_reduce", "cs_segmented_topk", "cs_vocab_topk_workspace_size",
     "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
-    "cs_beam_decode_step",
+    "cs_beam_decode_step", "cs_beam_select",
 )
 
 
@@ -92,6 +92,8 @@ def load():
                                       ctypes.c_int, f32, vp, vp, vp, i32, vp, vp, vp, vp,
                                       ctypes.c_size_t, vp]
     L.cs_beam_decode_step.restype = ctypes.c_int
+    L.cs_beam_select.argtypes = [vp, i32, ctypes.c_int, vp, i32, i32, vp, vp, vp, vp, vp]
+    L.cs_beam_select.restype = ctypes.c_int
     _lib = L
     return L
 

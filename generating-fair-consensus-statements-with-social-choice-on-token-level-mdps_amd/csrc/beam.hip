@@ -217,6 +217,13 @@ struct BeamLds {
   uint32_t* sm_n;
 };
 
+template <int BLOCK>
+__device__ __forceinline__ void beam_order(const BeamLds& L, uint32_t* Uw, int32_t A, int32_t C,
+                                           int32_t n_order, int32_t n2,
+                                           int32_t* __restrict__ out_order,
+                                           float* __restrict__ out_val,
+                                           float* __restrict__ out_kept);
+
 // Run by the last workgroup of a beam step once every U value (and, for MIN / MAX, every
 // welfare key) is published: W for every candidate, then the order (radix-select top-n
 // or the full bitonic sort) and the kept beams' rewards.
@@ -257,6 +264,27 @@ __device__ __forceinline__ void beam_tail(const BeamLds& L, uint32_t* Uw, uint32
     }
   }
   if (!sort_here) return;  // block-uniform
+  beam_order<BLOCK>(L, Uw, A, C, n_order, n2, out_order, out_val, out_kept);
+}
+
+// The order of the C welfare values in L.sm_w (written by the calling block): the n_order
+// best (radix-select threshold / wave bound + rank counting, or the full bitonic sort) by
+// (W desc, index asc), NaN last, and the kept beams' rewards out_kept[a][r] = U[a][order[r]].
+template <int BLOCK>
+__device__ __forceinline__ void beam_order(const BeamLds& L, uint32_t* Uw, int32_t A, int32_t C,
+                                           int32_t n_order, int32_t n2,
+                                           int32_t* __restrict__ out_order,
+                                           float* __restrict__ out_val,
+                                           float* __restrict__ out_kept) {
+  const int tid = threadIdx.x;
+  unsigned long long* keys = L.keys;
+  unsigned long long* keys2 = L.keys2;
+  unsigned long long* sel_cand = L.sel_cand;
+  float* sm_w = L.sm_w;
+  int32_t* sm_ord = L.sm_ord;
+  uint32_t* sm_tw = L.sm_tw;
+  int* sm_res = L.sm_res;
+  uint32_t& sm_n = *L.sm_n;
   __syncthreads();
   if (n_order <= kSelectMax) {
     // the n_order best by histogram threshold + rank counting (as vocab_topk): the
@@ -864,7 +892,54 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
 
 }  // namespace
 
+namespace {
+// cs_beam_select: one workgroup orders C <= kFusedSort welfare values and keeps the
+// rewards of the n_order best columns (beam_order), after the agent-sharded all-reduce.
+constexpr int kSelectBlock = 256;
+__global__ __launch_bounds__(kSelectBlock) void beam_select_kernel(
+    const float* __restrict__ Win, int32_t C, int unfill, uint32_t* __restrict__ Uw, int32_t A,
+    float* __restrict__ W_out, int32_t n_order, int32_t n2, int32_t* __restrict__ out_order,
+    float* __restrict__ out_val, float* __restrict__ out_kept) {
+  __shared__ __attribute__((aligned(16))) unsigned long long pool[2 * kFusedSort + kTopkCand + kFusedSort];
+  __shared__ uint32_t sm_tw[2 * kSelectBlock / 64];
+  __shared__ int sm_res[2];
+  __shared__ uint32_t sm_n;
+  unsigned long long* sel_cand = pool + 2 * kFusedSort;
+  float* sm_w = reinterpret_cast<float*>(sel_cand + kTopkCand);
+  int32_t* sm_ord = reinterpret_cast<int32_t*>(sm_w + kFusedSort);
+  const BeamLds L{pool, pool + kFusedSort, sel_cand, sm_w, sm_ord, sm_tw, sm_res, &sm_n};
+  for (int32_t c = threadIdx.x; c < C; c += kSelectBlock) {
+    float w = Win[c];
+    if ((unfill == CS_UNFILL_POSINF && w == INFINITY) || (unfill == CS_UNFILL_NEGINF && w == -INFINITY))
+      w = __builtin_nanf("");
+    sm_w[c] = w;
+    if (W_out) W_out[c] = w;
+  }
+  beam_order<kSelectBlock>(L, Uw, A, C, n_order, n2, out_order, out_val, out_kept);
+}
+}  // namespace
+
 extern "C" {
+
+int cs_beam_select(const float* W, int32_t C, int unfill, const float* U, int32_t A,
+                   int32_t n_order, float* out_W, int32_t* out_order, float* out_order_val,
+                   float* out_kept, cs_stream_t stream) {
+  const char* w = "cs_beam_select: ";
+  if (C <= 0 || C > kFusedSort) return fail(CS_ERR_INVALID, std::string(w) + "need 0 < C <= 1024");
+  if (n_order <= 0 || n_order > C) return fail(CS_ERR_INVALID, std::string(w) + "need 0 < n_order <= C");
+  if (unfill != CS_UNFILL_NONE && unfill != CS_UNFILL_POSINF && unfill != CS_UNFILL_NEGINF)
+    return fail(CS_ERR_INVALID, std::string(w) + "unknown unfill mode");
+  if (A < 0) return fail(CS_ERR_INVALID, std::string(w) + "need A >= 0");
+  if (!W || !out_order || (out_kept && A > 0 && !U))
+    return fail(CS_ERR_INVALID, std::string(w) + "NULL pointer");
+  int32_t n2 = 2;
+  while (n2 < C) n2 <<= 1;
+  hipLaunchKernelGGL(beam_select_kernel, dim3(1), dim3(kSelectBlock), 0,
+                     static_cast<hipStream_t>(stream), W, C, unfill,
+                     reinterpret_cast<uint32_t*>(const_cast<float*>(U)), out_kept ? A : 0, out_W,
+                     n_order, n2, out_order, out_order_val, out_kept);
+  return check_launch("cs_beam_select");
+}
 
 size_t cs_beam_step_workspace_size(int64_t rows, int64_t vocab) {
   if (rows <= 0 || vocab <= 0) return 0;

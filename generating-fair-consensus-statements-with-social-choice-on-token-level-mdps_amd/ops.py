@@ -200,10 +200,50 @@ def topk(W: torch.Tensor, k: int, *, with_values: bool = True):
     return idx, val
 
 
+UNFILL = {None: 0, "none": 0, "+inf": 1, "min": 1, "-inf": 2, "max": 2}
+
+
+def beam_select(W: torch.Tensor, n_order: int, *, U: Optional[torch.Tensor] = None,
+                unfill=None, kept_out: Optional[torch.Tensor] = None, W_out: Optional[torch.Tensor] = None,
+                with_values: bool = False):
+    """Selection half of an agent-sharded beam step, one launch (cs_beam_select).
+
+    W [C] float32 all-reduced welfare (C <= 1024); unfill '+inf'/'min' maps +inf back to
+    NaN (the MIN combine's fill for columns without a usable utility), '-inf'/'max' -inf.
+    Returns (order [n_order] int32 by (W desc, index asc), NaN last; values or None).
+    With U [A, C] (this rank's agents) and kept_out [A, n_order]: kept_out[a, r] =
+    U[a, order[r]], the kept beams' cumulative rewards.  W_out (nullable) receives W after
+    unfill.  Bit-identical to topk(W) + U.index_select(1, order).
+    Restates the stable sort + keep of beam_search.py:558-593 on one agent shard."""
+    L = _lib.load()
+    if W.dim() != 1 or W.dtype != torch.float32 or not W.is_contiguous():
+        raise CSError("W must be a contiguous 1-D float32 tensor")
+    _require_cuda(W)
+    C = W.shape[0]
+    A = 0
+    if kept_out is not None:
+        if U is None or U.dtype != torch.float32 or not U.is_contiguous() or U.dim() != 2 \
+                or U.shape[1] != C:
+            raise CSError("kept_out needs U [A, C] contiguous float32")
+        A = U.shape[0]
+        if kept_out.shape != (A, n_order) or kept_out.dtype != torch.float32 \
+                or not kept_out.is_contiguous():
+            raise CSError("kept_out must be [A, n_order] contiguous float32")
+    order = torch.empty(n_order, dtype=torch.int32, device=W.device)
+    val = torch.empty(n_order, dtype=torch.float32, device=W.device) if with_values else None
+    rc = L.cs_beam_select(W.data_ptr(), C, UNFILL[unfill], U.data_ptr() if A else None, A,
+                          int(n_order), W_out.data_ptr() if W_out is not None else None,
+                          order.data_ptr(), val.data_ptr() if val is not None else None,
+                          kept_out.data_ptr() if kept_out is not None else None, _stream())
+    _lib.check(rc, "cs_beam_select")
+    return order, val
+
+
 def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor, kind="min", *,
               n_order: Optional[int] = None, vocab: Optional[int] = None, softcap: float = 0.0,
               eps: float = 1e-9, workspace: Optional[Workspace] = None,
-              kept_out: Optional[torch.Tensor] = None):
+              kept_out: Optional[torch.Tensor] = None,
+              out_U: Optional[torch.Tensor] = None, out_W: Optional[torch.Tensor] = None):
     """One beam-search scoring step after the LM head, fused into one launch.
 
     logits  [A*B, ld] agent rows (row a*B + b = agent a, beam b);
@@ -237,8 +277,11 @@ def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor
     C = B * K
     n_order = C if n_order is None else int(n_order)
     dev = logits.device
-    U = torch.empty((A, C), dtype=torch.float32, device=dev)
-    W = torch.empty(C, dtype=torch.float32, device=dev)
+    U = torch.empty((A, C), dtype=torch.float32, device=dev) if out_U is None else out_U
+    W = torch.empty(C, dtype=torch.float32, device=dev) if out_W is None else out_W
+    if (U.shape != (A, C) or W.shape != (C,) or U.dtype != torch.float32 or
+            W.dtype != torch.float32 or not U.is_contiguous() or not W.is_contiguous()):
+        raise CSError(f"out_U / out_W must be contiguous float32 [{A}, {C}] / [{C}]")
     order = torch.empty(max(n_order, 0), dtype=torch.int32, device=dev)
     oval = torch.empty(max(n_order, 0), dtype=torch.float32, device=dev)
     nbytes = int(L.cs_beam_step_workspace_size(rows, vocab))
@@ -269,7 +312,8 @@ def beam_decode_step(ref_logits: torch.Tensor, logits: torch.Tensor, rewards: to
                      k: int, kind="min", *, n_order: Optional[int] = None,
                      vocab: Optional[int] = None, softcap: float = 0.0, eps: float = 1e-9,
                      workspace: Optional[Workspace] = None,
-                     kept_out: Optional[torch.Tensor] = None):
+                     kept_out: Optional[torch.Tensor] = None,
+                     out_U: Optional[torch.Tensor] = None, out_W: Optional[torch.Tensor] = None):
     """Proposer + scoring of one beam decode step in ONE launch (cs_beam_decode_step).
 
     ref_logits [B, ld_ref] reference-policy rows; logits [A*B, ld] agent rows (row a*B+b);
@@ -296,8 +340,11 @@ def beam_decode_step(ref_logits: torch.Tensor, logits: torch.Tensor, rewards: to
     n_order = C if n_order is None else int(n_order)
     dev = logits.device
     ids = torch.empty((B, k), dtype=torch.int32, device=dev)
-    U = torch.empty((A, C), dtype=torch.float32, device=dev)
-    W = torch.empty(C, dtype=torch.float32, device=dev)
+    U = torch.empty((A, C), dtype=torch.float32, device=dev) if out_U is None else out_U
+    W = torch.empty(C, dtype=torch.float32, device=dev) if out_W is None else out_W
+    if (U.shape != (A, C) or W.shape != (C,) or U.dtype != torch.float32 or
+            W.dtype != torch.float32 or not U.is_contiguous() or not W.is_contiguous()):
+        raise CSError(f"out_U / out_W must be contiguous float32 [{A}, {C}] / [{C}]")
     order = torch.empty(max(n_order, 0), dtype=torch.int32, device=dev)
     oval = torch.empty(max(n_order, 0), dtype=torch.float32, device=dev)
     nbytes = int(L.cs_beam_decode_workspace_size(A, B, vocab, k))

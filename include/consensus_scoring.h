@@ -203,6 +203,28 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
                         size_t workspace_bytes, cs_stream_t stream);
 
 /*
+ * cs_beam_select — the selection half of an agent-sharded beam step, after the welfare
+ * all-reduce: out_order[r] = index of rank r of W by (W desc, index asc), NaN last,
+ * r < n_order (as cs_segmented_topk); out_order_val (nullable) = W there; out_kept
+ * (nullable) [A][n_order] = U[a*C + out_order[r]] for this rank's A agents (U [A][C],
+ * the out_U of its cs_beam_decode_step / cs_beam_step); out_W (nullable) = W after
+ * unfill.  unfill: CS_UNFILL_POSINF turns +inf back into NaN (the MIN combine fills
+ * columns without a usable utility with +inf before the all-reduce, parallel.py),
+ * CS_UNFILL_NEGINF does the same for -inf (MAX), CS_UNFILL_NONE leaves W as is.
+ * One workgroup, one launch; C <= 1024, 0 < n_order <= C.  Bit-identical to
+ * cs_segmented_topk + the column gather.
+ *
+ * Replaces: the stable sort by min over agents and the keep of the first beam_width of
+ *   src/methods/beam_search.py:558-593 on a rank that holds a subset of the agents.
+ */
+#define CS_UNFILL_NONE 0
+#define CS_UNFILL_POSINF 1
+#define CS_UNFILL_NEGINF 2
+int cs_beam_select(const float* W, int32_t C, int unfill, const float* U, int32_t A,
+                   int32_t n_order, float* out_W, int32_t* out_order, float* out_order_val,
+                   float* out_kept, cs_stream_t stream);
+
+/*
  * cs_vocab_topk — deterministic candidate proposer: the k largest (soft-capped)
  * logits of every row, ordered by (value desc, token id asc).
  *

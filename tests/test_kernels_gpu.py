@@ -367,6 +367,50 @@ def test_beam_step_sort_skipped_for_sharded_runs(ops, dev):
         ops.beam_step(x, t, torch.zeros(A, B + 1, device=dev), "min")
 
 
+@pytest.mark.parametrize("C,n,case", [(40, 4, "rand"), (256, 8, "rand"), (800, 16, "rand"),
+                                      (1024, 300, "rand"), (800, 16, "ties"), (512, 64, "clustered"),
+                                      (97, 97, "rand"), (1, 1, "rand")])
+def test_beam_select_is_topk_plus_keep(ops, orc, dev, C, n, case):
+    """cs_beam_select (sharded tail: unfill, stable top-n, kept columns) == the unfused
+    where + cs_segmented_topk + index_select, and == the oracle's stable order."""
+    g = torch.Generator(device=dev).manual_seed(C * 7 + n)
+    A = 3
+    U = torch.randn(A, C, generator=g, device=dev) * 4.0
+    if case == "ties":
+        U = torch.round(U)
+    if case == "clustered":
+        U = U * 1e-3 - 2.5e6
+    W = U.min(0).values
+    if C > 4:   # columns without a usable utility: filled with +inf before the MIN all-reduce
+        W[3] = float("nan")
+        W[C // 2] = float("nan")
+    Wx = torch.where(torch.isnan(W), torch.full_like(W, float("inf")), W)
+    kept = torch.empty(A, n, device=dev)
+    W_out = torch.empty_like(W)
+    order, val = ops.beam_select(Wx, n, U=U, unfill="min", kept_out=kept, W_out=W_out,
+                                 with_values=True)
+    Wn = torch.where(torch.isinf(Wx) & (Wx > 0), torch.full_like(Wx, float("nan")), Wx)
+    ref_order, ref_val = ops.topk(Wn, n)
+    assert torch.equal(order, ref_order)
+    assert torch.equal(torch.nan_to_num(val, nan=1234.5), torch.nan_to_num(ref_val, nan=1234.5))
+    assert torch.equal(kept, U.index_select(1, ref_order.long()))
+    assert torch.equal(torch.isnan(W_out), torch.isnan(W)) and \
+        torch.equal(torch.nan_to_num(W_out), torch.nan_to_num(W))
+    assert np.array_equal(order.cpu().numpy(), orc.topk(Wn.cpu().numpy().astype(np.float64), n)[0])
+    o2, v2 = ops.beam_select(Wn, n)                 # no unfill, no kept
+    assert torch.equal(o2, ref_order) and v2 is None
+
+
+def test_beam_select_rejects_bad_arguments(ops, dev):
+    W = torch.randn(2000, device=dev)
+    with pytest.raises(ops.CSError):
+        ops.beam_select(W, 4)                        # C > 1024
+    with pytest.raises(ops.CSError):
+        ops.beam_select(W[:10], 11)                  # n_order > C
+    with pytest.raises(ops.CSError):
+        ops.beam_select(W[:10], 0)
+
+
 def test_beam_step_partial_order_with_ties_and_nan(ops, dev):
     """Every candidate ties (constant rows, equal rewards) except a few NaN slots: the
     threshold-selection order must still be index order with NaN last."""
