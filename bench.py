@@ -256,7 +256,8 @@ def run_beam(name, world, rank, dev, steps, warmup, comm=None):
     Rs = [torch.zeros(A_loc, B, dtype=torch.float32, device=dev) for _ in range(2)]
     R = Rs[0]
     ws_p, ws_b, ws_d = ops.Workspace(), ops.Workspace(zeroed=True), ops.Workspace(zeroed=True)
-    sharded = world > 1 or os.environ.get("CS_BENCH_FORCE_SHARDED") == "1"   # (diagnostics: the sharded step on one rank)
+    # CS_BENCH_FORCE_SHARDED=1 (diagnostics): the sharded step on one rank, under torchrun
+    sharded = world > 1 or os.environ.get("CS_BENCH_FORCE_SHARDED") == "1"
 
     # sharded: persistent U / W buffers so that one captured graph can run the select of
     # step i and the scoring of step i + 1 back to back; W is all-reduced in place

@@ -75,6 +75,54 @@ __global__ __launch_bounds__(256) void welfare_kernel(const float* __restrict__ 
   W[c] = any ? static_cast<float>(acc) : __builtin_nanf("");
 }
 
+// ---------------------------------------------------------------------------
+// stable top-k by selection (k <= kTopkSelectMax): one 256-thread workgroup per segment,
+// radix select over the (order key, ~index) composite keys read straight from W (one
+// coalesced pass per digit, no key array), the <= k + 64 survivors ranked by counting.
+// The keys are distinct, so the result is exactly the full sort's first k (value desc,
+// index asc, NaN last) — what topk_kernel's LDS bitonic gives, without its log^2(n)
+// barrier stages (55 for 1,024 slots).
+// ---------------------------------------------------------------------------
+constexpr int kTopkSelectMax = 256;
+
+__global__ __launch_bounds__(256) void topk_select_kernel(const float* __restrict__ W,
+                                                          int32_t seg_len, int64_t ld, int32_t k,
+                                                          int32_t* __restrict__ out_idx,
+                                                          float* __restrict__ out_val) {
+  __shared__ uint32_t hist[kTopkBins];
+  __shared__ unsigned long long cand[kTopkCand];
+  __shared__ uint32_t sm_w[256 / 64];
+  __shared__ int sm_res[2];
+  __shared__ uint32_t sm_n;
+  const int64_t seg = blockIdx.x;
+  const float* base = W + seg * ld;
+  const int tid = threadIdx.x;
+  auto key = [&](int i) -> unsigned long long {
+    return (static_cast<unsigned long long>(order_key(base[i])) << 32) |
+           static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(i));
+  };
+  auto each = [&](auto f) {
+    for (int i = tid; i < seg_len; i += 256) f(key(i));
+  };
+  if (tid == 0) sm_n = 0u;
+  // the last digit (shift 4) leaves at most k + 15 candidates: the 64-bit keys are distinct
+  const RadixCut cut = radix_select<256>(each, static_cast<uint32_t>(k),
+                                         static_cast<uint32_t>(k + 64), hist, sm_w, sm_res);
+  each([&](unsigned long long c) {
+    if ((c >> cut.shift) >= cut.prefix) {
+      const uint32_t at = atomicAdd(&sm_n, 1u);
+      if (at < kTopkCand) cand[at] = c;
+    }
+  });
+  __syncthreads();
+  const int nc = static_cast<int>(min(sm_n, static_cast<uint32_t>(kTopkCand)));
+  rank_candidates<256>(cand, nc, k, [&](int r, unsigned long long c) {
+    const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull);
+    out_idx[seg * k + r] = static_cast<int32_t>(idx);
+    if (out_val) out_val[seg * k + r] = base[idx];
+  });
+}
+
 }  // namespace
 
 extern "C" {
@@ -119,6 +167,11 @@ int cs_segmented_topk(const float* W, int32_t n_seg, int32_t seg_len, int64_t ld
   if (k > seg_len) return fail(CS_ERR_INVALID, "cs_segmented_topk: k > seg_len");
   if (n_seg == 0 || k == 0) return CS_OK;
   if (!W || !out_idx) return fail(CS_ERR_INVALID, "cs_segmented_topk: NULL pointer");
+  if (k <= kTopkSelectMax && seg_len > 64) {
+    hipLaunchKernelGGL(topk_select_kernel, dim3(static_cast<uint32_t>(n_seg)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), W, seg_len, ld, k, out_idx, out_val);
+    return check_launch("cs_segmented_topk");
+  }
   int32_t n2 = 2;
   while (n2 < seg_len) n2 <<= 1;
   hipLaunchKernelGGL(topk_kernel, dim3(static_cast<uint32_t>(n_seg)), dim3(256),

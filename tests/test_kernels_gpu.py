@@ -198,6 +198,35 @@ def test_topk_matches_stable_sort(ops, orc, dev, seg_len):
     assert np.array_equal(np.isnan(v), np.isnan(np.take_along_axis(W, ref, 1)))
 
 
+@pytest.mark.parametrize("seg_len", [65, 256, 800, 4096, 16384])
+@pytest.mark.parametrize("k", [1, 16, 255, 256])
+@pytest.mark.parametrize("case", ["ties", "clustered", "all_nan", "constant"])
+def test_topk_selection_path(ops, orc, dev, seg_len, k, case):
+    """k <= 256 of more than 64 values goes through the radix-select kernel: the exact
+    stable order (value desc, index asc, NaN last) under ties, one exponent bin, all-NaN
+    and constant segments, with a leading-dimension stride."""
+    if k > seg_len:
+        pytest.skip("k > seg_len")
+    rng = np.random.default_rng(seg_len * 31 + k)
+    n_seg, ld = 3, seg_len + 5
+    if case == "ties":
+        W = rng.integers(-3, 3, size=(n_seg, ld)).astype(np.float32)
+        W[:, rng.integers(0, seg_len, size=max(1, seg_len // 20))] = np.nan
+    elif case == "clustered":
+        W = (-2.5e6 - rng.random((n_seg, ld))).astype(np.float32)
+    elif case == "all_nan":
+        W = np.full((n_seg, ld), np.nan, dtype=np.float32)
+    else:
+        W = np.full((n_seg, ld), 1.25, dtype=np.float32)
+    Wt = torch.as_tensor(W, device=dev)[:, :seg_len]
+    idx, val = ops.topk(Wt, k)
+    ref = orc.topk(W[:, :seg_len].astype(np.float64), k)
+    assert np.array_equal(idx.cpu().numpy(), ref)
+    v = val.cpu().numpy()
+    r = np.take_along_axis(W[:, :seg_len], ref, 1)
+    assert np.array_equal(np.isnan(v), np.isnan(r)) and np.array_equal(v[~np.isnan(v)], r[~np.isnan(r)])
+
+
 def test_core_drop_in_matches_reference_golden(pkg, golden_dir, dev):
     import importlib
     core = importlib.import_module(pkg.__name__ + ".core")
