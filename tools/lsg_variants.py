@@ -16,7 +16,8 @@ sys.path.insert(0, REPO)
 ops = importlib.import_module(
     "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd.ops")
 
-NAMES = {0: "auto", 5: "b256_u4", 1: "b512_u4", 2: "b1024_u1", 3: "b1024_u2", 4: "b256_u8"}
+NAMES = {0: "auto", 5: "b256_u4", 1: "b512_u4", 2: "b1024_u1", 3: "b1024_u2", 4: "b256_u8",
+         6: "b1024_u4", 7: "b512_u8"}
 
 
 def main():
