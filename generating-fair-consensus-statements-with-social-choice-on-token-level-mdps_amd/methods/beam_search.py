@@ -14,6 +14,10 @@ Reference step (beam_search.py:439-617), same config keys:
     its beam, U = R + lp, min over agents, stable order over all B*K candidates.
   * dedupe / EOS / keep beam_width walk (:562-600) and final >= 5-word filter +
     selection (:619-667): host logic over the kernel's order, as in the reference.
+Under torchrun over several ranks the agents are sharded (parallel.method_shard): each
+rank holds its agents' prefix K/V and beam streams (plus the reference prompt's), scores
+its agents, and the candidates' min welfare is an all-reduce(MIN) before the same stable
+order on every rank; rank 0's proposals are used everywhere.
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ from typing import List, Optional, Tuple
 
 import torch
 
-from .. import ops, runtime
+from .. import ops, parallel, runtime
 from ..engine import BeamState
 from .base import BaseGenerator
 from .prompts import BEAM, opinions_text
@@ -100,19 +104,22 @@ class BeamSearchGenerator(BaseGenerator):
         if A == 0:
             return ""
         engine, tok = runtime.get_engine(self.model_identifier)
+        shard = parallel.method_shard(A, self.config)
+        ops_all = list(agent_opinions.values())
         agent_prefixes = [tok.chat_prefix(BEAM["agent_system"],
-                                          BEAM["agent_user"].format(issue=issue, opinion=op))
-                          for op in agent_opinions.values()]
+                                          BEAM["agent_user"].format(issue=issue, opinion=ops_all[a]))
+                          for a in shard.local]
+        A_loc = len(agent_prefixes)      # this rank's agents (all of them on one rank)
         ref_user = BEAM["ref_user"].format(issue=issue, opinions_text=opinions_text(agent_opinions))
         ref_prefix = tok.render_raw(f"{BEAM['ref_system']}\n\n{ref_user}")
         cache = engine.prefill(agent_prefixes + [ref_prefix])
-        st = BeamState(engine, cache, n_prefix=A + 1)
+        st = BeamState(engine, cache, n_prefix=A_loc + 1)
         bias = (runtime.bias_token_ids(tok, self.bias_against_tokens)
                 if self.use_token_biasing and self.bias_against_tokens else [])
         dev = engine.device
 
-        beams: List[Tuple[str, List[float]]] = [("", [0.0] * A)]
-        rewards = torch.zeros(A, 1, dtype=torch.float32, device=dev)   # cumulative, per beam
+        beams: List[Tuple[str, List[float]]] = [("", [0.0] * A_loc)]
+        rewards = torch.zeros(A_loc, 1, dtype=torch.float32, device=dev)   # cumulative, per beam
         completed: List[Tuple[str, List[float]]] = []
         self.step_log = []
         for step in range(self.max_tokens):
@@ -120,7 +127,8 @@ class BeamSearchGenerator(BaseGenerator):
                 break
             step_base_seed = (self.seed + step * self.max_sampling_attempts * len(beams) * (A + 1)
                               if self.seed is not None else None)
-            props = self._propose(st, A, bias, step_base_seed, tok)
+            props = parallel.same_on_all_ranks(self._propose(st, A_loc, bias, step_base_seed, tok),
+                                               shard)
             cb, ct = [], []                           # candidate (beam, token id), insertion order
             for b, toks in enumerate(props):
                 for v in toks:
@@ -141,13 +149,26 @@ class BeamSearchGenerator(BaseGenerator):
             # agent rows -> lp at every candidate, U = R + lp, min over agents, stable
             # order over the B*K slots (padded slots are NaN: ranked after every real one,
             # so the order of the real candidates is the reference's stable sort)
-            Up, Wp, order, _ = ops.beam_step(st.agent_logits(A), tgt.to(dev), rewards, "min",
-                                             softcap=st.e.softcap, workspace=st.e.beam_ws)
             slot_t = torch.as_tensor(slots, dtype=torch.long, device=dev)
-            U = Up[:, slot_t].contiguous()                                    # [A, n_cand]
-            W = Wp[slot_t]
-            cand_of = {s: i for i, s in enumerate(slots)}
-            order = [cand_of[c] for c in order.cpu().tolist() if c in cand_of]
+            if shard.world == 1:
+                Up, Wp, order, _ = ops.beam_step(st.agent_logits(A), tgt.to(dev), rewards, "min",
+                                                 softcap=st.e.softcap, workspace=st.e.beam_ws)
+                U = Up[:, slot_t].contiguous()                                # [A, n_cand]
+                W = Wp[slot_t]
+                cand_of = {s: i for i, s in enumerate(slots)}
+                order = [cand_of[c] for c in order.cpu().tolist() if c in cand_of]
+            else:
+                # this rank's agents (no order in the launch), min over ALL agents by an
+                # all-reduce, then the same stable order on every rank
+                if A_loc:
+                    Up, _, _, _ = ops.beam_step(st.agent_logits(A_loc), tgt.to(dev), rewards, "min",
+                                                n_order=0, softcap=st.e.softcap,
+                                                workspace=st.e.beam_ws)
+                    U = Up[:, slot_t].contiguous()                            # [A_loc, n_cand]
+                else:
+                    U = torch.empty(0, len(slots), dtype=torch.float32, device=dev)
+                W = parallel.combine_welfare(U, "min", shard)
+                order = ops.topk(W, len(slots))[0].cpu().tolist()
             Uh = U.double().cpu().numpy()
             new_beams, new_idx, seen = [], [], set()
             for i in order:
@@ -175,8 +196,9 @@ class BeamSearchGenerator(BaseGenerator):
         if not completed:
             return ""
         pool = [(s, r) for s, r in completed if len(s.strip().split()) >= 5] or completed
-        Uf = torch.tensor([r for _, r in pool], dtype=torch.float32, device=dev).t().contiguous()
-        Wf = ops.welfare(Uf, "min")
+        Uf = torch.tensor([r for _, r in pool], dtype=torch.float32,
+                          device=dev).reshape(len(pool), A_loc).t().contiguous()
+        Wf = parallel.combine_welfare(Uf, "min", shard)
         best, _ = ops.topk(Wf, 1)
         final = pool[int(best.item())][0].strip()
         self.pre_brushup_statement = final

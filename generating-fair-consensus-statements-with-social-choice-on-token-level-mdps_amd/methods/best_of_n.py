@@ -10,15 +10,18 @@ Reference flow (best_of_n.py:53-207), same config keys and outputs:
      per-agent prefix K/V, LM head, cs_logsoftmax_gather, cs_segment_reduce.
   3. nan_to_num(nan -> -10, +inf -> 20, -inf -> -20), min over agents (:384-408)
      -> cs_welfare_reduce(MIN, REPLACE);  np.argmax (:198) -> cs_segmented_topk(k=1).
+Under torchrun (one process per GPU, default process group over several ranks) the agents
+are sharded (parallel.method_shard): each rank scores its agents x all candidates and the
+welfare is combined with an all-reduce(MIN); every rank returns the same statement.
 """
 from __future__ import annotations
 
 import logging
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 import torch
 
-from .. import ops, runtime, utils
+from .. import ops, parallel, runtime, utils
 from .base import BaseGenerator
 from .prompts import BON, opinions_text
 
@@ -68,29 +71,42 @@ class BestOfNGenerator(BaseGenerator):
         seeds = [seed + i if seed is not None else None for i in range(n)]
         outs = runtime.generate(engine, tok, ref_ids, seeds, max_tokens, float(temperature))
         cands = [c for c in (clean_generated_text(tok.decode(o)) for o in outs) if c]
+        shard = parallel.method_shard(len(agent_opinions), cfg)
+        cands = parallel.same_on_all_ranks(cands, shard)   # seed=None draws differ per rank
         self.last_candidates = cands
         if not cands:
             logger.error("No valid candidate statements were generated.")
             return "[ERROR: Failed to generate any candidates]"
 
-        U = self.score_candidates(issue, agent_opinions, cands)          # [A, N] device
-        W = ops.welfare(U, "min", nonfinite="replace", nan_val=self.DEFAULT_REWARD,
-                        posinf_val=self.REWARD_CLIP_MAX, neginf_val=self.REWARD_CLIP_MIN)
+        U = self.score_candidates(issue, agent_opinions, cands, shard)   # [A_local, N] device
+        W = parallel.combine_welfare(U, "min", shard, nonfinite="replace",
+                                     nan_val=self.DEFAULT_REWARD, posinf_val=self.REWARD_CLIP_MAX,
+                                     neginf_val=self.REWARD_CLIP_MIN)
         best, _ = ops.topk(W, 1)
         b = int(best.item())
         self.last_welfare = W.double().cpu().tolist()
         logger.info("Selected best candidate index: %d (Score: %.4f)", b, self.last_welfare[b])
         return cands[b]
 
-    def score_candidates(self, issue: str, agent_opinions: dict, cands: List[str]) -> torch.Tensor:
-        """Mean log-prob utility U[a, c] of every candidate under every agent (device, fp32)."""
+    def score_candidates(self, issue: str, agent_opinions: dict, cands: List[str],
+                         shard: Optional[parallel.AgentShard] = None) -> torch.Tensor:
+        """Mean log-prob utility U[a, c] of every candidate under every agent of this
+        rank's shard (all agents on one rank; device, fp32, rows in agent order)."""
         engine, tok = runtime.get_engine(self.model_identifier)
+        shard = shard or parallel.AgentShard(len(agent_opinions))
+        ops_all = list(agent_opinions.values())
+        mine = [ops_all[a] for a in shard.local]
+        C = len(cands)
+        if not mine:   # more ranks than agents: nothing to score here
+            U = torch.empty(0, C, dtype=torch.float32, device=engine.device)
+            self._record_rewards(agent_opinions, U, shard)
+            return U
         prefixes = []
-        for op in agent_opinions.values():
+        for op in mine:
             system = BON["agent_system"] + "\n\n" + BON["agent_user"].format(issue=issue, opinion=op)
             prefixes.append(tok.chat_prefix(system, ""))
         cache = engine.prefill(prefixes)
-        A, C = len(prefixes), len(cands)
+        A = len(prefixes)
         cand_ids = [tok.encode(c) for c in cands]
         owner = [a for a in range(A) for _ in range(C)]
         conts = [cand_ids[c] for _ in range(A) for c in range(C)]
@@ -100,12 +116,18 @@ class BestOfNGenerator(BaseGenerator):
         U = torch.where(cnt > 0, seg["sum_lp"] / cnt.clamp(min=1.0),
                         torch.full_like(cnt, self.DEFAULT_REWARD)).view(A, C)
         # candidates the reference's find() would locate inside the prompt: text-compat path
-        for a, op in enumerate(agent_opinions.values()):
+        for a, op in enumerate(mine):
             system = BON["agent_system"] + "\n\n" + BON["agent_user"].format(issue=issue, opinion=op)
             for c, cand in enumerate(cands):
                 if not utils.span_found_at_user(tok, system, cand):
                     m_lp, _, n_ok = utils.text_compat_mean(self.model_identifier, system, cand)
                     U[a, c] = m_lp if n_ok else self.DEFAULT_REWARD
-        self.last_agent_rewards = {aid: U[i].double().cpu().tolist()
+        U = U.contiguous()
+        self._record_rewards(agent_opinions, U, shard)
+        return U
+
+    def _record_rewards(self, agent_opinions: dict, U: torch.Tensor, shard) -> None:
+        """last_agent_rewards for every agent (gathered from the ranks when sharded)."""
+        allU = parallel.gather_agents(U, shard)
+        self.last_agent_rewards = {aid: allU[i].double().cpu().tolist()
                                    for i, aid in enumerate(agent_opinions)}
-        return U.contiguous()

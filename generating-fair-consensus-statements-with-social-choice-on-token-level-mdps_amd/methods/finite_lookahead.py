@@ -18,6 +18,10 @@ Per committed token (finite_lookahead.py:99-153):
      b + ... + b^d rows per agent instead of d * b^d.
   3. Commit the best path's first token; stop on "DONE" / newline tokens (:141-144).
 
+Under torchrun over several ranks the agents are sharded (parallel.method_shard): each
+rank scores its agents' rows of the tree, the welfare is an all-reduce(MIN), and rank 0's
+lookahead paths are used everywhere.
+
 Reference quirk kept: a one-token draw that hits an end-of-sequence token returns
 "" (generate_text drops stop tokens), so a path element can be empty; the reward
 then still averages the last len(path) log-probs of the user span, reaching back
@@ -30,7 +34,7 @@ from typing import List, Optional, Tuple
 
 import torch
 
-from .. import ops, runtime
+from .. import ops, parallel, runtime
 from .base import BaseGenerator
 from .prompts import FL, opinions_text
 
@@ -118,14 +122,20 @@ class FiniteLookaheadGenerator(BaseGenerator):
 
     # --- scoring ------------------------------------------------------------------
     def path_rewards(self, issue: str, agent_opinions: dict, current: str,
-                     paths: List[Tuple[List[str], List[int]]]) -> torch.Tensor:
-        """U[a, p] = mean of the last len(path) user-span log-probs (device fp32)."""
+                     paths: List[Tuple[List[str], List[int]]],
+                     shard: Optional[parallel.AgentShard] = None) -> torch.Tensor:
+        """U[a, p] = mean of the last len(path) user-span log-probs (device fp32), for the
+        agents of this rank's shard (every agent on one rank), rows in agent order."""
         engine, tok = runtime.get_engine(self.model_identifier)
+        shard = shard or parallel.AgentShard(len(agent_opinions))
+        ops_all = list(agent_opinions.values())
         prefixes = [tok.chat_prefix(FL["agent_system"],
-                                    FL["agent_user"].format(issue=issue, opinion=op) + current)
-                    for op in agent_opinions.values()]
-        cache = engine.prefill(prefixes)
+                                    FL["agent_user"].format(issue=issue, opinion=ops_all[a]) + current)
+                    for a in shard.local]
         A, R = len(prefixes), len(paths)
+        if A == 0:   # more ranks than agents
+            return torch.empty(0, R, dtype=torch.float32, device=engine.device)
+        cache = engine.prefill(prefixes)
         # the paths form a token tree: every node is scored once per agent (shared
         # prefixes of the lookahead paths are not re-scored), then each path's log-probs
         # are its nodes'
@@ -174,18 +184,20 @@ class FiniteLookaheadGenerator(BaseGenerator):
         seed = cfg.get("seed")
         current, count = "", 0
         self.trace = []
+        shard = parallel.method_shard(len(agent_opinions), cfg)
         while count < max_tokens:
             paths = self.tree_paths(issue, agent_opinions, current, bf, depth, seed)
+            paths = parallel.same_on_all_ranks(paths, shard)   # seed=None draws differ per rank
             if not paths:
                 logger.warning("No valid tree paths generated. Ending generation.")
                 break
-            U = self.path_rewards(issue, agent_opinions, current, paths)
-            W = ops.welfare(U, "min")
+            U = self.path_rewards(issue, agent_opinions, current, paths, shard)
+            W = parallel.combine_welfare(U, "min", shard)
             best, _ = ops.topk(W, 1)
             b = int(best.item())
             nxt = paths[b][0][0]
             self.trace.append({"paths": [p[0] for p in paths], "best": b,
-                               "rewards": U[:, b].double().cpu().tolist()})
+                               "rewards": parallel.gather_agents(U, shard)[:, b].double().cpu().tolist()})
             if nxt.strip() in ["DONE"]:
                 break
             if nxt in FL["stop_tokens"]:

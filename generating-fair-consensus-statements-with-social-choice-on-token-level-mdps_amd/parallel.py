@@ -52,6 +52,46 @@ class AgentShard:
         return pos
 
 
+def method_shard(n_agents: int, config: Optional[dict] = None) -> AgentShard:
+    """The agent shard of this process for one generate_statement call.
+
+    Launched one process per GPU (torchrun) with the default process group initialized
+    over more than one rank, the methods split the agents round-robin over the ranks:
+    each rank prefills and scores only its agents (their prefix K/V live on its GPU) and
+    the per-candidate welfare is combined with combine_welfare; every rank reaches the
+    same statement.  config ``shard_agents: false`` keeps every agent on every rank."""
+    cfg = config or {}
+    if (cfg.get("shard_agents", True) and dist.is_available() and dist.is_initialized()
+            and dist.get_world_size() > 1):
+        return AgentShard(n_agents, dist.get_rank(), dist.get_world_size())
+    return AgentShard(n_agents, 0, 1)
+
+
+def same_on_all_ranks(obj, shard: AgentShard, group: Optional[dist.ProcessGroup] = None):
+    """Rank 0's value of ``obj`` on every rank (candidate sets drawn with seed=None, or any
+    host decision that must not diverge between ranks); identity on one rank."""
+    if shard.world == 1:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=0, group=group)
+    return box[0]
+
+
+def gather_agents(U_local: torch.Tensor, shard: AgentShard,
+                  group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Every agent's rows [A, C] in agent order on every rank, from each rank's
+    [A_local, C] (all_gather of rank-major padded blocks, then the global order)."""
+    if shard.world == 1:
+        return U_local
+    C = U_local.shape[1]
+    m = shard.max_local()
+    pad = torch.full((m, C), float("nan"), dtype=U_local.dtype, device=U_local.device)
+    pad[:U_local.shape[0]] = U_local
+    bufs = [torch.empty_like(pad) for _ in range(shard.world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat(bufs, 0)[torch.as_tensor(shard.global_order(), device=U_local.device)]
+
+
 def combine_welfare(U_local: torch.Tensor, kind: str, shard: AgentShard,
                     group: Optional[dist.ProcessGroup] = None, eps: float = 1e-9,
                     nonfinite: str = "skip", nan_val: float = -10.0, posinf_val: float = 20.0,
@@ -77,12 +117,7 @@ def combine_welfare(U_local: torch.Tensor, kind: str, shard: AgentShard,
         return torch.where(torch.isinf(W) & (W > 0 if kind == "min" else W < 0),
                            torch.full_like(W, float("nan")), W)
     # sum / sumlog: gather every agent's utilities, fold in global agent order
-    m = shard.max_local()
-    pad = torch.full((m, C), float("nan"), dtype=torch.float32, device=U_local.device)
-    pad[:U_local.shape[0]] = U_local
-    bufs = [torch.empty_like(pad) for _ in range(shard.world)]
-    dist.all_gather(bufs, pad, group=group)
-    allU = torch.cat(bufs, 0)[torch.as_tensor(shard.global_order(), device=U_local.device)]
+    allU = gather_agents(U_local.to(torch.float32), shard, group)
     return ops.welfare(allU.contiguous(), kind, **kw)
 
 

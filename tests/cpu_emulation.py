@@ -13,7 +13,7 @@ import oracle as orc
 
 PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
 NAMES = ("logsoftmax_gather", "segment_reduce", "welfare", "topk", "vocab_sample", "vocab_topk",
-         "beam_step", "beam_decode_step")
+         "beam_step", "beam_decode_step", "beam_select")
 
 
 def _lsg(logits, targets, *, vocab=None, softcap=0.0, workspace=None, want_lse=False, **kw):
@@ -90,7 +90,21 @@ def _bd(ref_logits, logits, rewards, k, kind="min", *, n_order=None, vocab=None,
     return ids, U, W, order, val
 
 
-_IMPL = {"logsoftmax_gather": _lsg, "segment_reduce": _seg, "welfare": _wel, "topk": _tk,
+def _sel(W, n_order, *, U=None, unfill=None, kept_out=None, W_out=None, with_values=False):
+    fill = {None: None, "none": None, "+inf": np.inf, "min": np.inf, "-inf": -np.inf,
+            "max": -np.inf}[unfill]
+    Wn = W.clone()
+    if fill is not None:
+        Wn[Wn == fill] = float("nan")
+    if W_out is not None:
+        W_out.copy_(Wn)
+    order, val = _tk(Wn, n_order)
+    if kept_out is not None and U is not None:
+        kept_out.copy_(U[:, order.long()])
+    return order.to(torch.int32), (val if with_values else None)
+
+
+_IMPL = {"beam_select": _sel, "logsoftmax_gather": _lsg, "segment_reduce": _seg, "welfare": _wel, "topk": _tk,
          "vocab_sample": _vs, "vocab_topk": _vt, "beam_step": _bs, "beam_decode_step": _bd}
 
 
