@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, gpu=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), here, os.path.join(os.path.dirname(here), "oracle")):
@@ -32,12 +32,15 @@ def _worker(rank, world, port, q):
     import cpu_emulation
     import method_parity as mpar
     torch.set_num_threads(2)
-    cpu_emulation.install()
+    if gpu:   # the real HIP library on the box's one GPU, every rank on cuda:0
+        torch.cuda.set_device(0)
+    else:
+        cpu_emulation.install()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     traces = mpar.load_traces("method_traces.json")
     traces = dict(traces, runs=[r for r in traces["runs"] if r["method"] in METHODS])
-    mpar.register_fixture_engine(traces, torch.device("cpu"))
+    mpar.register_fixture_engine(traces, torch.device("cuda:0" if gpu else "cpu"))
     import importlib
     par = importlib.import_module(cpu_emulation.PKG + ".parallel")
     A = len(traces["agent_opinions"])
@@ -50,12 +53,11 @@ def _worker(rank, world, port, q):
     q.put((rank, failures, stmts, len(traces["runs"])))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_methods_replay_reference_traces(world):
+def _run(world, gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, gpu)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -69,3 +71,15 @@ def test_sharded_methods_replay_reference_traces(world):
         assert n_runs > 0
         assert not failures, f"rank {rank}:\n" + "\n".join(failures)
         assert stmts == res[0][1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_methods_replay_reference_traces(world):
+    _run(world, gpu=False)
+
+
+@pytest.mark.gpu
+def test_sharded_methods_on_gpu_gloo_rehearsal():
+    """The same replay through the real HIP library: 2 ranks on the one GPU of the box,
+    gloo collectives on device tensors (RCCL needs one GPU per rank)."""
+    _run(2, gpu=True)
