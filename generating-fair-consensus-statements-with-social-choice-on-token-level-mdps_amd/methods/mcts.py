@@ -19,6 +19,9 @@ Same class name, config keys, tree policy and seed schedule as the reference
     over agents by cs_welfare_reduce(MIN).
   * UCB1 selection over children in token-string order, backpropagation from the
     expanded node, most-visited child advances the root (mcts.py:370-468, 884-930).
+Under torchrun over several ranks the agents are sharded (parallel.method_shard): every
+rank runs the same search (one run seed drawn on rank 0 when ``seed`` is None) and scores
+only its agents' prompts; each reward is an all-reduce(MIN) over the ranks.
 
 Reference defect, documented rather than reproduced: mcts.py:615 formats
 ``final_statement`` (commented out at :593) in a debug f-string inside the rollout's
@@ -36,7 +39,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from .. import ops, runtime, utils
+from .. import ops, parallel, runtime, utils
 from .base import BaseGenerator
 from .prompts import MCTS, opinions_text
 
@@ -83,6 +86,7 @@ class MCTSGenerator(BaseGenerator):
         self.brushup = config.get("brushup", False)
         self.strict_nameerror = bool(config.get("reference_rollout_nameerror", False))
         self.trace: List[dict] = []
+        self._shard = parallel.AgentShard(0)
 
     # --- prompts (mcts.py:126-158) -----------------------------------------------------
     def _reference_prompt(self, issue: str, agent_opinions: dict, statement: str) -> str:
@@ -137,17 +141,26 @@ class MCTSGenerator(BaseGenerator):
         """(immediate reward, rollout reward or None): each the min over agents of the
         summed user-span log-probs, FAIL when any agent's call fails (mcts.py:742-782,
         611-651)."""
-        A = len(agent_opinions)
-        systems = self._agent_systems(issue, agent_opinions, parent_statement)
+        shard = self._shard
+        local = shard.local
+        A = len(local)                    # this rank's agents (all of them on one rank)
+        cols = 2 if rollout else 1
+        par_sys = self._agent_systems(issue, agent_opinions, parent_statement)
+        systems = [par_sys[a] for a in local]
         users = [token] * A
         if rollout:
-            systems += self._agent_systems(issue, agent_opinions, child_statement)
+            child_sys = self._agent_systems(issue, agent_opinions, child_statement)
+            systems += [child_sys[a] for a in local]
             users += [rollout] * A
-        sums = utils.user_span_sums(self.model_identifier, systems, users, device_out=True)
-        cols = 2 if rollout else 1
-        U = sums.view(cols, A).t().to(torch.float32).contiguous()       # [A, cols]
-        W = ops.welfare(U, "min").double().cpu().tolist()
-        bad = torch.isnan(sums).view(cols, A).any(dim=1).cpu().tolist()
+        engine, _ = runtime.get_engine(self.model_identifier)
+        if A:
+            sums = utils.user_span_sums(self.model_identifier, systems, users, device_out=True)
+            sums = sums.to(engine.device)
+        else:
+            sums = torch.empty(0, dtype=torch.float64, device=engine.device)
+        U = sums.view(cols, A).t().to(torch.float32).contiguous()       # [A_local, cols]
+        W = parallel.combine_welfare(U, "min", shard).double().cpu().tolist()
+        bad = parallel.any_rank(torch.isnan(sums).view(cols, A).any(dim=1), shard).cpu().tolist()
         imm = self.FAIL if bad[0] else W[0]
         roll = None
         if rollout:
@@ -243,6 +256,17 @@ class MCTSGenerator(BaseGenerator):
         if A == 0:
             logger.warning("No agent opinions provided.")
             return ""
+        self._shard = parallel.method_shard(A, self.config)
+        seed_cfg = self.seed
+        if self._shard.world > 1 and self.seed is None:   # one search on every rank
+            self.seed = parallel.same_on_all_ranks(random.randint(0, 2 ** 30), self._shard)
+        try:
+            return self._search(issue, agent_opinions)
+        finally:
+            self.seed = seed_cfg
+
+    def _search(self, issue: str, agent_opinions: dict) -> str:
+        A = len(agent_opinions)
         root = Node(statement="")
         current = ""
         for step in range(self.max_tokens):

@@ -77,6 +77,16 @@ def same_on_all_ranks(obj, shard: AgentShard, group: Optional[dist.ProcessGroup]
     return box[0]
 
 
+def any_rank(flags: torch.Tensor, shard: AgentShard,
+             group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Element-wise OR of a bool tensor over the ranks (all_reduce MAX); identity on one rank."""
+    if shard.world == 1:
+        return flags
+    t = flags.to(torch.float32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t > 0
+
+
 def gather_agents(U_local: torch.Tensor, shard: AgentShard,
                   group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """Every agent's rows [A, C] in agent order on every rank, from each rank's

@@ -1,5 +1,5 @@
-"""Agent-sharded methods on CPU (gloo, 2 and 3 ranks): beam search, Best-of-N and finite
-lookahead split the agents over the ranks (parallel.method_shard), combine the welfare
+"""Agent-sharded methods on CPU (gloo, 2 and 3 ranks): beam search, Best-of-N, finite
+lookahead and MCTS split the agents over the ranks (parallel.method_shard), combine the welfare
 across them, and must still replay the reference's own traces — the same statements,
 BoN candidates, rewards and welfare as one process — on every rank.  The kernels are
 emulated by the oracle (tests/cpu_emulation.py); the collectives are real
@@ -10,7 +10,7 @@ import socket
 import pytest
 import torch.multiprocessing as mp
 
-METHODS = ("beam_search", "best_of_n", "finite_lookahead")
+METHODS = ("beam_search", "best_of_n", "finite_lookahead", "mcts")
 
 
 def _free_port():
