@@ -227,7 +227,7 @@ def gpu_busy(stream, ms=20.0):
                 a = a @ a.T * 1e-3
 
 
-def run_beam(name, world, rank, dev, steps, warmup, comm=None):
+def run_beam(name, world, rank, dev, steps, warmup, comm=None, pmc_json=None):
     """Beam-search decode steps on resident logits (BASELINE C1 / C3 / C5).
 
     One decode step, per rank:
@@ -393,6 +393,8 @@ def run_beam(name, world, rank, dev, steps, warmup, comm=None):
                                     "vocab stream + gather + welfare" +
                                     ("" if sharded else " + top-B") + ")"),
                          "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
+                         "traffic": (read_traffic(pmc_json, "beam_" + name, A_loc * B + B, V)
+                                     if pmc_json else None),
                          "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "collective": {"op": ("all_reduce(MIN) of W" + (" (direct RCCL communicator)" if comm
@@ -537,7 +539,7 @@ def main():
             print(f"bench: direct RCCL communicator unavailable ({e}); using the ProcessGroup",
                   file=sys.stderr, flush=True)
     for name in beams:
-        beam[name] = run_beam(name, world, rank, dev, args.beam_steps, 20, comm)
+        beam[name] = run_beam(name, world, rank, dev, args.beam_steps, 20, comm, args.pmc_json)
     if comm is not None:
         comm.close()
     if rank == 0:

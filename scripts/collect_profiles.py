@@ -56,6 +56,11 @@ traffic = {"c2": {
     "source": f"profiles/{prefix}_pmc_fetch_lsg.csv, profiles/{prefix}_pmc_write_lsg.csv "
               "(rocprofv3 --pmc, separate passes)",
     "kernel_config": "lsg_stream_kernel<bf16, 1024 threads, 2 x 16 B in flight, nt>"}}
+try:   # keep the other entries (beam_*: scripts/collect_pmc_beam.py)
+    with open(os.path.join(PROF, "pmc_traffic.json")) as f:
+        traffic = {**json.load(f), **traffic}
+except (OSError, ValueError):
+    pass
 with open(os.path.join(PROF, "pmc_traffic.json"), "w") as f:
     json.dump(traffic, f, indent=1)
 print(json.dumps({"tests": tests[-1] if tests else None, "value": line["value"],
