@@ -575,3 +575,58 @@ def test_fused_beam_launches_stress_shared_workspace(ops, dev):
         assert torch.equal(ids, ids2), it
         assert torch.equal(U, U2) and torch.equal(W, W2), it
         assert torch.equal(o[:o2.numel()], o2), it
+
+
+def _fuzz_cases(n=24, seed=2024):
+    rng = np.random.default_rng(seed)
+    cases = []
+    for i in range(n):
+        dtype = [torch.float32, torch.bfloat16, torch.float16][rng.integers(0, 3)]
+        A = int(rng.integers(1, 40))
+        B = int(rng.integers(1, 20))
+        vocab = int(rng.choice([97, 1000, 4099, 33333, 70001, 128256]))
+        K = int(min(rng.integers(1, 65), vocab, 16384 // B))
+        softcap = float(rng.choice([0.0, 0.0, 30.0, 50.0])) if dtype != torch.float16 else 0.0
+        kind = ["min", "min", "max", "sum", "sumlog"][rng.integers(0, 5)]
+        pattern = ["randn", "ties", "masked"][rng.integers(0, 3)]
+        cases.append((i, dtype, A, B, K, vocab, softcap, kind, pattern))
+    return cases
+
+
+@pytest.mark.parametrize("i,dtype,A,B,K,vocab,softcap,kind,pattern", _fuzz_cases())
+def test_beam_decode_fuzz(ops, orc, dev, i, dtype, A, B, K, vocab, softcap, kind, pattern):
+    """Seeded random shapes (dtype, agents, beams, K, vocab, soft-cap, welfare kind, tie /
+    mask patterns): the fused decode step equals cs_vocab_topk + cs_beam_step bit for bit,
+    its proposer equals the oracle's top-K, and its partial order + kept rewards equal the
+    full order's prefix."""
+    if A * B > 65536:
+        pytest.skip("shape outside the launch limits")
+    g = torch.Generator().manual_seed(1000 + i)
+    ref = torch.randn(B, vocab, generator=g) * 3.0
+    x = torch.randn(A * B, vocab, generator=g) * 3.0
+    if pattern == "ties":
+        ref = torch.round(ref)
+        x = torch.round(x * 2) / 2
+    elif pattern == "masked":
+        m = torch.rand(B, vocab, generator=g) < 0.5
+        ref[m] = float("-inf")
+    ref, x = ref.to(dtype).to(dev), x.to(dtype).to(dev)
+    R = (-torch.rand(A, B, generator=g) * 20.0).to(dev)
+    ids, _ = ops.vocab_topk(ref, K, softcap=softcap)
+    o_ids, _ = orc.vocab_topk(ref.double().cpu().numpy() if softcap == 0.0 else
+                              (softcap * torch.tanh(ref.double().cpu() / softcap)).numpy(), K)
+    U, W, o, _ = ops.beam_step(x, ids, R, kind, softcap=softcap)
+    ids2, U2, W2, o2, _ = ops.beam_decode_step(ref, x, R, K, kind, softcap=softcap)
+    assert torch.equal(ids, ids2)
+    if softcap == 0.0:   # (soft-capped ties can merge differently in fp64 -> checked via ids)
+        assert np.array_equal(ids.cpu().numpy(), o_ids)
+    assert torch.equal(torch.nan_to_num(U, nan=7.0), torch.nan_to_num(U2, nan=7.0))
+    assert torch.equal(torch.nan_to_num(W, nan=7.0), torch.nan_to_num(W2, nan=7.0))
+    assert torch.equal(o, o2)
+    n = min(B, B * K)
+    kept = torch.empty(A, n, device=dev) if B * K <= 1024 else None
+    _, _, _, on, _ = ops.beam_decode_step(ref, x, R, K, kind, n_order=n, softcap=softcap,
+                                          kept_out=kept)
+    assert torch.equal(on, o[:n])
+    if kept is not None:
+        assert torch.equal(kept, U[:, on.long()])
