@@ -44,7 +44,21 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("dtype,rows,vocab,ld_pad,k,softcap", CASES)
+def _lsg_fuzz(n=30, seed=77):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        dtype = [torch.float32, torch.bfloat16, torch.float16][rng.integers(0, 3)]
+        rows = int(rng.choice([1, 2, 5, 31, 255, 256, 257, 1023, 2048, 3001]))
+        vocab = int(rng.choice([1, 2, 9, 64, 1000, 4097, 32000, 128256, 256000]))
+        if rows * vocab > 40_000_000:
+            rows = max(1, 40_000_000 // vocab)
+        out.append((dtype, rows, vocab, int(rng.integers(0, 9)), int(rng.integers(0, 9)),
+                    float(rng.choice([0.0, 0.0, 30.0, 50.0])) if dtype != torch.float16 else 0.0))
+    return out
+
+
+@pytest.mark.parametrize("dtype,rows,vocab,ld_pad,k,softcap", CASES + _lsg_fuzz())
 def test_logsoftmax_gather_matches_oracle(ops, orc, dev, dtype, rows, vocab, ld_pad, k, softcap):
     g = torch.Generator().manual_seed(rows * 7 + vocab)
     full = (torch.randn(rows, vocab + ld_pad, generator=g) * 3.0).to(dtype)
@@ -55,7 +69,8 @@ def test_logsoftmax_gather_matches_oracle(ops, orc, dev, dtype, rows, vocab, ld_
     host, bf16 = _host_logits(full)
     o_tok, o_lse = orc.logsoftmax_gather(np.ascontiguousarray(host), tgt.numpy(), softcap=softcap,
                                          bf16=bf16, vocab=vocab)
-    assert np.max(np.abs(tok.cpu().numpy() - o_tok)) < LP_TOL
+    if k:
+        assert np.max(np.abs(tok.cpu().numpy() - o_tok)) < LP_TOL
     assert np.max(np.abs(lse.cpu().numpy() - o_lse)) < LP_TOL
     del logits
 
