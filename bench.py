@@ -186,7 +186,8 @@ def end_to_end(A, N, T, V, wkind, dev, steps=2, prefix_len=200, seed=0):
     model = M.Model(cfg, dev, torch.bfloat16, seed=seed)
     torch.cuda.synchronize()
     init_s = time.perf_counter() - t0
-    eng = E.ScoringEngine(model, max_rows_per_chunk=16384)
+    # every pass re-encodes the prefixes in full (no reuse of the previous pass's K/V)
+    eng = E.ScoringEngine(model, max_rows_per_chunk=16384, reuse_caches=0)
     g = torch.Generator().manual_seed(11)
     prefixes = [torch.randint(300, V, (prefix_len,), generator=g).tolist() for _ in range(A)]
     cands = [torch.randint(300, V, (T,), generator=g).tolist() for _ in range(N)]

@@ -19,9 +19,11 @@ Everything after the LM head runs in the HIP kernels (ops.*).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import ops
@@ -51,11 +53,31 @@ def _pad(seqs: Sequence[Sequence[int]], device, fill: int = 0):
     return out.to(device, non_blocking=True), lens.to(device, non_blocking=True)
 
 
+def _lcp(a: np.ndarray, b: np.ndarray) -> int:
+    """Length of the common leading run of two token-id arrays."""
+    n = min(a.shape[0], b.shape[0])
+    if n == 0:
+        return 0
+    d = np.flatnonzero(a[:n] != b[:n])
+    return int(d[0]) if d.size else n
+
+
 class ScoringEngine:
-    """Owns a model on one device and scores continuations under many prefixes."""
+    """Owns a model on one device and scores continuations under many prefixes.
+
+    Prefix reuse: the reference re-encodes every prompt from scratch on every call
+    (src/utils.py:249-259).  Consecutive calls of one method mostly share their prompts'
+    leading tokens (MCTS: every simulation's 2A scoring prompts and the reference
+    prompt differ from the previous call's only in the statement's last tokens;
+    finite lookahead: one step's agent prompts extend the previous step's), so
+    ``prefill`` keeps its last ``reuse_caches`` results and runs only each new prefix's
+    tokens past its longest common token prefix with a stored row through the model
+    (K/V of a causal prefix depend on that prefix alone).  ``reuse_caches = 0`` (or env
+    CS_PREFIX_REUSE=0) prefills every prompt in full."""
 
     def __init__(self, model: Model, max_rows_per_chunk: int = 32768,
-                 max_streams_per_chunk: int = 1024):
+                 max_streams_per_chunk: int = 1024, reuse_caches: Optional[int] = None,
+                 reuse_min_tokens: int = 16):
         self.model = model
         self.device = model.device
         self.softcap = model.cfg.final_softcap
@@ -63,19 +85,107 @@ class ScoringEngine:
         self.max_streams = max_streams_per_chunk
         self.ws = ops.Workspace()
         self.beam_ws = ops.Workspace(zeroed=True)   # cs_beam_step (arrival counters)
+        if reuse_caches is None:
+            reuse_caches = 0 if os.environ.get("CS_PREFIX_REUSE", "1") == "0" else 4
+        self.reuse_caches = int(reuse_caches)
+        self.reuse_min_tokens = max(1, int(reuse_min_tokens))
+        self._store: List[tuple] = []     # (PrefixCache, [np.int64 ids per row]), newest last
+        self.reuse_stats = {"prefills": 0, "reused": 0, "tokens": 0, "tokens_run": 0}
 
     # --- prefixes ---------------------------------------------------------------
     @torch.no_grad()
     def prefill(self, prefixes: Sequence[Sequence[int]]) -> PrefixCache:
         if any(len(p) == 0 for p in prefixes):
             raise ValueError("every prefix needs at least one token (BOS)")
-        ids, lens = _pad(prefixes, self.device)
-        kv, h, valid = self.model.prefill(ids, lens)
-        last = h[torch.arange(h.shape[0], device=self.device), lens - 1]
+        rows = [np.asarray(list(p), dtype=np.int64) for p in prefixes]
+        total = sum(r.shape[0] for r in rows)
+        self.reuse_stats["prefills"] += 1
+        self.reuse_stats["tokens"] += total
+        plan = self._reuse_plan(rows) if self.reuse_caches > 0 else None
+        if plan is not None:
+            cache = self._prefill_extending(prefixes, rows, *plan)
+            self.reuse_stats["reused"] += 1
+        else:
+            self.reuse_stats["tokens_run"] += len(rows) * max(r.shape[0] for r in rows)
+            ids, lens = _pad(prefixes, self.device)
+            kv, h, valid = self.model.prefill(ids, lens)
+            last = h[torch.arange(h.shape[0], device=self.device), lens - 1]
+            P = ids.shape[1]
+            pos = torch.arange(P, device=self.device)[None].expand(ids.shape[0], P)
+            cache = PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid,
+                                hidden=h, ids=ids)
+        if self.reuse_caches > 0:
+            self._store.append((cache, rows))
+            del self._store[:-self.reuse_caches]
+        return cache
+
+    def reset_prefix_store(self) -> None:
+        self._store = []
+
+    def _reuse_plan(self, rows):
+        """(stored cache, source row per prefix, reused length per prefix) from the stored
+        cache that saves the most padded work, or None when a full prefill is as cheap."""
+        best = None
+        full_cost = len(rows) * max(r.shape[0] for r in rows)
+        for cache, srows in self._store:
+            src, lcp = [], []
+            for r in rows:
+                bi, bl = 0, 0
+                for j, s in enumerate(srows):
+                    l = _lcp(r, s)
+                    if l > bl:
+                        bi, bl = j, l
+                bl = min(bl, r.shape[0] - 1)          # at least one token runs
+                if bl < self.reuse_min_tokens:
+                    bl = 0
+                src.append(bi)
+                lcp.append(bl)
+            cost = len(rows) * max(r.shape[0] - l for r, l in zip(rows, lcp))
+            if best is None or cost < best[0]:
+                best = (cost, cache, src, lcp)
+        if best is None or 2 * best[0] > full_cost:
+            return None
+        self.reuse_stats["tokens_run"] += best[0]
+        return best[1], best[2], best[3]
+
+    def _prefill_extending(self, prefixes, rows, base: PrefixCache, src, lcp) -> PrefixCache:
+        """The PrefixCache ``prefill(prefixes)`` returns, with row r's first lcp[r]
+        positions (K/V, hidden) taken from ``base`` row src[r] and only the rest run
+        through the model (extend over base's K/V, visible up to lcp[r])."""
+        dev = self.device
+        R = len(rows)
+        lens_l = [r.shape[0] for r in rows]
+        S = max(n - l for n, l in zip(lens_l, lcp))
+        suf = torch.zeros(R, S, dtype=torch.long)
+        for i, (r, l) in enumerate(zip(rows, lcp)):
+            suf[i, :r.shape[0] - l] = torch.from_numpy(r[l:])
+        suf = suf.to(dev, non_blocking=True)
+        l_t = torch.as_tensor(lcp, dtype=torch.long).to(dev, non_blocking=True)
+        s_t = torch.as_tensor(src, dtype=torch.long).to(dev, non_blocking=True)
+        Pc = base.ids.shape[1]
+        pos = l_t[:, None] + torch.arange(S, device=dev)[None]
+        cmask = torch.arange(Pc, device=dev)[None] < l_t[:, None]
+        ctx = [(k[s_t], v[s_t]) for k, v in base.kv]
+        h_new, new = self.model.extend(suf, pos, ctx, cmask, base.pos[s_t])
+        # contiguous layout, position j of row r: base row j (j < lcp) or new j - lcp
+        ids, lens = _pad(prefixes, dev)
         P = ids.shape[1]
-        pos = torch.arange(P, device=self.device)[None].expand(ids.shape[0], P)
-        return PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid, hidden=h,
-                           ids=ids)
+        j = torch.arange(P, device=dev)[None]
+        idx = torch.where(j < l_t[:, None], j, Pc + (j - l_t[:, None]).clamp(max=S - 1))
+        idx = idx.clamp(max=Pc + S - 1)
+
+        def merge(old, fresh):                   # [R, H, Pc, D] + [R, H, S, D] -> [R, H, P, D]
+            both = torch.cat([old, fresh], dim=2)
+            g = idx[:, None, :, None].expand(R, both.shape[1], P, both.shape[3])
+            return torch.gather(both, 2, g)
+
+        kv = [(merge(ck, nk), merge(cv, nv)) for (ck, cv), (nk, nv) in zip(ctx, new)]
+        hb = torch.cat([base.hidden[s_t], h_new], dim=1)
+        h = torch.gather(hb, 1, idx[:, :, None].expand(R, P, hb.shape[2]))
+        valid = j < lens[:, None]
+        last = h[torch.arange(R, device=dev), lens - 1]
+        return PrefixCache(kv=kv, lengths=lens, last_hidden=last,
+                           pos=j.expand(R, P), valid=valid, hidden=h, ids=ids)
 
     @torch.no_grad()
     def prefix_tail_logprobs(self, cache: PrefixCache, m: int) -> torch.Tensor:
