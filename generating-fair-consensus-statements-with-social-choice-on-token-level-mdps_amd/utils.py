@@ -57,12 +57,10 @@ def prompt_logprobs_ids(model: str, ids: Sequence[int]) -> List[Optional[float]]
     """log p(ids[i] | ids[:i]) for every position (None for position 0): the echo=True
     prompt log-probs, computed by one forward + cs_logsoftmax_gather."""
     engine, _ = runtime.get_engine(model)
-    m = engine.model
-    dev = engine.device
-    t = torch.as_tensor(list(ids), dtype=torch.long, device=dev)[None]
-    _, h, _ = m.prefill(t, torch.tensor([len(ids)], device=dev))
     if len(ids) < 2:
         return [None] * len(ids)
+    t = torch.as_tensor(list(ids), dtype=torch.long, device=engine.device)[None]
+    h = engine.prefill([list(ids)]).hidden          # reuses a stored common prefix
     rows = h[0, :-1]
     tgt = t[0, 1:].to(torch.int32)[:, None]
     lp = engine.rows_logprobs(rows, tgt).view(-1).double().cpu().tolist()
@@ -172,13 +170,53 @@ def user_span_sums(model, systems: Sequence[Optional[str]], users: Sequence[str]
         if device_out and len(fast) == n:
             return sums
         out[torch.as_tensor(fast)] = sums.cpu()
-    for i in range(n):
-        if i in fast_set or not users[i]:
-            continue
-        _, lps = get_prompt_logprobs(model, systems[i], users[i])
-        if lps and all(v is not None for v in lps):
-            out[i] = float(sum(lps))
+    slow = [i for i in range(n) if i not in fast_set and users[i]]
+    if slow:
+        vals = text_compat_span_sums(engine, tok, [systems[i] for i in slow],
+                                     [users[i] for i in slow])
+        out[torch.as_tensor(slow)] = torch.as_tensor(vals, dtype=torch.float64)
     return out.to(engine.device) if device_out else out
+
+
+@torch.no_grad()
+def text_compat_span_sums(engine, tok, systems: Sequence[Optional[str]],
+                          users: Sequence[str]) -> List[float]:
+    """``sum(get_prompt_logprobs(.., systems[i], users[i])[1])`` (NaN where that call gives
+    no usable log-probs) for many pairs in ONE batched prefill: the reference's span
+    (first-occurrence ``find``, char overlap; src/utils.py:284-373) depends only on the
+    token strings, so only the kept positions' rows go through the LM head."""
+    n = len(users)
+    res = [float("nan")] * n
+    idss, keeps = [], []
+    for s, u in zip(systems, users):
+        try:
+            api_user = u + MARKER if u.endswith(("\n", " ")) else u
+            ids, _ = tok.render_chat(s or None, api_user)
+            data = SimpleNamespace(tokens=tok.tokens(ids), token_logprobs=list(range(len(ids))))
+            _, keep = extract_user_prompt_logprobs(data, u)
+        except Exception as e:       # get_prompt_logprobs would return ([], [])
+            logger.error("get_prompt_logprobs failed: %s", e)
+            ids, keep = [], []
+        idss.append(list(ids))
+        keeps.append(keep)
+    # position 0 has no log-prob (None in the reference's list -> no usable sum)
+    todo = [j for j in range(n) if keeps[j] and keeps[j][0] > 0]
+    if not todo:
+        return res
+    dev = engine.device
+    cache = engine.prefill([idss[j] for j in todo])
+    r_idx = [r for r, j in enumerate(todo) for _ in keeps[j]]
+    p_idx = [i - 1 for j in todo for i in keeps[j]]
+    tgt = [idss[j][i] for j in todo for i in keeps[j]]
+    rows = cache.hidden[torch.as_tensor(r_idx, device=dev), torch.as_tensor(p_idx, device=dev)]
+    lp = engine.rows_logprobs(rows, torch.as_tensor(tgt, dtype=torch.int32, device=dev)[:, None])
+    lp = lp.view(-1).double().cpu().tolist()
+    o = 0
+    for j in todo:                   # the reference's Python sum, in span order
+        k = len(keeps[j])
+        res[j] = float(sum(lp[o:o + k]))
+        o += k
+    return res
 
 
 def get_token_ids(model, text) -> Dict[str, int]:

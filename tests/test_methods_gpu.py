@@ -85,3 +85,30 @@ def test_score_tree_matches_per_path_scoring(traces):
         offs = engine.offsets(paths, engine.device)
         last = lp[offs[1:].long() - 1]                                       # each path's last token
         assert torch.max(torch.abs(last - node_lp[a])).item() < 1e-4
+
+
+def test_batched_span_sums_match_per_call_reference_semantics(traces):
+    """utils.user_span_sums (id-level fast path + the batched text-compat path, with the
+    engine's prefix reuse) == the sum of get_prompt_logprobs per (system, user) call, the
+    reference's own per-call primitive (src/utils.py:201-373; mcts.py:270-320, 343-368),
+    including spans the first-occurrence find lands on inside the system text, the
+    U+200B marker, empty and absent user prompts."""
+    utils = importlib.import_module(mp.PKG + ".utils")
+    mid = traces["model_id"]
+    op = next(iter(traces["agent_opinions"].values()))
+    sysA = f"You are a participant.\n\nIssue: {traces['issue']}\nOpinion: {op}\nStatement: We"
+    sysB = sysA + " should act"
+    pairs = [(sysA, " should"), (sysB, "e"), (sysA, "a "), (sysB, " together\n"),
+             (None, "hello there"), (sysA, ""), (sysB, op[:12]), (sysA, " act now"),
+             (sysB, "ct")]
+    systems, users = [p[0] for p in pairs], [p[1] for p in pairs]
+    want = []
+    for s, u in pairs:
+        _, lps = utils.get_prompt_logprobs(mid, s, u)
+        want.append(float(sum(lps)) if lps and all(v is not None for v in lps) else float("nan"))
+    got = utils.user_span_sums(mid, systems, users).tolist()
+    got2 = utils.user_span_sums(mid, systems, users).tolist()     # served from the store
+    for w, g, g2 in zip(want, got, got2):
+        assert (w != w) == (g != g) == (g2 != g2)
+        if w == w:
+            assert abs(w - g) <= 1e-3 and abs(w - g2) <= 1e-3, (w, g, g2)
