@@ -162,11 +162,16 @@ class Model:
             return (y * (1.0 + w.float())).to(x.dtype)
         return (w * y.to(x.dtype)) if x.dtype != torch.float32 else (w.float() * y)
 
-    def _rope(self, x: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
-        """x [B, H, T, D], pos [B, T] (half-rotation convention)."""
+    def _rope_tables(self, pos: torch.Tensor, dtype) -> tuple:
+        """(cos, sin) [B, 1, T, D] of positions pos [B, T]; computed once per forward and
+        shared by every layer's q and k."""
         ang = pos.to(torch.float32)[:, None, :, None] * self.inv_freq[None, None, None, :]
-        cos = torch.cat([ang.cos(), ang.cos()], dim=-1).to(x.dtype)
-        sin = torch.cat([ang.sin(), ang.sin()], dim=-1).to(x.dtype)
+        c, s = ang.cos(), ang.sin()
+        return torch.cat([c, c], dim=-1).to(dtype), torch.cat([s, s], dim=-1).to(dtype)
+
+    def _rope(self, x: torch.Tensor, pos: torch.Tensor, tables: Optional[tuple] = None) -> torch.Tensor:
+        """x [B, H, T, D], pos [B, T] (half-rotation convention)."""
+        cos, sin = tables if tables is not None else self._rope_tables(pos, x.dtype)
         h = x.shape[-1] // 2
         rot = torch.cat([-x[..., h:], x[..., :h]], dim=-1)
         return x * cos + rot * sin
@@ -202,34 +207,33 @@ class Model:
             return p @ v
         return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=scale)
 
-    def _layer(self, i, h, pos, ctx_k, ctx_v, ctx_mask, ctx_pos, self_mask=None):
+    def _layer(self, i, h, pos, ctx_k, ctx_v, ctx_mask, ctx_pos, self_mask=None, pre=None):
         """One decoder layer over new tokens h [B,T,d] at positions pos [B,T].
 
         ctx_k/ctx_v [B,Hkv,S,D] is the earlier context (prefix + history), visible
         where ctx_mask [B,S] is True.  The new tokens see each other causally, or through
         self_mask [T,T] (True = attend; e.g. a token tree: ancestors and self).
-        Returns (h, k_new, v_new)."""
+        ``pre`` = _prepare(...) of this forward (rope tables, mask, key positions), shared
+        by the layers.  Returns (h, k_new, v_new)."""
         c = self.cfg
         p = f"l{i}."
         B, T, _ = h.shape
+        if pre is None:
+            pre = self._prepare(pos, h.dtype, ctx_mask if ctx_k is not None else None, ctx_pos,
+                                self_mask)
+        tables, m, kp = pre
         x = self._rms(h, self.w[p + "attn_norm"])
         q = (x @ self.w[p + "wq"].t()).view(B, T, c.n_heads, c.head_dim).transpose(1, 2)
         k = (x @ self.w[p + "wk"].t()).view(B, T, c.n_kv_heads, c.head_dim).transpose(1, 2)
         v = (x @ self.w[p + "wv"].t()).view(B, T, c.n_kv_heads, c.head_dim).transpose(1, 2)
-        q = self._rope(q, pos)
-        k = self._rope(k, pos)
-        causal = (torch.ones(T, T, dtype=torch.bool, device=h.device).tril()
-                  if self_mask is None else self_mask)
+        q = self._rope(q, pos, tables)
+        k = self._rope(k, pos, tables)
         if ctx_k is not None:
             K = torch.cat([ctx_k, k], dim=2)
             V = torch.cat([ctx_v, v], dim=2)
-            S = ctx_k.shape[2]
-            m = torch.cat([ctx_mask[:, None, :].expand(B, T, S), causal[None].expand(B, T, T)], -1)
-            kp = torch.cat([ctx_pos, pos], dim=1)
         else:
-            K, V, kp = k, v, pos
-            m = causal[None].expand(B, T, T)
-        o = self._attend(i, q, K, V, m[:, None], pos, kp)
+            K, V = k, v
+        o = self._attend(i, q, K, V, m, pos, kp)
         o = o.transpose(1, 2).reshape(B, T, c.n_heads * c.head_dim) @ self.w[p + "wo"].t()
         if c.family == "gemma2":
             o = self._rms(o, self.w[p + "post_attn_norm"])
@@ -239,6 +243,21 @@ class Model:
         if c.family == "gemma2":
             y = self._rms(y, self.w[p + "post_mlp_norm"])
         return h + y, k, v
+
+    def _prepare(self, pos, dtype, ctx_mask=None, ctx_pos=None, self_mask=None):
+        """Per-forward inputs every layer shares: rope tables, the attention mask
+        [B, 1, T, S+T] (context where ctx_mask, the new tokens causally or by self_mask)
+        and the key positions."""
+        B, T = pos.shape
+        causal = (torch.ones(T, T, dtype=torch.bool, device=pos.device).tril()
+                  if self_mask is None else self_mask)
+        if ctx_mask is not None:
+            S = ctx_mask.shape[1]
+            m = torch.cat([ctx_mask[:, None, :].expand(B, T, S), causal[None].expand(B, T, T)], -1)
+            kp = torch.cat([ctx_pos, pos], dim=1)
+        else:
+            m, kp = causal[None].expand(B, T, T), pos
+        return self._rope_tables(pos, dtype), m[:, None], kp
 
     # --- public forward ----------------------------------------------------------
     @torch.no_grad()
@@ -250,9 +269,10 @@ class Model:
         valid = pos < lengths[:, None]
         h = self._embed(ids)
         kv = []
+        pre = self._prepare(pos, h.dtype)
         for i in range(self.cfg.n_layers):
             # padding keys sit after every valid key, so the causal mask already hides them
-            h, k, v = self._layer(i, h, pos, None, None, None, None)
+            h, k, v = self._layer(i, h, pos, None, None, None, None, pre=pre)
             kv.append((k, v))
         h = self._rms(h, self.w["norm"])
         return kv, h, valid
@@ -265,9 +285,11 @@ class Model:
         (final-norm hidden [R, T, d], new kv per layer)."""
         h = self._embed(tokens)
         new = []
+        pre = self._prepare(pos, h.dtype, ctx_mask if ctx_kv is not None else None, ctx_pos,
+                            self_mask)
         for i in range(self.cfg.n_layers):
             ck, cv = ctx_kv[i] if ctx_kv is not None else (None, None)
-            h, k, v = self._layer(i, h, pos, ck, cv, ctx_mask, ctx_pos, self_mask)
+            h, k, v = self._layer(i, h, pos, ck, cv, ctx_mask, ctx_pos, self_mask, pre=pre)
             new.append((k, v))
         return self._rms(h, self.w["norm"]), new
 
