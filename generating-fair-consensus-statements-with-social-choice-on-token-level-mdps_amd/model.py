@@ -190,14 +190,21 @@ class Model:
         return (act * u) @ self.w[p + "w_down"].t()
 
     def _attend(self, i: int, q, k, v, mask, q_pos, k_pos):
-        """q [B,H,T,D]; k,v [B,Hkv,S,D]; mask [B,1,T,S] bool (True = attend)."""
+        """q [B,H,T,D]; k,v [B,Hkv,S,D]; mask [B,1,rep*T,S] bool (True = attend; row r*T+t
+        is query t, see _prepare).  The rep query heads that share a K/V head ride along the
+        query axis ([B,Hkv,rep*T,D]), so K/V are attended in place, never repeated."""
         c = self.cfg
+        B, H, T, D = q.shape
         rep = c.n_heads // c.n_kv_heads
         if rep > 1:
-            k = k.repeat_interleave(rep, dim=1)
-            v = v.repeat_interleave(rep, dim=1)
+            q = q.reshape(B, c.n_kv_heads, rep * T, D)
+            q_pos = q_pos.repeat(1, rep)
         if c.sliding_window and i % 2 == 0:
             mask = mask & ((q_pos[:, None, :, None] - k_pos[:, None, None, :]) < c.sliding_window)
+        return self._attend_grouped(q, k, v, mask).reshape(B, H, T, D)
+
+    def _attend_grouped(self, q, k, v, mask):
+        c = self.cfg
         scale = (c.query_pre_attn_scalar ** -0.5) if c.query_pre_attn_scalar else c.head_dim ** -0.5
         if c.attn_softcap > 0:
             s = (q.float() @ k.float().transpose(-1, -2)) * scale
@@ -257,7 +264,11 @@ class Model:
             kp = torch.cat([ctx_pos, pos], dim=1)
         else:
             m, kp = causal[None].expand(B, T, T), pos
-        return self._rope_tables(pos, dtype), m[:, None], kp
+        m = m[:, None]
+        rep = self.cfg.n_heads // self.cfg.n_kv_heads
+        if rep > 1:                       # rows r*T + t: query t of group member r (_attend)
+            m = m.repeat(1, 1, rep, 1)
+        return self._rope_tables(pos, dtype), m, kp
 
     # --- public forward ----------------------------------------------------------
     @torch.no_grad()

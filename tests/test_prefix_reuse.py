@@ -71,3 +71,29 @@ def test_reuse_off_by_env(monkeypatch):
     eng.prefill([[1, 2, 3] * 10])
     eng.prefill([[1, 2, 3] * 10 + [4]])
     assert eng.reuse_stats["reused"] == 0 and not eng._store
+
+
+@pytest.mark.parametrize("preset", ["tiny-llama", "tiny-gemma"])
+def test_grouped_query_attention_equals_repeated_kv(preset):
+    """Model._attend runs the query heads of a K/V group along the query axis instead of
+    repeating K/V (GQA); the result equals attention over repeat_interleave'd K/V, with
+    the sliding window (gemma even layers) applied on the grouped positions."""
+    cfg = M.preset(preset, vocab=300)
+    m = M.Model(cfg, "cpu", torch.float32, seed=1)
+    g = torch.Generator().manual_seed(2)
+    B, T, S = 3, 5, 11
+    rep = cfg.n_heads // cfg.n_kv_heads
+    q = torch.randn(B, cfg.n_heads, T, cfg.head_dim, generator=g)
+    k = torch.randn(B, cfg.n_kv_heads, S, cfg.head_dim, generator=g)
+    v = torch.randn(B, cfg.n_kv_heads, S, cfg.head_dim, generator=g)
+    mask = torch.rand(B, 1, T, S, generator=g) > 0.3
+    mask[..., S - T:] |= torch.eye(T, dtype=torch.bool)          # every query sees itself
+    qp = torch.arange(S - T, S)[None].expand(B, T)
+    kp = torch.arange(S)[None].expand(B, S)
+    for layer in (0, 1):
+        got = m._attend(layer, q, k, v, mask.repeat(1, 1, rep, 1), qp, kp)
+        mm = mask
+        if cfg.sliding_window and layer % 2 == 0:
+            mm = mm & ((qp[:, None, :, None] - kp[:, None, None, :]) < cfg.sliding_window)
+        want = m._attend_grouped(q, k.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1), mm)
+        torch.testing.assert_close(got, want, atol=1e-6, rtol=1e-6)
