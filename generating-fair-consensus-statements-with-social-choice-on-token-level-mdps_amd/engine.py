@@ -20,6 +20,7 @@ Everything after the LM head runs in the HIP kernels (ops.*).
 from __future__ import annotations
 
 import os
+import threading
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -77,7 +78,7 @@ class ScoringEngine:
 
     def __init__(self, model: Model, max_rows_per_chunk: int = 32768,
                  max_streams_per_chunk: int = 1024, reuse_caches: Optional[int] = None,
-                 reuse_min_tokens: int = 16):
+                 reuse_min_tokens: int = 16, reuse_max_tokens: int = 1 << 18):
         self.model = model
         self.device = model.device
         self.softcap = model.cfg.final_softcap
@@ -89,7 +90,9 @@ class ScoringEngine:
             reuse_caches = 0 if os.environ.get("CS_PREFIX_REUSE", "1") == "0" else 4
         self.reuse_caches = int(reuse_caches)
         self.reuse_min_tokens = max(1, int(reuse_min_tokens))
+        self.reuse_max_tokens = int(reuse_max_tokens)   # bound on stored rows x width
         self._store: List[tuple] = []     # (PrefixCache, [np.int64 ids per row]), newest last
+        self._store_lock = threading.Lock()
         self.reuse_stats = {"prefills": 0, "reused": 0, "tokens": 0, "tokens_run": 0}
 
     # --- prefixes ---------------------------------------------------------------
@@ -101,7 +104,8 @@ class ScoringEngine:
         total = sum(r.shape[0] for r in rows)
         self.reuse_stats["prefills"] += 1
         self.reuse_stats["tokens"] += total
-        plan = self._reuse_plan(rows) if self.reuse_caches > 0 else None
+        with self._store_lock:
+            plan = self._reuse_plan(rows) if self.reuse_caches > 0 else None
         if plan is not None:
             cache = self._prefill_extending(prefixes, rows, *plan)
             self.reuse_stats["reused"] += 1
@@ -114,13 +118,17 @@ class ScoringEngine:
             pos = torch.arange(P, device=self.device)[None].expand(ids.shape[0], P)
             cache = PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid,
                                 hidden=h, ids=ids)
-        if self.reuse_caches > 0:
-            self._store.append((cache, rows))
-            del self._store[:-self.reuse_caches]
+        if self.reuse_caches > 0 and cache.ids.numel() <= self.reuse_max_tokens:
+            with self._store_lock:
+                self._store.append((cache, rows))
+                del self._store[:-self.reuse_caches]
+                while sum(c.ids.numel() for c, _ in self._store) > self.reuse_max_tokens:
+                    del self._store[0]
         return cache
 
     def reset_prefix_store(self) -> None:
-        self._store = []
+        with self._store_lock:
+            self._store = []
 
     def _reuse_plan(self, rows):
         """(stored cache, source row per prefix, reused length per prefix) from the stored

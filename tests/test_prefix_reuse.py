@@ -97,3 +97,16 @@ def test_grouped_query_attention_equals_repeated_kv(preset):
             mm = mm & ((qp[:, None, :, None] - kp[:, None, None, :]) < cfg.sliding_window)
         want = m._attend_grouped(q, k.repeat_interleave(rep, 1), v.repeat_interleave(rep, 1), mm)
         torch.testing.assert_close(got, want, atol=1e-6, rtol=1e-6)
+
+
+def test_store_is_bounded_by_tokens():
+    cfg = M.preset("tiny-llama", vocab=300)
+    eng = E.ScoringEngine(M.Model(cfg, "cpu", torch.float32, seed=3), reuse_caches=4,
+                          reuse_max_tokens=100)
+    eng.prefill([[5] * 60])
+    eng.prefill([[6] * 30])
+    assert [c.ids.numel() for c, _ in eng._store] == [60, 30]
+    eng.prefill([[7] * 50])                      # 140 > 100: the oldest goes
+    assert [c.ids.numel() for c, _ in eng._store] == [30, 50]
+    eng.prefill([[8] * 101])                     # larger than the whole budget: not stored
+    assert [c.ids.numel() for c, _ in eng._store] == [30, 50]
