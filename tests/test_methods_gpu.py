@@ -112,3 +112,42 @@ def test_batched_span_sums_match_per_call_reference_semantics(traces):
         assert (w != w) == (g != g) == (g2 != g2)
         if w == w:
             assert abs(w - g) <= 1e-3 and abs(w - g2) <= 1e-3, (w, g, g2)
+
+
+def test_methods_match_reference_traces_without_prefix_reuse(traces):
+    """The same replays with the engine's prefix reuse off (every prompt encoded in full,
+    as the reference does): reuse changes how much is encoded, not what is decided."""
+    runtime = importlib.import_module(mp.PKG + ".runtime")
+    eng, _ = runtime.get_engine(traces["model_id"])
+    keep = eng.reuse_caches
+    eng.reuse_caches = 0
+    eng.reset_prefix_store()
+    try:
+        failures = mp.check_methods(traces)
+    finally:
+        eng.reuse_caches = keep
+    assert not failures, "\n".join(failures)
+
+
+def test_prefix_reuse_prefill_matches_full_prefill_on_gpu(traces):
+    """An extending prefill (stored K/V + only the new tokens) equals a full prefill on the
+    device's attention / GEMM kernels (fp32 fixture model)."""
+    runtime = importlib.import_module(mp.PKG + ".runtime")
+    E = importlib.import_module(mp.PKG + ".engine")
+    eng, _ = runtime.get_engine(traces["model_id"])
+    g = torch.Generator().manual_seed(9)
+    V = traces["vocab"]
+    base = [torch.randint(3, V, (n,), generator=g).tolist() for n in (70, 41, 96)]
+    new = [base[0] + [5, 6, 7], base[2][:80] + [9] * 11, base[1][:30], base[0][:69] + [4]]
+    ref = E.ScoringEngine(eng.model, reuse_caches=0).prefill(new)
+    e2 = E.ScoringEngine(eng.model, reuse_caches=4, reuse_min_tokens=4)
+    e2.prefill(base)
+    got = e2.prefill(new)
+    assert e2.reuse_stats["reused"] == 1
+    v = ref.valid
+    torch.testing.assert_close(got.last_hidden, ref.last_hidden, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(got.hidden[v], ref.hidden[v], atol=1e-4, rtol=1e-4)
+    for (ka, va), (kb, vb) in zip(got.kv, ref.kv):
+        m = v[:, None, :, None].expand_as(ka)
+        torch.testing.assert_close(ka[m], kb[m], atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(va[m], vb[m], atol=1e-4, rtol=1e-4)
