@@ -180,18 +180,18 @@ class Model:
         return (y * (1.0 + w.float())).to(x.dtype)
 
     def _rope_tables(self, pos: torch.Tensor, dtype) -> tuple:
-        """(cos, sin) [B, 1, T, D] of positions pos [B, T]; computed once per forward and
-        shared by every layer's q and k."""
+        """(cos, signed sin) [B, 1, T, D] of positions pos [B, T]: [cos, cos] and
+        [-sin, sin]; computed once per forward and shared by every layer's q and k."""
         ang = pos.to(torch.float32)[:, None, :, None] * self.inv_freq[None, None, None, :]
         c, s = ang.cos(), ang.sin()
-        return torch.cat([c, c], dim=-1).to(dtype), torch.cat([s, s], dim=-1).to(dtype)
+        return torch.cat([c, c], dim=-1).to(dtype), torch.cat([-s, s], dim=-1).to(dtype)
 
     def _rope(self, x: torch.Tensor, pos: torch.Tensor, tables: Optional[tuple] = None) -> torch.Tensor:
-        """x [B, H, T, D], pos [B, T] (half-rotation convention)."""
-        cos, sin = tables if tables is not None else self._rope_tables(pos, x.dtype)
-        h = x.shape[-1] // 2
-        rot = torch.cat([-x[..., h:], x[..., :h]], dim=-1)
-        return x * cos + rot * sin
+        """x [B, H, T, D], pos [B, T] (half-rotation convention):
+        x * cos + [-x2, x1] * sin, with [x2, x1] = roll(x, D/2) and the sign in the table
+        (3 launches instead of 5)."""
+        cos, ssin = tables if tables is not None else self._rope_tables(pos, x.dtype)
+        return torch.addcmul(x * cos, x.roll(x.shape[-1] // 2, dims=-1), ssin)
 
     def _embed(self, ids: torch.Tensor) -> torch.Tensor:
         h = self.w["embed"][ids]

@@ -110,3 +110,19 @@ def test_store_is_bounded_by_tokens():
     assert [c.ids.numel() for c, _ in eng._store] == [30, 50]
     eng.prefill([[8] * 101])                     # larger than the whole budget: not stored
     assert [c.ids.numel() for c, _ in eng._store] == [30, 50]
+
+
+def test_rope_matches_half_rotation_formula():
+    """Model._rope (roll + signed-sin table) == x*cos + cat(-x2, x1)*sin, the HF
+    rotate_half convention the reference models use."""
+    cfg = M.preset("tiny-llama", vocab=300)
+    m = M.Model(cfg, "cpu", torch.float32, seed=1)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, cfg.n_heads, 7, cfg.head_dim, generator=g)
+    pos = torch.arange(3, 10)[None].expand(2, 7)
+    ang = pos.float()[:, None, :, None] * m.inv_freq[None, None, None, :]
+    cos = torch.cat([ang.cos(), ang.cos()], -1)
+    sin = torch.cat([ang.sin(), ang.sin()], -1)
+    h = cfg.head_dim // 2
+    want = x * cos + torch.cat([-x[..., h:], x[..., :h]], -1) * sin
+    torch.testing.assert_close(m._rope(x, pos), want, atol=1e-6, rtol=1e-6)
