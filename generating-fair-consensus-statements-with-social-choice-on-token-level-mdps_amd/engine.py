@@ -26,6 +26,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
+import torch.nn.functional as F
 
 from . import ops
 from .model import Model
@@ -276,8 +277,13 @@ class ScoringEngine:
             inp = toks[:, :T - 1]
             plen = cache.lengths[own]
             pos = plen[:, None] + torch.arange(T - 1, device=dev)[None]
-            ctx = [(k[own], v[own]) for k, v in cache.kv]
+            # per-stream context with T - 1 free key slots: extend writes the new keys into
+            # them instead of concatenating per layer (padding the n_prefix source rows is
+            # cheap; the gather to R streams happens once either way)
+            room = (0, 0, 0, T - 1)
+            ctx = [(F.pad(k, room)[own], F.pad(v, room)[own]) for k, v in cache.kv]
             h, _ = m.extend(inp, pos, ctx, cache.valid[own], cache.pos[own])
+            del ctx
         flat_h, flat_t = [], []
         lens_l = lens.tolist()
         last = cache.last_hidden[own]

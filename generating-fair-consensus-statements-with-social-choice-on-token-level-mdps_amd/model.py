@@ -268,7 +268,14 @@ class Model:
         v = v.contiguous().view(B, T, c.n_kv_heads, c.head_dim).transpose(1, 2)
         q = self._rope(q, pos, tables_q)
         k = self._rope(k, pos, tables)
-        if ctx_k is not None:
+        if ctx_k is not None and ctx_k.shape[2] == ctx_mask.shape[1] + T:
+            # the caller left T free key slots after the context: write the new keys there
+            # instead of concatenating (one copy of the context per layer saved)
+            S = ctx_mask.shape[1]
+            ctx_k[:, :, S:] = k
+            ctx_v[:, :, S:] = v
+            K, V = ctx_k, ctx_v
+        elif ctx_k is not None:
             K = torch.cat([ctx_k, k], dim=2)
             V = torch.cat([ctx_v, v], dim=2)
         else:
@@ -328,7 +335,9 @@ class Model:
     def extend(self, tokens: torch.Tensor, pos: torch.Tensor, ctx_kv, ctx_mask: torch.Tensor,
                ctx_pos: torch.Tensor, self_mask: torch.Tensor = None):
         """tokens [R, T], pos [R, T]; ctx_kv per layer (k, v) [R, Hkv, S, D] with
-        ctx_mask [R, S]; self_mask [T, T] (optional, default causal).  Returns
+        ctx_mask [R, S] (or [R, Hkv, S + T, D] buffers whose last T slots are free: the new
+        keys are written there, the buffers are modified); self_mask [T, T] (optional,
+        default causal).  Returns
         (final-norm hidden [R, T, d], new kv per layer)."""
         h = self._embed(tokens)
         new = []
