@@ -55,13 +55,25 @@ def _pad(seqs: Sequence[Sequence[int]], device, fill: int = 0):
     return out.to(device, non_blocking=True), lens.to(device, non_blocking=True)
 
 
-def _lcp(a: np.ndarray, b: np.ndarray) -> int:
-    """Length of the common leading run of two token-id arrays."""
-    n = min(a.shape[0], b.shape[0])
+def _id_matrix(rows) -> np.ndarray:
+    """Token ids of stored rows as one [n, width] array, right-padded with -1 (never a
+    token id, so it ends every common run)."""
+    m = np.full((len(rows), max(r.shape[0] for r in rows)), -1, dtype=np.int64)
+    for i, r in enumerate(rows):
+        m[i, :r.shape[0]] = r
+    return m
+
+
+def _best_lcp(r: np.ndarray, smat: np.ndarray):
+    """(first stored row with the longest common token prefix with r, that length): one
+    vectorised compare against every stored row."""
+    n = min(r.shape[0], smat.shape[1])
     if n == 0:
-        return 0
-    d = np.flatnonzero(a[:n] != b[:n])
-    return int(d[0]) if d.size else n
+        return 0, 0
+    mism = smat[:, :n] != r[None, :n]
+    lcp = np.where(mism.any(axis=1), mism.argmax(axis=1), n)
+    j = int(lcp.argmax())
+    return j, int(lcp[j])
 
 
 class ScoringEngine:
@@ -92,7 +104,7 @@ class ScoringEngine:
         self.reuse_caches = int(reuse_caches)
         self.reuse_min_tokens = max(1, int(reuse_min_tokens))
         self.reuse_max_tokens = int(reuse_max_tokens)   # bound on stored rows x width
-        self._store: List[tuple] = []     # (PrefixCache, [np.int64 ids per row]), newest last
+        self._store: List[tuple] = []     # (PrefixCache, [rows, width] ids, -1 padded), newest last
         self._store_lock = threading.Lock()
         self.reuse_stats = {"prefills": 0, "reused": 0, "tokens": 0, "tokens_run": 0}
 
@@ -121,7 +133,7 @@ class ScoringEngine:
                                 hidden=h, ids=ids)
         if self.reuse_caches > 0 and cache.ids.numel() <= self.reuse_max_tokens:
             with self._store_lock:
-                self._store.append((cache, rows))
+                self._store.append((cache, _id_matrix(rows)))
                 del self._store[:-self.reuse_caches]
                 while sum(c.ids.numel() for c, _ in self._store) > self.reuse_max_tokens:
                     del self._store[0]
@@ -136,14 +148,10 @@ class ScoringEngine:
         cache that saves the most padded work, or None when a full prefill is as cheap."""
         best = None
         full_cost = len(rows) * max(r.shape[0] for r in rows)
-        for cache, srows in self._store:
+        for cache, smat in self._store:
             src, lcp = [], []
             for r in rows:
-                bi, bl = 0, 0
-                for j, s in enumerate(srows):
-                    l = _lcp(r, s)
-                    if l > bl:
-                        bi, bl = j, l
+                bi, bl = _best_lcp(r, smat)
                 bl = min(bl, r.shape[0] - 1)          # at least one token runs
                 if bl < self.reuse_min_tokens:
                     bl = 0

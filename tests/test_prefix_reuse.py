@@ -126,3 +126,25 @@ def test_rope_matches_half_rotation_formula():
     h = cfg.head_dim // 2
     want = x * cos + torch.cat([-x[..., h:], x[..., :h]], -1) * sin
     torch.testing.assert_close(m._rope(x, pos), want, atol=1e-6, rtol=1e-6)
+
+
+def test_best_common_prefix_search_matches_pairwise_scan():
+    import numpy as np
+    rng = np.random.default_rng(0)
+    base = rng.integers(0, 5, 40)
+    stored = [np.concatenate([base[:rng.integers(0, 40)], rng.integers(0, 5, rng.integers(0, 9))])
+              for _ in range(25)] + [base[:0] + 1, base.copy()]
+    stored = [s if s.size else base[:1] for s in stored]
+    smat = E._id_matrix(stored)
+    for _ in range(50):
+        r = np.concatenate([base[:rng.integers(0, 41)], rng.integers(0, 5, rng.integers(0, 6))])
+        if r.size == 0:
+            continue
+        want_j, want_l = 0, 0
+        for j, s in enumerate(stored):                 # first row with the longest run
+            n = min(len(r), len(s))
+            l = next((i for i in range(n) if r[i] != s[i]), n)
+            if l > want_l:
+                want_j, want_l = j, l
+        got_j, got_l = E._best_lcp(r, smat)
+        assert got_l == want_l and (want_l == 0 or got_j == want_j)
