@@ -151,3 +151,35 @@ def test_prefix_reuse_prefill_matches_full_prefill_on_gpu(traces):
         m = v[:, None, :, None].expand_as(ka)
         torch.testing.assert_close(ka[m], kb[m], atol=1e-4, rtol=1e-4)
         torch.testing.assert_close(va[m], vb[m], atol=1e-4, rtol=1e-4)
+
+
+def test_score_matches_full_forward_of_prefix_plus_continuation(traces):
+    """engine.score (prefix K/V once per agent, continuations batched as streams with free
+    key slots, chunked) == the log-probs of a plain full forward over prefix +
+    continuation for every stream (ragged lengths, several owners, tiny chunks)."""
+    R = importlib.import_module(mp.PKG + ".runtime")
+    E = importlib.import_module(mp.PKG + ".engine")
+    base, tok = R.get_engine(traces["model_id"])
+    eng = E.ScoringEngine(base.model, max_rows_per_chunk=23, max_streams_per_chunk=3,
+                          reuse_caches=0)
+    g = torch.Generator().manual_seed(8)
+    V = traces["vocab"]
+    prefixes = [[tok.bos_id] + torch.randint(3, V, (n,), generator=g).tolist() for n in (9, 30, 17)]
+    conts = [torch.randint(3, V, (n,), generator=g).tolist() for n in (1, 7, 12, 3, 1, 9, 5)]
+    owner = [0, 1, 2, 1, 0, 2, 0]
+    cache = eng.prefill(prefixes)
+    lp = eng.score(cache, owner, conts).double().cpu()
+    offs = [0]
+    for c in conts:
+        offs.append(offs[-1] + len(c))
+    for r, (o, c) in enumerate(zip(owner, conts)):
+        ids = torch.as_tensor(prefixes[o] + c, device=eng.device)[None]
+        _, h, _ = eng.model.prefill(ids, torch.tensor([ids.shape[1]], device=eng.device))
+        P = len(prefixes[o])
+        rows = h[0, P - 1:P - 1 + len(c)]
+        z = eng.model.lm_head(rows).double()
+        if eng.softcap:                          # gemma-2 final logit soft-cap
+            z = eng.softcap * torch.tanh(z / eng.softcap)
+        want = torch.log_softmax(z, -1)
+        want = want[torch.arange(len(c)), torch.as_tensor(c, device=eng.device)].cpu()
+        assert torch.max(torch.abs(lp[offs[r]:offs[r + 1]] - want)).item() < 1e-4, r
