@@ -412,7 +412,6 @@ class BeamState:
         c = self.cache
         plen = c.lengths[own]
         pos = (plen + self.G)[:, None]
-        ctx, cmask, cpos = [], None, None
         pre_mask = c.valid[own]
         pre_pos = c.pos[own]
         if self.G > 0:
@@ -420,17 +419,23 @@ class BeamState:
             cmask = torch.cat([pre_mask, torch.ones(len(own), self.G, dtype=torch.bool,
                                                     device=dev)], 1)
             cpos = torch.cat([pre_pos, gpos], 1)
-            for (pk, pv), (gk, gv) in zip(c.kv, self.gen_kv):
-                ctx.append((torch.cat([pk[own], gk[src]], 2), torch.cat([pv[own], gv[src]], 2)))
         else:
             cmask, cpos = pre_mask, pre_pos
-            ctx = [(pk[own], pv[own]) for pk, pv in c.kv]
-        h, new = m.extend(tok, pos, ctx, cmask, cpos)
-        if self.G > 0:
-            self.gen_kv = [(torch.cat([gk[src], nk], 2), torch.cat([gv[src], nv], 2))
-                           for (gk, gv), (nk, nv) in zip(self.gen_kv, new)]
-        else:
-            self.gen_kv = new
+        # per stream one buffer [prefix | history | 1 free slot]: the prefix rows padded once
+        # and gathered, the parents' history written in, the new key written into the slot
+        # by extend; the next history is a view of the buffer (no concatenations)
+        Pm = c.kv[0][0].shape[2]
+        room = (0, 0, 0, self.G + 1)
+        ctx = []
+        for li, (pk, pv) in enumerate(c.kv):
+            kb, vb = F.pad(pk, room)[own], F.pad(pv, room)[own]
+            if self.G > 0:
+                gk, gv = self.gen_kv[li]
+                kb[:, :, Pm:Pm + self.G] = gk[src]
+                vb[:, :, Pm:Pm + self.G] = gv[src]
+            ctx.append((kb, vb))
+        h, _ = m.extend(tok, pos, ctx, cmask, cpos)
+        self.gen_kv = [(kb[:, :, Pm:], vb[:, :, Pm:]) for kb, vb in ctx]
         self.G += 1
         self.n_beams = Bn
         self.next_hidden = h[:, 0, :]
