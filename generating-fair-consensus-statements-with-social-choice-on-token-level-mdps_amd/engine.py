@@ -231,7 +231,8 @@ class ScoringEngine:
             return out
         toks, lens = _pad(conts, dev)
         pos = cache.lengths[own][:, None] + torch.arange(toks.shape[1], device=dev)[None]
-        ctx = [(k[own], v[own]) for k, v in cache.kv]
+        room = (0, 0, 0, toks.shape[1])             # free key slots (see _score_chunk)
+        ctx = [(F.pad(k, room)[own], F.pad(v, room)[own]) for k, v in cache.kv]
         h, _ = self.model.extend(toks, pos, ctx, cache.valid[own], cache.pos[own])
         has = lens > 0
         idx = (lens - 1).clamp(min=0)
@@ -346,7 +347,8 @@ class ScoringEngine:
             it = toks[:, ii.to(dev)]
             pos = cache.lengths[own][:, None] + torch.as_tensor([depth[n] for n in internal],
                                                                 device=dev)[None]
-            ctx = [(k[own], v[own]) for k, v in cache.kv]
+            room = (0, 0, 0, len(internal))         # free key slots (see _score_chunk)
+            ctx = [(F.pad(k, room)[own], F.pad(v, room)[own]) for k, v in cache.kv]
             h, _ = self.model.extend(it, pos, ctx, cache.valid[own], cache.pos[own],
                                      self_mask=anc[ii][:, ii].to(dev))
             hpad = torch.cat([last[:, None, :], h], dim=1)
