@@ -182,8 +182,9 @@ class ScoringEngine:
         Pc = base.ids.shape[1]
         pos = l_t[:, None] + torch.arange(S, device=dev)[None]
         cmask = torch.arange(Pc, device=dev)[None] < l_t[:, None]
-        ctx = [(k[s_t], v[s_t]) for k, v in base.kv]
-        h_new, new = self.model.extend(suf, pos, ctx, cmask, base.pos[s_t])
+        room = (0, 0, 0, S)            # free key slots: extend writes the new keys there
+        ctx = [(F.pad(k, room)[s_t], F.pad(v, room)[s_t]) for k, v in base.kv]
+        h_new, _ = self.model.extend(suf, pos, ctx, cmask, base.pos[s_t])
         # contiguous layout, position j of row r: base row j (j < lcp) or new j - lcp
         ids, lens = _pad(prefixes, dev)
         P = ids.shape[1]
@@ -191,12 +192,11 @@ class ScoringEngine:
         idx = torch.where(j < l_t[:, None], j, Pc + (j - l_t[:, None]).clamp(max=S - 1))
         idx = idx.clamp(max=Pc + S - 1)
 
-        def merge(old, fresh):                   # [R, H, Pc, D] + [R, H, S, D] -> [R, H, P, D]
-            both = torch.cat([old, fresh], dim=2)
+        def merge(both):                         # [R, H, Pc + S, D] -> [R, H, P, D]
             g = idx[:, None, :, None].expand(R, both.shape[1], P, both.shape[3])
             return torch.gather(both, 2, g)
 
-        kv = [(merge(ck, nk), merge(cv, nv)) for (ck, cv), (nk, nv) in zip(ctx, new)]
+        kv = [(merge(kb), merge(vb)) for kb, vb in ctx]
         hb = torch.cat([base.hidden[s_t], h_new], dim=1)
         h = torch.gather(hb, 1, idx[:, :, None].expand(R, P, hb.shape[2]))
         valid = j < lens[:, None]
