@@ -437,7 +437,139 @@ class BeamState:
                 vb[:, :, Pm:Pm + self.G] = gv[src]
             ctx.append((kb, vb))
         h, _ = m.extend(tok, pos, ctx, cmask, cpos)
-        self.gen_kv = [(kb[:, :, Pm:], vb[:, :, Pm:]) for kb, vb in ctx]
+        # compact history copies: views would keep every layer's whole [prefix | history]
+        # context buffer alive until the next advance (2x the persistent K/V at peak)
+        self.gen_kv = [(kb[:, :, Pm:].clone(), vb[:, :, Pm:].clone()) for kb, vb in ctx]
+        del ctx
         self.G += 1
         self.n_beams = Bn
         self.next_hidden = h[:, 0, :]
+
+
+def _ceil32(n: int) -> int:
+    return max(32, (int(n) + 31) // 32 * 32)
+
+
+@dataclass
+class FusedPrefix:
+    """Prefix K/V in the cs_prefix_attention layouts (include/consensus_scoring.h)."""
+    k: list                     # per layer [n_prefix, Hkv, ldp, D]
+    vt: list                    # per layer [n_prefix, Hkv, D, ldp] (V transposed)
+    lengths: torch.Tensor       # [n_prefix] int32 (device)
+    ldp: int
+
+
+def fused_prefix(cache: PrefixCache) -> FusedPrefix:
+    """The prefill's K/V re-laid for the stream kernels: key capacity rounded up to 32
+    (zero-filled), V transposed so its rows are key-contiguous.  One copy per prefill."""
+    n, Hkv, P, D = cache.kv[0][0].shape
+    ldp = _ceil32(P)
+    ks, vts = [], []
+    for k, v in cache.kv:
+        kp = torch.zeros(n, Hkv, ldp, D, dtype=k.dtype, device=k.device)
+        kp[:, :, :P] = k
+        vt = torch.zeros(n, Hkv, D, ldp, dtype=v.dtype, device=v.device)
+        vt[..., :P] = v.transpose(2, 3)
+        ks.append(kp)
+        vts.append(vt)
+    return FusedPrefix(k=ks, vt=vts, lengths=cache.lengths.to(torch.int32), ldp=ldp)
+
+
+class DecodeState:
+    """Static-shape incremental decode of n_beams streams per prefix on the HIP stream
+    kernels (bf16 models; BeamState is the general eager path).
+
+    Streams are prefix-major, s = p * n_beams + b, always n_beams of them per prefix (the
+    caller pads missing beams with copies and ignores their candidates).  Every stream's
+    generated K/V lives in a preallocated history buffer [S, Hkv, ldh, D] (V transposed),
+    slot t = the token of step t; the prefix K/V is shared by the stream's n_beams
+    siblings through cs_prefix_attention.  ``advance`` = gather the parents' histories
+    (one index_select per buffer into the other half of a ping-pong pair), forward the new
+    tokens with hist_base = t read from device memory, keep the final-norm hidden.  After
+    the first (eager) advance each parity's step is captured once in a hipGraph and
+    replayed, so a decode step costs one graph launch plus its inputs' copies; ``post``
+    (optional, fixed per state) is captured with it, e.g. the LM head + the fused
+    cs_beam_decode_step of the beam search.
+
+    Restates the reference's per-step re-encoding of every agent prompt + beam text
+    (src/methods/beam_search.py:491-538 through src/utils.py:249-259) as one token per
+    stream per step."""
+
+    def __init__(self, engine: "ScoringEngine", cache: PrefixCache, n_prefix: int, n_beams: int,
+                 max_steps: int, use_graphs: bool = True):
+        self.e = engine
+        m = engine.model
+        c = m.cfg
+        self.P, self.B = int(n_prefix), int(n_beams)
+        self.S = self.P * self.B
+        dev = engine.device
+        self.pfx = fused_prefix(cache)
+        self.ldh = _ceil32(max_steps)
+        self.max_steps = int(max_steps)
+
+        def buffers():
+            return ([torch.zeros(self.S, c.n_kv_heads, self.ldh, c.head_dim, dtype=m.dtype, device=dev)
+                     for _ in range(c.n_layers)],
+                    [torch.zeros(self.S, c.n_kv_heads, c.head_dim, self.ldh, dtype=m.dtype, device=dev)
+                     for _ in range(c.n_layers)])
+
+        self.hist = [buffers(), buffers()]
+        self.cur = 0
+        self.steps = 0                                   # tokens appended so far (host copy)
+        self.hist_base = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.src = torch.arange(self.S, dtype=torch.long, device=dev)
+        self.tok = torch.zeros(self.S, dtype=torch.long, device=dev)
+        self.hidden = cache.last_hidden.repeat_interleave(self.B, dim=0).contiguous()   # [S, d]
+        self.use_graphs = use_graphs
+        self._graphs: dict = {}
+        self._pool = None
+
+    @property
+    def n_beams(self) -> int:
+        return self.B
+
+    def _body(self, post) -> None:
+        m = self.e.model
+        old_k, old_v = self.hist[self.cur]
+        new_k, new_v = self.hist[1 - self.cur]
+        for i in range(len(old_k)):
+            torch.index_select(old_k[i], 0, self.src, out=new_k[i])
+            torch.index_select(old_v[i], 0, self.src, out=new_v[i])
+        h = m.forward_streams(self.tok, self.pfx, new_k, new_v, self.hist_base, self.B, 1)
+        self.hidden.copy_(h)
+        self.hist_base += 1
+        if post is not None:
+            post()
+
+    @torch.no_grad()
+    def advance(self, parent: Sequence[int], tokens: Sequence[int], post=None) -> None:
+        """New beam j of every prefix = (parent beam parent[j], token tokens[j]), j < n_beams."""
+        if len(parent) != self.B or len(tokens) != self.B:
+            raise ValueError(f"advance takes exactly n_beams = {self.B} (parent, token) pairs")
+        if self.steps >= self.ldh:
+            raise ValueError("history capacity exhausted (max_steps)")
+        dev = self.e.device
+        P, B = self.P, self.B
+        par = torch.as_tensor(list(parent), dtype=torch.long)
+        src = (torch.arange(P)[:, None] * B + par[None, :]).reshape(-1)
+        tok = torch.as_tensor(list(tokens), dtype=torch.long).repeat(P)
+        self.src.copy_(src.to(dev, non_blocking=True))
+        self.tok.copy_(tok.to(dev, non_blocking=True))
+        key = (self.cur, post)
+        if not self.use_graphs or self.steps == 0:
+            self._body(post)                      # the first step runs eagerly (warm-up)
+        else:
+            g = self._graphs.get(key)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                s = torch.cuda.Stream(device=dev)
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, pool=self._pool, stream=s):
+                        self._body(post)
+                torch.cuda.current_stream().wait_stream(s)
+                self._pool = g.pool()
+                self._graphs[key] = g
+            g.replay()
+        self.cur = 1 - self.cur
+        self.steps += 1

@@ -14,6 +14,14 @@ Reference step (beam_search.py:439-617), same config keys:
     its beam, U = R + lp, min over agents, stable order over all B*K candidates.
   * dedupe / EOS / keep beam_width walk (:562-600) and final >= 5-word filter +
     selection (:619-667): host logic over the kernel's order, as in the reference.
+
+Decode state: bf16 models run engine.DecodeState (static per-stream K/V, the prefix
+shared by a prefix's beams through cs_prefix_attention, one captured hipGraph per
+step); other models the eager engine.BeamState.  With proposer="topk" on one rank the
+whole step after the host walk is ONE graph replay: parents' histories, the forward of
+the new tokens, the LM head, the reference rows' logit bias and the fused
+cs_beam_decode_step (proposer + agent scoring + welfare + stable order) — then one
+device->host copy of (ids, order, W, U) for the walk.
 Under torchrun over several ranks the agents are sharded (parallel.method_shard): each
 rank holds its agents' prefix K/V and beam streams (plus the reference prompt's), scores
 its agents, and the candidates' min welfare is an all-reduce(MIN) before the same stable
@@ -24,14 +32,52 @@ from __future__ import annotations
 import logging
 from typing import List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from .. import ops, parallel, runtime
-from ..engine import BeamState
+from ..engine import BeamState, DecodeState
 from .base import BaseGenerator
 from .prompts import BEAM, opinions_text
 
 logger = logging.getLogger(__name__)
+
+
+class _LiveBeams:
+    """DecodeState seen through the BeamState interface.  The state always holds
+    beam_width streams per prefix (n_beams); the first n_live are the reference's beams,
+    the rest padded copies whose candidates the loop drops.  The LM head runs once per
+    step over every stream (the shape the fast top-K step uses, so both loops see
+    bit-identical logits)."""
+
+    def __init__(self, st: DecodeState):
+        self.st = st
+        self.e = st.e
+        self.n_live = 1                   # step 0: every stream holds the prefix's last hidden
+        self._logits = None
+
+    @property
+    def n_beams(self) -> int:
+        return self.st.B
+
+    def _all(self) -> torch.Tensor:
+        if self._logits is None:
+            self._logits = self.e.model.lm_head(self.st.hidden)
+        return self._logits
+
+    def next_logits(self, prefix_idx: int) -> torch.Tensor:
+        B = self.st.B
+        return self._all()[prefix_idx * B:(prefix_idx + 1) * B]
+
+    def agent_logits(self, n_prefix: int) -> torch.Tensor:
+        return self._all()[:n_prefix * self.st.B]
+
+    def advance(self, parent, tokens) -> None:
+        n = len(parent)
+        pad = self.st.B - n
+        self.st.advance(list(parent) + [parent[0]] * pad, list(tokens) + [tokens[0]] * pad)
+        self.n_live = n
+        self._logits = None
 
 
 class BeamSearchGenerator(BaseGenerator):
@@ -57,10 +103,14 @@ class BeamSearchGenerator(BaseGenerator):
             self.bias_against_tokens.extend(c["additional_bias_tokens"])
         self.proposer = c.get("proposer", "sample")
         self.top_k = c.get("top_k", self.beam_width)
+        self.fused_decode = c.get("fused_decode", True)
+        self.fast_topk = c.get("fast_topk", True)
         self.step_log: List[dict] = []
+        self.decode_path = None
+        self.steps_run = 0
 
     # --- candidate proposal ------------------------------------------------------
-    def _propose(self, st: BeamState, ref_idx: int, bias: List[int], step_base_seed: Optional[int],
+    def _propose(self, st, ref_idx: int, bias: List[int], step_base_seed: Optional[int],
                  tok) -> List[List[int]]:
         logits = st.next_logits(ref_idx).float()
         if bias:
@@ -98,12 +148,35 @@ class BeamSearchGenerator(BaseGenerator):
             uniq.append(got)
         return uniq
 
+    # --- the reference's walk over the sorted candidates (beam_search.py:562-600) -------
+    def _walk(self, order, seq_of, tok_str_of, rewards_of, completed):
+        """order: candidate indices in (min reward desc, index asc) order.  Returns the new
+        beams [(seq, rewards)] and their candidate indices; EOS candidates go to
+        ``completed`` (every one of them, as in the reference, which walks all of them)."""
+        new_beams, new_idx, seen = [], [], set()
+        for i in order:
+            seq = seq_of(i)
+            if seq in seen:
+                continue
+            if tok_str_of(i) in self.LLAMA3_EOS_TOKENS:
+                completed.append((seq, rewards_of(i)))
+            elif len(new_beams) < self.beam_width:
+                new_beams.append((seq, rewards_of(i)))
+                new_idx.append(i)
+                seen.add(seq)
+        return new_beams, new_idx
+
     # --- main loop -----------------------------------------------------------------
     def generate_statement(self, issue: str, agent_opinions: dict) -> str:
         A = len(agent_opinions)
         if A == 0:
             return ""
         engine, tok = runtime.get_engine(self.model_identifier)
+        with runtime.device_lock(engine.device):
+            return self._generate(engine, tok, issue, agent_opinions)
+
+    def _generate(self, engine, tok, issue: str, agent_opinions: dict) -> str:
+        A = len(agent_opinions)
         shard = parallel.method_shard(A, self.config)
         ops_all = list(agent_opinions.values())
         agent_prefixes = [tok.chat_prefix(BEAM["agent_system"],
@@ -112,23 +185,48 @@ class BeamSearchGenerator(BaseGenerator):
         A_loc = len(agent_prefixes)      # this rank's agents (all of them on one rank)
         ref_user = BEAM["ref_user"].format(issue=issue, opinions_text=opinions_text(agent_opinions))
         ref_prefix = tok.render_raw(f"{BEAM['ref_system']}\n\n{ref_user}")
-        cache = engine.prefill(agent_prefixes + [ref_prefix])
-        st = BeamState(engine, cache, n_prefix=A_loc + 1)
+        all_prefixes = agent_prefixes + [ref_prefix]
+        cache = engine.prefill(all_prefixes)
         bias = (runtime.bias_token_ids(tok, self.bias_against_tokens)
                 if self.use_token_biasing and self.bias_against_tokens else [])
-        dev = engine.device
-
-        beams: List[Tuple[str, List[float]]] = [("", [0.0] * A_loc)]
-        rewards = torch.zeros(A_loc, 1, dtype=torch.float32, device=dev)   # cumulative, per beam
-        completed: List[Tuple[str, List[float]]] = []
+        max_ctx = max(len(p) for p in all_prefixes) + int(self.max_tokens)
+        fused = (self.fused_decode and int(self.max_tokens) > 0 and int(self.beam_width) > 0
+                 and engine.model.fused_ok(max_ctx))
         self.step_log = []
+        self.steps_run = 0
+        if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk:
+            self.decode_path = "fused-topk"
+            st = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
+                             max_steps=int(self.max_tokens))
+            completed, beams = self._loop_fused_topk(engine, tok, st, A_loc, bias)
+        else:
+            if fused:
+                self.decode_path = "fused"
+                st = _LiveBeams(DecodeState(engine, cache, n_prefix=A_loc + 1,
+                                            n_beams=int(self.beam_width),
+                                            max_steps=int(self.max_tokens)))
+            else:
+                self.decode_path = "eager"
+                st = BeamState(engine, cache, n_prefix=A_loc + 1)
+            completed, beams = self._loop(engine, tok, st, A, A_loc, shard, bias)
+        return self._final(completed, beams, engine.device, A_loc, shard)
+
+    def _loop(self, engine, tok, st, A, A_loc, shard, bias):
+        """Per-step proposals on the host (sample / top-k / sharded), cs_beam_step scoring."""
+        dev = engine.device
+        beams: List[Tuple[str, List[float]]] = [("", [0.0] * A_loc)]
+        rewards = torch.zeros(A_loc, st.n_beams, dtype=torch.float32, device=dev)   # per beam
+        completed: List[Tuple[str, List[float]]] = []
         for step in range(self.max_tokens):
             if not beams:
                 break
+            self.steps_run += 1
             step_base_seed = (self.seed + step * self.max_sampling_attempts * len(beams) * (A + 1)
                               if self.seed is not None else None)
+            n_live = getattr(st, "n_live", st.n_beams)
             props = parallel.same_on_all_ranks(self._propose(st, A_loc, bias, step_base_seed, tok),
                                                shard)
+            props = props[:n_live] + [[] for _ in range(st.n_beams - n_live)]   # padded beams
             cb, ct = [], []                           # candidate (beam, token id), insertion order
             for b, toks in enumerate(props):
                 for v in toks:
@@ -170,29 +268,113 @@ class BeamSearchGenerator(BaseGenerator):
                 W = parallel.combine_welfare(U, "min", shard)
                 order = ops.topk(W, len(slots))[0].cpu().tolist()
             Uh = U.double().cpu().numpy()
-            new_beams, new_idx, seen = [], [], set()
-            for i in order:
-                b, v = cb[i], ct[i]
-                s_tok = tok.token_str(v)
-                seq = beams[b][0] + s_tok
-                if seq in seen:
-                    continue
-                r = Uh[:, i].tolist()
-                if s_tok in self.LLAMA3_EOS_TOKENS:
-                    completed.append((seq, r))
-                elif len(new_beams) < self.beam_width:
-                    new_beams.append((seq, r))
-                    new_idx.append(i)
-                    seen.add(seq)
-            self.step_log.append({"candidates": [(beams[b][0] + tok.token_str(v)) for b, v in zip(cb, ct)],
-                                  "min_rewards": W.double().cpu().tolist(), "kept": [s for s, _ in new_beams]})
+            tstr = [tok.token_str(v) for v in ct]
+            new_beams, new_idx = self._walk(order, lambda i: beams[cb[i]][0] + tstr[i],
+                                            lambda i: tstr[i], lambda i: Uh[:, i].tolist(),
+                                            completed)
+            self.step_log.append({"candidates": [(beams[b][0] + s) for b, s in zip(cb, tstr)],
+                                  "min_rewards": W.double().cpu().tolist(),
+                                  "kept": [s for s, _ in new_beams]})
             beams = new_beams
             if not beams:
                 break
-            rewards = U[:, torch.as_tensor(new_idx, device=dev)].contiguous()
-            st.advance([cb[i] for i in new_idx], [ct[i] for i in new_idx])
+            if step + 1 < self.max_tokens:
+                st.advance([cb[i] for i in new_idx], [ct[i] for i in new_idx])
+                keep = new_idx + [new_idx[0]] * (st.n_beams - len(new_idx))   # padded beams
+                rewards = U[:, torch.as_tensor(keep, device=dev)].contiguous()
+        return completed, beams
 
-        completed.extend(beams)
+    def _loop_fused_topk(self, engine, tok, st: DecodeState, A: int, bias):
+        """Top-K proposer on one rank: after the host walk a decode step is ONE graph
+        replay ending in cs_beam_decode_step; one device->host copy per step."""
+        dev = engine.device
+        m = engine.model
+        B, K = st.B, int(self.top_k)
+        C = B * K
+        if K > m.cfg.vocab:
+            raise ValueError("top_k exceeds the vocabulary")
+        bias_t = torch.as_tensor(bias, dtype=torch.long, device=dev) if bias else None
+        bias_v = float(self.bias_value)
+        U_buf = torch.empty(A, C, dtype=torch.float32, device=dev)
+        W_buf = torch.empty(C, dtype=torch.float32, device=dev)
+        rewards = torch.zeros(A, B, dtype=torch.float32, device=dev)
+        kidx = torch.zeros(B, dtype=torch.long, device=dev)
+        ids_buf = torch.empty(B, K, dtype=torch.int32, device=dev)
+        order_buf = torch.empty(C, dtype=torch.int32, device=dev)
+        ws = ops.Workspace(zeroed=True)
+        # every output the host reads is a persistent buffer: the two captured step graphs
+        # (ping-pong parities) must write to the same storage
+
+        def score():
+            logits = m.lm_head(st.hidden)                                # [(A + 1) * B, V]
+            ref = logits[A * B:]
+            if bias_t is not None:
+                ref.index_add_(1, bias_t, torch.full((B, bias_t.numel()), bias_v, dtype=ref.dtype,
+                                                     device=dev))
+            ops.beam_decode_step(ref, logits[:A * B], rewards, K, "min", n_order=C,
+                                 softcap=engine.softcap, workspace=ws, out_U=U_buf, out_W=W_buf,
+                                 out_ids=ids_buf, out_order=order_buf)
+
+        def post():
+            torch.index_select(U_buf, 1, kidx, out=rewards)
+            score()
+
+        score()                                   # step 0 (eager): every beam = the prefix
+        host = _HostCopy()
+        beams: List[Tuple[str, List[float]]] = [("", [0.0] * A)]
+        n_live = 1
+        completed: List[Tuple[str, List[float]]] = []
+        for step in range(self.max_tokens):
+            self.steps_run += 1
+            ids_h, order_h, W_h, U_h = host.fetch(ids_buf, order_buf, W_buf, U_buf)
+            ids_f = ids_h.reshape(-1)
+            live = order_h[order_h < n_live * K]                          # beams b < n_live
+            tstr = {}
+
+            def ts(i):
+                s = tstr.get(i)
+                if s is None:
+                    s = tstr[i] = tok.token_str(int(ids_f[i]))
+                return s
+
+            new_beams, new_idx = self._walk_fast(live, beams, K, ts, U_h, completed)
+            self.step_log.append({"candidates": [beams[i // K][0] + ts(i) for i in range(n_live * K)],
+                                  "min_rewards": W_h[:n_live * K].astype(np.float64).tolist(),
+                                  "kept": [s for s, _ in new_beams]})
+            beams = new_beams
+            if not beams or step + 1 >= self.max_tokens:
+                break
+            n = len(new_idx)
+            kept = new_idx + [new_idx[0]] * (B - n)
+            kidx.copy_(torch.as_tensor(kept, dtype=torch.long).to(dev, non_blocking=True))
+            st.advance([i // K for i in kept], [int(ids_f[i]) for i in kept], post=post)
+            n_live = n
+        return completed, beams
+
+    def _walk_fast(self, order, beams, K, ts, U_h, completed):
+        """The reference walk (beam_search.py:562-600) over a full candidate order: once
+        beam_width beams are kept only EOS candidates still matter, and only they are
+        visited."""
+        new_beams, new_idx, seen = [], [], set()
+        eos = self.LLAMA3_EOS_TOKENS
+        for i in order.tolist():
+            s = ts(i)
+            is_eos = s in eos
+            if len(new_beams) >= self.beam_width and not is_eos:
+                continue
+            seq = beams[i // K][0] + s
+            if seq in seen:
+                continue
+            if is_eos:
+                completed.append((seq, U_h[:, i].astype(np.float64).tolist()))
+            else:
+                new_beams.append((seq, U_h[:, i].astype(np.float64).tolist()))
+                new_idx.append(i)
+                seen.add(seq)
+        return new_beams, new_idx
+
+    def _final(self, completed, beams, dev, A_loc, shard) -> str:
+        completed = completed + beams
         if not completed:
             return ""
         pool = [(s, r) for s, r in completed if len(s.strip().split()) >= 5] or completed
@@ -206,3 +388,21 @@ class BeamSearchGenerator(BaseGenerator):
             logger.warning("brushup (a remote LLM rewrite of the ending) is not part of the "
                            "local scoring path; returning the statement unchanged")
         return final
+
+
+class _HostCopy:
+    """Device -> pinned host copies of several tensors, ONE stream synchronisation."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def fetch(self, *ts):
+        outs = []
+        for j, t in enumerate(ts):
+            b = self.bufs.get(j)
+            if b is None or b.shape != t.shape or b.dtype != t.dtype:
+                b = self.bufs[j] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            b.copy_(t, non_blocking=True)
+            outs.append(b)
+        torch.cuda.current_stream().synchronize()
+        return [o.numpy() for o in outs]

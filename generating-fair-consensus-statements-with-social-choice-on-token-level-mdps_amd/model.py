@@ -196,7 +196,13 @@ class Model:
     def _embed(self, ids: torch.Tensor) -> torch.Tensor:
         h = self.w["embed"][ids]
         if self.cfg.family == "gemma2":
-            h = h * torch.tensor(self.cfg.d_model ** 0.5, dtype=h.dtype, device=h.device)
+            # the normalizer in the activation dtype, made once (no host copy inside a
+            # captured decode step)
+            sc = getattr(self, "_emb_scale", None)
+            if sc is None or sc.dtype != h.dtype:
+                sc = self._emb_scale = torch.tensor(self.cfg.d_model ** 0.5, dtype=h.dtype,
+                                                    device=h.device)
+            h = h * sc
         return h
 
     def _mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
@@ -352,6 +358,60 @@ class Model:
     def lm_head(self, h: torch.Tensor) -> torch.Tensor:
         W = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
         return h.to(W.dtype) @ W.t()
+
+    # --- stream forward over shared prefixes (HIP attention) ----------------------
+    def attn_scale(self) -> float:
+        c = self.cfg
+        return (c.query_pre_attn_scalar ** -0.5) if c.query_pre_attn_scalar else c.head_dim ** -0.5
+
+    def fused_ok(self, max_ctx: int = 0) -> bool:
+        """Whether forward_streams (cs_rope_place + cs_prefix_attention) serves this model:
+        bf16 weights on a HIP device, head_dim in {64, 128, 256}, and every context within
+        Gemma-2's sliding window (the kernel attends the whole visible range)."""
+        c = self.cfg
+        return (self.device.type == "cuda" and self.dtype == torch.bfloat16
+                and c.head_dim in (64, 128, 256) and c.n_heads % c.n_kv_heads == 0
+                and (not c.sliding_window or max_ctx <= c.sliding_window))
+
+    @torch.no_grad()
+    def forward_streams(self, tokens: torch.Tensor, pfx, hist_k: List[torch.Tensor],
+                        hist_vt: List[torch.Tensor], hist_base: torch.Tensor, n_str: int, T: int,
+                        group_prefix: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """T new tokens for each of S = n_groups * n_str streams (tokens [S*T], stream-major):
+        stream s = i * n_str + b attends to its group's prefix (pfx.k / pfx.vt / pfx.lengths,
+        the layouts of include/consensus_scoring.h cs_prefix_attention; group i uses prefix
+        group_prefix[i] or i) and to its own history slots [0, hist_base + t] in
+        hist_k[layer] [S, Hkv, ldh, D] / hist_vt[layer] [S, Hkv, D, ldh]; the new tokens'
+        K / V are written to slots hist_base + t.  Per layer: one fused q|k|v GEMM,
+        cs_rope_place, cs_prefix_attention, output GEMM, MLP.  No host synchronisation and
+        no shape depends on hist_base: a decode step is graph-capturable.  Returns the
+        final-norm hidden [S*T, d]."""
+        from . import ops   # local: model.py stays importable without the library
+        c = self.cfg
+        H, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
+        n_tok = tokens.shape[0]
+        scale = self.attn_scale()
+        h = self._embed(tokens)
+        for i in range(c.n_layers):
+            p = f"l{i}."
+            x = self._rms(h, self.w[p + "attn_norm"])
+            qkv = x @ self.wf[p + "qkv"].t()
+            q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
+            ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
+                           hist_k[i], hist_vt[i], group_prefix=group_prefix)
+            o = ops.prefix_attention(q, pfx.k[i], pfx.vt[i], pfx.lengths, hist_k[i], hist_vt[i],
+                                     hist_base, n_str, T, scale=scale, softcap=c.attn_softcap,
+                                     group_prefix=group_prefix)
+            o = o.view(n_tok, H * D) @ self.w[p + "wo"].t()
+            if c.family == "gemma2":
+                o = self._rms(o, self.w[p + "post_attn_norm"])
+            h = h + o
+            x = self._rms(h, self.w[p + "mlp_norm"])
+            y = self._mlp(i, x)
+            if c.family == "gemma2":
+                y = self._rms(y, self.w[p + "post_mlp_norm"])
+            h = h + y
+        return self._rms(h, self.w["norm"])
 
 
 def hf_state_dict(model: Model) -> Dict[str, torch.Tensor]:

@@ -313,7 +313,9 @@ def beam_decode_step(ref_logits: torch.Tensor, logits: torch.Tensor, rewards: to
                      vocab: Optional[int] = None, softcap: float = 0.0, eps: float = 1e-9,
                      workspace: Optional[Workspace] = None,
                      kept_out: Optional[torch.Tensor] = None,
-                     out_U: Optional[torch.Tensor] = None, out_W: Optional[torch.Tensor] = None):
+                     out_U: Optional[torch.Tensor] = None, out_W: Optional[torch.Tensor] = None,
+                     out_ids: Optional[torch.Tensor] = None,
+                     out_order: Optional[torch.Tensor] = None):
     """Proposer + scoring of one beam decode step in ONE launch (cs_beam_decode_step).
 
     ref_logits [B, ld_ref] reference-policy rows; logits [A*B, ld] agent rows (row a*B+b);
@@ -332,20 +334,25 @@ def beam_decode_step(ref_logits: torch.Tensor, logits: torch.Tensor, rewards: to
     A, B = rewards.shape
     if B_ref != B or rows != A * B:
         raise CSError(f"shape mismatch: ref rows {B_ref}, agent rows {rows}, rewards {tuple(rewards.shape)}")
-    _require_cuda(ref_logits, logits, rewards)
+    _require_cuda(ref_logits, logits, rewards, out_ids, out_order)
     if isinstance(kind, str):
         kind = WELFARE[kind]
     k = int(k)
     C = B * k
     n_order = C if n_order is None else int(n_order)
     dev = logits.device
-    ids = torch.empty((B, k), dtype=torch.int32, device=dev)
+    ids = torch.empty((B, k), dtype=torch.int32, device=dev) if out_ids is None else out_ids
+    if ids.shape != (B, k) or ids.dtype != torch.int32 or not ids.is_contiguous():
+        raise CSError(f"out_ids must be a contiguous int32 [{B}, {k}] tensor")
     U = torch.empty((A, C), dtype=torch.float32, device=dev) if out_U is None else out_U
     W = torch.empty(C, dtype=torch.float32, device=dev) if out_W is None else out_W
     if (U.shape != (A, C) or W.shape != (C,) or U.dtype != torch.float32 or
             W.dtype != torch.float32 or not U.is_contiguous() or not W.is_contiguous()):
         raise CSError(f"out_U / out_W must be contiguous float32 [{A}, {C}] / [{C}]")
-    order = torch.empty(max(n_order, 0), dtype=torch.int32, device=dev)
+    order = (torch.empty(max(n_order, 0), dtype=torch.int32, device=dev) if out_order is None
+             else out_order)
+    if order.shape != (max(n_order, 0),) or order.dtype != torch.int32 or not order.is_contiguous():
+        raise CSError(f"out_order must be a contiguous int32 [{n_order}] tensor")
     oval = torch.empty(max(n_order, 0), dtype=torch.float32, device=dev)
     nbytes = int(L.cs_beam_decode_workspace_size(A, B, vocab, k))
     if workspace is None:
@@ -431,3 +438,89 @@ def vocab_sample(logits: torch.Tensor, seeds: torch.Tensor, *, temperature: floa
                            ws.numel() if ws is not None else 0, _stream())
     _lib.check(rc, "cs_vocab_sample")
     return ids, lp
+
+
+_attn_ws: dict = {}
+
+
+def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.Tensor,
+                     prefix_len: torch.Tensor, k_hist: torch.Tensor, vt_hist: torch.Tensor,
+                     hist_base: torch.Tensor, n_str: int, T: int, *, scale: float,
+                     softcap: float = 0.0, group_prefix: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None, workspace: Optional[Workspace] = None):
+    """Cascade attention of candidate streams over shared per-agent prefix K/V
+    (cs_prefix_attention; layouts in include/consensus_scoring.h).
+
+    q [n_groups*n_str*T, H, D] bf16; k_prefix [n_prefix, Hkv, ldp, D], vt_prefix
+    [n_prefix, Hkv, D, ldp]; prefix_len [n_prefix] int32; k_hist [S, Hkv, ldh, D], vt_hist
+    [S, Hkv, D, ldh] (S = n_groups*n_str); hist_base [1] int32 (device).  Returns out
+    [n_tok, H, D] bf16.  Replaces the per-call prompt re-encoding of src/utils.py:249-259."""
+    L = _lib.load()
+    if q.dim() != 3 or q.dtype != torch.bfloat16 or not q.is_contiguous():
+        raise CSError("q must be a contiguous [n_tok, H, D] bfloat16 tensor")
+    n_tok, H, D = q.shape
+    n_prefix, Hkv, ldp, Dk = k_prefix.shape
+    S, Hkv2, ldh, Dh = k_hist.shape
+    if Dk != D or Dh != D or Hkv2 != Hkv:
+        raise CSError("head layout mismatch between q, k_prefix and k_hist")
+    if tuple(vt_prefix.shape) != (n_prefix, Hkv, D, ldp) or tuple(vt_hist.shape) != (S, Hkv, D, ldh):
+        raise CSError("vt_prefix / vt_hist must be the transposed [.., Hkv, D, ld] layouts")
+    for t in (k_prefix, vt_prefix, k_hist, vt_hist):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise CSError("K/V buffers must be contiguous bfloat16")
+    if n_str <= 0 or T <= 0 or S % n_str != 0 or n_tok != S * T:
+        raise CSError(f"n_tok {n_tok} != streams {S} x T {T} (n_str {n_str})")
+    n_groups = S // n_str
+    if group_prefix is None and n_groups != n_prefix:
+        raise CSError("n_groups must equal n_prefix without group_prefix")
+    if group_prefix is not None and (group_prefix.dtype != torch.int32 or group_prefix.numel() != n_groups):
+        raise CSError("group_prefix must be int32 [n_groups]")
+    if prefix_len.dtype != torch.int32 or prefix_len.numel() != n_prefix:
+        raise CSError("prefix_len must be int32 [n_prefix]")
+    if hist_base.dtype != torch.int32 or hist_base.numel() != 1:
+        raise CSError("hist_base must be a one-element int32 device tensor")
+    _require_cuda(q, k_prefix, vt_prefix, prefix_len, k_hist, vt_hist, hist_base, group_prefix, out)
+    if out is None:
+        out = torch.empty_like(q)
+    nbytes = int(L.cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, ldp))
+    if workspace is None:
+        workspace = _attn_ws.setdefault(q.device, Workspace())
+    ws = workspace.get(nbytes, q.device)
+    rc = L.cs_prefix_attention(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), ldp,
+                               prefix_len.data_ptr(),
+                               group_prefix.data_ptr() if group_prefix is not None else None,
+                               n_groups, k_hist.data_ptr(), vt_hist.data_ptr(), ldh,
+                               hist_base.data_ptr(), n_str, T, H, Hkv, D, float(scale),
+                               float(softcap), out.data_ptr(),
+                               ws.data_ptr() if ws is not None else None,
+                               ws.numel() if ws is not None else 0, _stream())
+    _lib.check(rc, "cs_prefix_attention")
+    return out
+
+
+def rope_place(qkv: torch.Tensor, inv_freq: torch.Tensor, prefix_len: torch.Tensor,
+               hist_base: torch.Tensor, n_str: int, T: int, H: int, Hkv: int, D: int,
+               q_out: torch.Tensor, k_hist: torch.Tensor, vt_hist: torch.Tensor, *,
+               group_prefix: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """RoPE of the fused projection + placement of q / the new K, V (cs_rope_place)."""
+    L = _lib.load()
+    if qkv.dim() != 2 or qkv.dtype != torch.bfloat16 or qkv.stride(1) != 1:
+        raise CSError("qkv must be a 2-D bfloat16 tensor with unit column stride")
+    n_tok = qkv.shape[0]
+    S, Hkv2, ldh, Dk = k_hist.shape
+    if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != (S, Hkv, D, ldh):
+        raise CSError("k_hist / vt_hist layout mismatch")
+    if n_tok != S * T or S % n_str != 0:
+        raise CSError("qkv rows must be streams x T")
+    if tuple(q_out.shape) != (n_tok, H, D) or q_out.dtype != torch.bfloat16 or not q_out.is_contiguous():
+        raise CSError("q_out must be a contiguous [n_tok, H, D] bfloat16 tensor")
+    if inv_freq.dtype != torch.float32 or inv_freq.numel() != D // 2:
+        raise CSError("inv_freq must be float32 [D/2]")
+    _require_cuda(qkv, inv_freq, prefix_len, hist_base, q_out, k_hist, vt_hist, group_prefix)
+    ld = qkv.stride(0) if n_tok > 1 else qkv.shape[1]
+    rc = L.cs_rope_place(qkv.data_ptr(), ld, inv_freq.data_ptr(), prefix_len.data_ptr(),
+                         group_prefix.data_ptr() if group_prefix is not None else None,
+                         S // n_str, hist_base.data_ptr(), n_str, T, H, Hkv, D, q_out.data_ptr(),
+                         k_hist.data_ptr(), vt_hist.data_ptr(), ldh, _stream())
+    _lib.check(rc, "cs_rope_place")
+    return q_out

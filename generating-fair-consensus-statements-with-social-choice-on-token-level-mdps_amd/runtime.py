@@ -3,9 +3,21 @@
 The reference resolves a model identifier (e.g. "meta-llama/Meta-Llama-3.1-8B-Instruct-Turbo")
 to a remote endpoint through the module-global Together ``client`` (src/utils.py:69-74).
 Here the identifier resolves to a local ``ScoringEngine`` on the current HIP device:
-either one registered explicitly (``register_engine``; tests register the parity
-fixture model this way) or an architecture-exact, random-initialised model built
-from the preset whose name the identifier mentions (no checkpoints offline).
+  * one registered explicitly (``register_engine``; tests register the parity fixture
+    model this way);
+  * a local Hugging Face checkpoint directory (config.json + *.safetensors +
+    tokenizer.json): the identifier itself when it is a directory, or
+    ``$CS_MODEL_ROOT/<identifier>`` (``register_model_dir`` maps an id to a directory);
+  * ``random:<preset>`` (e.g. ``random:llama-3.1-8b``): an architecture-exact,
+    random-initialised bf16 model with a full-vocabulary synthetic tokenizer — for
+    throughput benchmarks only, the statements it produces mean nothing.
+A real model id with none of these raises: random weights are never substituted
+silently (set CS_ALLOW_RANDOM_INIT=1 to get the random-init model with a warning).
+
+Concurrency: the reference runs generators in threads against one process
+(src/experiment.py:283-322).  Everything that launches work on a device takes
+``device_lock(device)`` (re-entrant), so forward passes and the kernels' shared
+workspaces are used by one thread at a time per device.
 
 Seed semantics of the local samplers (the replacement for the remote API's
 ``seed`` argument) are defined here once and restated by the test fake client:
@@ -15,6 +27,7 @@ Seed semantics of the local samplers (the replacement for the remote API's
 """
 from __future__ import annotations
 
+import logging
 import os
 import re
 import threading
@@ -30,6 +43,9 @@ from .tokenizer import CharTokenizer
 _M64 = (1 << 64) - 1
 _lock = threading.RLock()
 _ENGINES: Dict[str, Tuple[ScoringEngine, CharTokenizer]] = {}
+_MODEL_DIRS: Dict[str, str] = {}
+_DEVICE_LOCKS: Dict[str, threading.RLock] = {}
+logger = logging.getLogger(__name__)
 
 _NAME_TO_PRESET = [
     (r"3\.3-70b|llama-3\.3-70b|70b", "llama-3.3-70b"),
@@ -56,9 +72,36 @@ def fresh_seed() -> int:
     return int.from_bytes(os.urandom(8), "little")
 
 
+def device_lock(device) -> threading.RLock:
+    """The re-entrant lock serialising work on one device (forward passes, workspaces)."""
+    key = str(torch.device(device))
+    with _lock:
+        lk = _DEVICE_LOCKS.get(key)
+        if lk is None:
+            lk = _DEVICE_LOCKS[key] = threading.RLock()
+        return lk
+
+
 def register_engine(model_identifier: str, engine: ScoringEngine, tokenizer: CharTokenizer) -> None:
     with _lock:
         _ENGINES[model_identifier] = (engine, tokenizer)
+
+
+def register_model_dir(model_identifier: str, path: str) -> None:
+    """Serve ``model_identifier`` from a local checkpoint directory (loaded on first use)."""
+    with _lock:
+        _MODEL_DIRS[model_identifier] = path
+
+
+def random_engine(preset_name: str, device=None, dtype=torch.bfloat16, seed: int = 0,
+                  **engine_kw) -> Tuple[ScoringEngine, CharTokenizer]:
+    """Architecture-exact random-init model + full-vocabulary synthetic tokenizer."""
+    cfg = preset(preset_name)
+    dev = torch.device(device) if device is not None else \
+        torch.device("cuda", torch.cuda.current_device())
+    model = Model(cfg, dev, dtype, seed=seed)
+    tok = CharTokenizer("gemma2" if cfg.family == "gemma2" else "llama3", vocab_size=cfg.vocab)
+    return ScoringEngine(model, **engine_kw), tok
 
 
 def clear_engines() -> None:
@@ -74,17 +117,44 @@ def resolve_preset(model_identifier: str) -> str:
     raise ValueError(f"no local architecture known for model identifier {model_identifier!r}")
 
 
+def _model_dir(model_identifier: str) -> Optional[str]:
+    if model_identifier in _MODEL_DIRS:
+        return _MODEL_DIRS[model_identifier]
+    if os.path.isdir(model_identifier) and os.path.exists(os.path.join(model_identifier, "config.json")):
+        return model_identifier
+    root = os.environ.get("CS_MODEL_ROOT")
+    if root:
+        cand = os.path.join(root, model_identifier)
+        if os.path.exists(os.path.join(cand, "config.json")):
+            return cand
+    return None
+
+
 def get_engine(model_identifier: str) -> Tuple[ScoringEngine, CharTokenizer]:
     with _lock:
         if model_identifier in _ENGINES:
             return _ENGINES[model_identifier]
         if not torch.cuda.is_available():
             raise ops.CSError("no HIP device: the scoring engine has no CPU path")
-        cfg = preset(resolve_preset(model_identifier))
-        dev = torch.device("cuda", torch.cuda.current_device())
-        model = Model(cfg, dev, torch.bfloat16, seed=0)
-        tok = CharTokenizer("gemma2" if cfg.family == "gemma2" else "llama3")
-        ent = (ScoringEngine(model), tok)
+        path = _model_dir(model_identifier)
+        if path is not None:
+            from .checkpoint import load_engine
+            ent = load_engine(path)
+        elif model_identifier.startswith("random:"):
+            ent = random_engine(model_identifier.split(":", 1)[1])
+        elif os.environ.get("CS_ALLOW_RANDOM_INIT") == "1":
+            name = resolve_preset(model_identifier)
+            logger.warning("model %r: no checkpoint found; using RANDOM-INIT %s weights "
+                           "(CS_ALLOW_RANDOM_INIT=1) -- statements will be meaningless",
+                           model_identifier, name)
+            ent = random_engine(name)
+        else:
+            raise ops.CSError(
+                f"no weights for model {model_identifier!r}: register an engine "
+                "(runtime.register_engine), give a local checkpoint directory (config.json, "
+                "*.safetensors, tokenizer.json) as the id, via runtime.register_model_dir or "
+                "under $CS_MODEL_ROOT, or use 'random:<preset>' for an architecture-exact "
+                "random-init benchmark model")
         _ENGINES[model_identifier] = ent
         return ent
 

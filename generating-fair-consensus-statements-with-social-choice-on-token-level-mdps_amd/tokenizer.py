@@ -25,10 +25,21 @@ EXTRA_CHARS = ["\u200b", "\u2018", "\u2019", "\u201c", "\u201d", "\u2013", "\u20
 UNK = "\ufffd"
 
 
-class CharTokenizer:
-    """Deterministic char tokenizer: specials, Latin-1, a few extra code points, <unk>."""
+# ids past the character table map to single code points from here on (planes 1-4 are
+# outside every text the prompts contain and hold no surrogates), so a full-vocabulary
+# tokenizer stays merge-free: every id is one distinct character
+SYNTH_BASE = 0x10000
 
-    def __init__(self, family: str = "llama3") -> None:
+
+class CharTokenizer:
+    """Deterministic char tokenizer: specials, Latin-1, a few extra code points, <unk>.
+
+    ``vocab_size`` > the character table (e.g. the model's 128,256 or 256,000) gives every
+    further id a distinct single synthetic character (chr(SYNTH_BASE + id)), for
+    random-initialised benchmark models whose proposals range over the whole vocabulary:
+    candidates stay distinct strings and encode(decode(ids)) == ids still holds."""
+
+    def __init__(self, family: str = "llama3", vocab_size: int = 0) -> None:
         self.family = family
         specials = LLAMA3_SPECIALS + GEMMA2_SPECIALS
         self.id_to_str: List[str] = list(specials)
@@ -51,18 +62,21 @@ class CharTokenizer:
         self.eos_id = self.special_ids[self.eos]
         self.eos_ids = tuple(self.special_ids[s] for s in self.eos_strings)
         self._specials_by_len = sorted(specials, key=len, reverse=True)
+        self.n_table = len(self.id_to_str)
+        self.full_vocab = max(int(vocab_size), self.n_table)
 
     @property
     def vocab_size(self) -> int:
-        return len(self.id_to_str)
+        return self.full_vocab
 
     # --- plain text ---------------------------------------------------------------
     def encode(self, text: str) -> List[int]:
         """Characters -> ids; special-token strings in the text map to their special id
         (so a sampled special token survives the reference's string round trip)."""
         cid = self.char_to_id
+        get = cid.get if self.full_vocab == self.n_table else self._char_id
         if "<" not in text:
-            return [cid.get(c, self.unk_id) for c in text]
+            return [get(c, self.unk_id) for c in text]
         out: List[int] = []
         i, n = 0, len(text)
         specials = self._specials_by_len
@@ -75,19 +89,27 @@ class CharTokenizer:
                         i += len(sp)
                         break
                 else:
-                    out.append(cid.get(c, self.unk_id))
+                    out.append(get(c, self.unk_id))
                     i += 1
             else:
-                out.append(cid.get(c, self.unk_id))
+                out.append(get(c, self.unk_id))
                 i += 1
         return out
 
+    def _char_id(self, c: str, default: int) -> int:
+        i = self.char_to_id.get(c)
+        if i is not None:
+            return i
+        j = ord(c) - SYNTH_BASE
+        return j if self.n_table <= j < self.full_vocab else default
+
     def decode(self, ids: Iterable[int]) -> str:
-        n = len(self.id_to_str)
-        return "".join(self.id_to_str[i] if 0 <= i < n else UNK for i in ids)
+        return "".join(self.token_str(i) for i in ids)
 
     def token_str(self, i: int) -> str:
-        return self.id_to_str[i] if 0 <= i < len(self.id_to_str) else UNK
+        if 0 <= i < self.n_table:
+            return self.id_to_str[i]
+        return chr(SYNTH_BASE + i) if self.n_table <= i < self.full_vocab else UNK
 
     def tokens(self, ids: Sequence[int]) -> List[str]:
         return [self.token_str(i) for i in ids]

@@ -262,6 +262,57 @@ int cs_vocab_sample(const void* logits, int dtype, int64_t rows, int64_t vocab, 
                     int32_t* out_ids, float* out_lp, void* workspace, size_t workspace_bytes,
                     cs_stream_t stream);
 
+/*
+ * cs_prefix_attention — cascade attention of many candidate streams over SHARED
+ * per-agent prefix K/V (bf16 in / bf16 out, fp32 online softmax, bf16 MFMA).
+ *
+ * n_groups groups of n_str streams each; group i uses prefix group_prefix[i] (NULL =
+ * identity).  Stream s = i*n_str + b carries T query tokens; token t of stream s is
+ * q[(s*T + t)][H][D] and sees
+ *     prefix keys  [0, prefix_len[pfx])       k_prefix [n_prefix][Hkv][ld_prefix][D],
+ *                                             vt_prefix [n_prefix][Hkv][D][ld_prefix]
+ *     its history  [0, *hist_base + t]        k_hist  [S][Hkv][ld_hist][D],
+ *                                             vt_hist [S][Hkv][D][ld_hist]
+ * (V transposed: key-contiguous rows; ld_prefix, ld_hist multiples of 32; key slots past
+ * the visible range must hold finite values).  out [(s*T + t)][H][D].  Query head h uses
+ * K/V head h / (H / Hkv).  scores = q.k * scale, then softcap * tanh(./softcap) when
+ * softcap > 0 (Gemma-2 attention soft-cap), softmax over the visible keys.  D in
+ * {64, 128, 256}.  hist_base lives in device memory so that a captured decode step
+ * replays with a growing history.  One workgroup holds all query rows of (group, K/V
+ * head) (64 per workgroup), so a prefix key block is read once for every candidate of
+ * that agent.  Workspace: cs_prefix_attention_workspace_size() bytes (0 = none needed);
+ * results are deterministic (fixed-order split merge).
+ *
+ * Replaces: the per-(agent, candidate) re-encoding of the agent's whole prompt behind
+ *   every get_prompt_logprobs call (src/utils.py:249-259; driven per candidate at
+ *   src/methods/beam_search.py:495-538, best_of_n.py:266-321,
+ *   finite_lookahead.py:464-524, src/evaluation.py:177-230).
+ */
+size_t cs_prefix_attention_workspace_size(int32_t n_groups, int32_t n_str, int32_t T, int32_t H,
+                                          int32_t Hkv, int32_t D, int64_t ld_prefix);
+int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
+                        int64_t ld_prefix, const int32_t* prefix_len, const int32_t* group_prefix,
+                        int32_t n_groups, const void* k_hist, const void* vt_hist, int64_t ld_hist,
+                        const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
+                        int32_t D, float scale, float softcap, void* out, void* workspace,
+                        size_t workspace_bytes, cs_stream_t stream);
+
+/*
+ * cs_rope_place — rotary embedding (half-rotation convention, angle = position *
+ * inv_freq[i]) of the fused projection qkv [(s*T + t)][ld_qkv] = [q (H*D) | k (Hkv*D) |
+ * v (Hkv*D)] and placement into the cs_prefix_attention layouts: q_out [(s*T+t)][H][D],
+ * k_hist[s][g][*hist_base + t][:] (rotated), vt_hist[s][g][:][*hist_base + t].  The
+ * position of token t of stream s (group i) is prefix_len[group_prefix[i]] + *hist_base + t.
+ * bf16 in / out, fp32 rotation.
+ *
+ * Replaces: the per-call re-encoding of the reference's prompts (src/utils.py:249-259):
+ *   a candidate token's K/V is computed once and kept for every later step of its stream.
+ */
+int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const int32_t* prefix_len,
+                  const int32_t* group_prefix, int32_t n_groups, const int32_t* hist_base,
+                  int32_t n_str, int32_t T, int32_t H, int32_t Hkv, int32_t D, void* q_out,
+                  void* k_hist, void* vt_hist, int64_t ld_hist, cs_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,252 @@
+"""GPU numerics of the stream-decode kernels (cs_prefix_attention, cs_rope_place) and of
+the engine paths built on them, against plain PyTorch fp32 references of the same ops.
+
+cs_prefix_attention is bf16 in / bf16 out with fp32 softmax and a bf16 P for the P.V
+MFMA, so it is held to bf16 tolerance against an fp32 attention over the SAME bf16
+inputs (|err| <= 2e-2 + 2e-2 |ref|; measured errors are ~4e-3).  The engine-level tests
+compare the fused decode (forward_streams / DecodeState) with the eager SDPA path of the
+same bf16 model: token log-probs within 3e-2 (both paths round activations to bf16 at
+different points), and graph replay against eager execution of the fused path bit for
+bit."""
+import importlib
+import math
+import zlib
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+
+
+def _ceil32(n):
+    return max(32, (n + 31) // 32 * 32)
+
+
+def ref_attention(q, kp, vp, plen, kh, vh, hist_base, n_str, T, scale, softcap, gpfx=None):
+    """fp32 reference.  q [n_tok, H, D]; kp/vp [n_prefix, Hkv, ldp, D]; kh/vh [S, Hkv, ldh, D]."""
+    n_tok, H, D = q.shape
+    S, Hkv = kh.shape[0], kh.shape[1]
+    rep = H // Hkv
+    out = torch.zeros(n_tok, H, D, dtype=torch.float32, device=q.device)
+    qf, kpf, vpf, khf, vhf = (x.float() for x in (q, kp, vp, kh, vh))
+    for s in range(S):
+        gi = s // n_str
+        p = int(gpfx[gi]) if gpfx is not None else gi
+        P = int(plen[p])
+        for t in range(T):
+            n_h = hist_base + t + 1
+            K = torch.cat([kpf[p, :, :P], khf[s, :, :n_h]], dim=1)       # [Hkv, n, D]
+            Vv = torch.cat([vpf[p, :, :P], vhf[s, :, :n_h]], dim=1)
+            qq = qf[s * T + t].view(Hkv, rep, D)
+            sc = torch.einsum("grd,gnd->grn", qq, K) * scale
+            if softcap > 0:
+                sc = softcap * torch.tanh(sc / softcap)
+            pr = torch.softmax(sc, dim=-1)
+            out[s * T + t] = torch.einsum("grn,gnd->grd", pr, Vv).reshape(H, D)
+    return out
+
+
+CASES = [
+    # n_prefix, n_str, T, H, Hkv, D, plens, hist_base, softcap, group map
+    (5, 4, 1, 32, 8, 64, [180, 201, 77, 160, 230], 3, 0.0, None),      # C1-like decode (1B)
+    (3, 16, 1, 16, 8, 256, [90, 140, 33], 20, 50.0, None),             # C3-like (Gemma-2, cap)
+    (4, 8, 1, 64, 8, 128, [300, 12, 64, 250], 47, 0.0, None),          # C5-like (70B, rep 8)
+    (2, 6, 37, 32, 8, 128, [45, 96], 0, 0.0, None),                    # scoring chunk (T > 1)
+    (3, 2, 5, 8, 2, 64, [40, 64, 1], 2, 0.0, [2, 0, 0]),               # group -> prefix map
+    (1, 64, 1, 32, 8, 128, [400], 9, 0.0, None),                       # one prefix, 64 streams
+    (2, 3, 1, 4, 4, 64, [31, 33], 0, 0.0, None),                       # rep 1, first step
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_prefix_attention_matches_fp32_reference(ops, dev, case):
+    n_prefix, n_str, T, H, Hkv, D, plens, hb, cap, gmap = case
+    g = torch.Generator(device="cpu").manual_seed(zlib.crc32(repr(case).encode()))
+    n_grp = len(gmap) if gmap is not None else n_prefix
+    S = n_grp * n_str
+    ldp = _ceil32(max(plens))
+    ldh = _ceil32(hb + T)
+    bf = torch.bfloat16
+
+    def rnd(*shape, s=1.0):
+        return (torch.randn(*shape, generator=g) * s).to(bf).to(dev)
+
+    q = rnd(S * T, H, D, s=1.0)
+    kp, vp = rnd(n_prefix, Hkv, ldp, D), rnd(n_prefix, Hkv, ldp, D)
+    kh, vh = rnd(S, Hkv, ldh, D), rnd(S, Hkv, ldh, D)
+    plen = torch.tensor(plens, dtype=torch.int32, device=dev)
+    hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
+    gp = torch.tensor(gmap, dtype=torch.int32, device=dev) if gmap is not None else None
+    scale = D ** -0.5 * (4.0 if cap else 1.0)      # the cap case drives scores into the cap
+    out = ops.prefix_attention(q, kp, vp.transpose(2, 3).contiguous(), plen, kh,
+                               vh.transpose(2, 3).contiguous(), hbt, n_str, T, scale=scale,
+                               softcap=cap, group_prefix=gp)
+    torch.cuda.synchronize()
+    ref = ref_attention(q, kp, vp, plens, kh, vh, hb, n_str, T, scale, cap, gmap)
+    err = (out.float() - ref).abs()
+    bound = 2e-2 + 2e-2 * ref.abs()
+    assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}"
+    # deterministic: a second launch is bit-identical
+    out2 = ops.prefix_attention(q, kp, vp.transpose(2, 3).contiguous(), plen, kh,
+                                vh.transpose(2, 3).contiguous(), hbt, n_str, T, scale=scale,
+                                softcap=cap, group_prefix=gp)
+    assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("D,H,Hkv,T", [(64, 8, 2, 3), (128, 32, 8, 1), (256, 16, 8, 2)])
+def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
+    M = importlib.import_module(PKG + ".model")
+    cfg = M.preset("tiny-llama", head_dim=D, n_heads=H, n_kv_heads=Hkv)
+    inv = M.rope_inv_freq(cfg, dev)
+    g = torch.Generator(device="cpu").manual_seed(D + H)
+    n_prefix, n_str = 3, 2
+    S = n_prefix * n_str
+    plens = [17, 250, 1000]
+    hb = 5
+    ldh = _ceil32(hb + T)
+    qkv = torch.randn(S * T, (H + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    plen = torch.tensor(plens, dtype=torch.int32, device=dev)
+    hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
+    q_out = torch.empty(S * T, H, D, dtype=torch.bfloat16, device=dev)
+    kh = torch.zeros(S, Hkv, ldh, D, dtype=torch.bfloat16, device=dev)
+    vth = torch.zeros(S, Hkv, D, ldh, dtype=torch.bfloat16, device=dev)
+    ops.rope_place(qkv, inv, plen, hbt, n_str, T, H, Hkv, D, q_out, kh, vth)
+    torch.cuda.synchronize()
+    # fp32 reference rotation
+    pos = torch.tensor([plens[s // n_str] + hb + t for s in range(S) for t in range(T)],
+                       dtype=torch.float32, device=dev)
+    ang = pos[:, None] * inv[None]
+    cos, sin = ang.cos(), ang.sin()
+    x = qkv.float().view(S * T, H + 2 * Hkv, D)
+    x1, x2 = x[..., :D // 2], x[..., D // 2:]
+    rot = torch.cat([x1 * cos[:, None] - x2 * sin[:, None], x2 * cos[:, None] + x1 * sin[:, None]], -1)
+    torch.testing.assert_close(q_out.float(), rot[:, :H], atol=2e-2, rtol=1e-2)
+    for s in range(S):
+        for t in range(T):
+            tok = s * T + t
+            torch.testing.assert_close(kh[s, :, hb + t].float(), rot[tok, H:H + Hkv], atol=2e-2, rtol=1e-2)
+            assert torch.equal(vth[s, :, :, hb + t], qkv[tok].view(-1, D)[H + Hkv:])
+    assert kh[:, :, :hb].abs().sum() == 0 and vth[..., hb + T:].abs().sum() == 0
+
+
+def _tiny(family, dev, seed=3, dtype=torch.bfloat16, weights=None):
+    M = importlib.import_module(PKG + ".model")
+    E = importlib.import_module(PKG + ".engine")
+    if family == "llama3":
+        cfg = M.preset("tiny-llama", vocab=512, d_model=256, n_heads=8, n_kv_heads=2, head_dim=64,
+                       d_ff=512, n_layers=3, init_std=0.05)
+    else:
+        cfg = M.preset("tiny-gemma", vocab=512, d_model=256, n_heads=4, n_kv_heads=2, head_dim=128,
+                       d_ff=512, n_layers=3, sliding_window=4096, query_pre_attn_scalar=128.0,
+                       init_std=0.05)
+    model = M.Model(cfg, dev, dtype, seed=seed, weights=weights)
+    return E.ScoringEngine(model, reuse_caches=0)
+
+
+def _fp32_twin(eng):
+    w = {k: v.float() for k, v in eng.model.w.items()}
+    fam = eng.model.cfg.family
+    M = importlib.import_module(PKG + ".model")
+    E = importlib.import_module(PKG + ".engine")
+    model = M.Model(eng.model.cfg, eng.device, torch.float32, weights=w)
+    return E.ScoringEngine(model, reuse_caches=0)
+
+
+@pytest.mark.parametrize("family", ["llama3", "gemma2"])
+def test_decode_state_matches_fp32_reference(dev, family):
+    """DecodeState (static K/V, cs_prefix_attention, graphs) against the eager path of the
+    SAME weights in fp32: next-token log-probs no further from fp32 than the eager bf16
+    path's (BeamState, SDPA over gathered contexts) plus 1e-2, and graph replays
+    bit-identical to the fused path run eagerly."""
+    E = importlib.import_module(PKG + ".engine")
+    eng = _tiny(family, dev)
+    e32 = _fp32_twin(eng)
+    g = torch.Generator().manual_seed(11)
+    prefixes = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (40, 23, 61)]
+    B, steps = 4, 6
+    cache = eng.prefill(prefixes)
+    c32 = e32.prefill(prefixes)
+    ref = E.BeamState(e32, c32, n_prefix=3)
+    eag = E.BeamState(eng, cache, n_prefix=3)
+    fus = E.DecodeState(eng, cache, n_prefix=3, n_beams=B, max_steps=steps)
+    fus_eager = E.DecodeState(eng, cache, n_prefix=3, n_beams=B, max_steps=steps, use_graphs=False)
+    V = eng.model.cfg.vocab
+    tgt = torch.randint(0, V, (3 * B, 16), generator=g).to(dev).to(torch.int32)
+    for step in range(steps):
+        parent = [0] * B if step == 0 else torch.randint(0, B, (B,), generator=g).tolist()
+        toks = torch.randint(5, 500, (B,), generator=g).tolist()
+        for st in (ref, eag, fus, fus_eager):
+            st.advance(parent, toks)
+        lp32 = e32.rows_logprobs(ref.next_hidden, tgt)
+        e_eag = float((eng.rows_logprobs(eag.next_hidden, tgt) - lp32).abs().max())
+        e_fus = float((eng.rows_logprobs(fus.hidden, tgt) - lp32).abs().max())
+        torch.cuda.synchronize()
+        assert e_fus <= 1.5 * e_eag + 1e-2, (step, e_fus, e_eag)
+        assert torch.equal(fus.hidden, fus_eager.hidden), step
+
+
+def test_forward_streams_scoring_chunk_matches_fp32(dev):
+    """T > 1 tokens per stream over shared prefixes (the Best-of-N scoring shape):
+    forward_streams vs model.extend over per-stream gathered contexts, both against the
+    fp32 twin of the model."""
+    E = importlib.import_module(PKG + ".engine")
+    eng = _tiny("llama3", dev, seed=5)
+    e32 = _fp32_twin(eng)
+    m = eng.model
+    g = torch.Generator().manual_seed(2)
+    prefixes = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (30, 52)]
+    n_str, T = 5, 13
+    toks = torch.randint(5, 500, (2 * n_str, T), generator=g).to(dev)
+    c = m.cfg
+    tgt = torch.randint(0, c.vocab, (2 * n_str * T, 4), generator=g).to(dev).to(torch.int32)
+    own = torch.arange(2, device=dev).repeat_interleave(n_str)
+
+    def eager(e):
+        cache = e.prefill(prefixes)
+        pos = cache.lengths[own][:, None] + torch.arange(T, device=dev)[None]
+        ctx = [(k[own], v[own]) for k, v in cache.kv]
+        h, _ = e.model.extend(toks, pos, ctx, cache.valid[own], cache.pos[own])
+        return e.rows_logprobs(h.reshape(-1, h.shape[-1]), tgt)
+
+    cache = eng.prefill(prefixes)
+    pfx = E.fused_prefix(cache)
+    hk = [torch.zeros(2 * n_str, c.n_kv_heads, 32, c.head_dim, dtype=torch.bfloat16, device=dev)
+          for _ in range(c.n_layers)]
+    hv = [torch.zeros(2 * n_str, c.n_kv_heads, c.head_dim, 32, dtype=torch.bfloat16, device=dev)
+          for _ in range(c.n_layers)]
+    hb = torch.zeros(1, dtype=torch.int32, device=dev)
+    h = m.forward_streams(toks.reshape(-1), pfx, hk, hv, hb, n_str, T)
+    lp = eng.rows_logprobs(h, tgt)
+    lp32 = eager(e32)
+    e_eag = float((eager(eng) - lp32).abs().max())
+    e_fus = float((lp - lp32).abs().max())
+    assert e_fus <= 1.5 * e_eag + 1e-2, (e_fus, e_eag)
+
+
+@pytest.mark.parametrize("family", ["llama3", "gemma2"])
+def test_beam_search_fast_topk_equals_host_loop(dev, family):
+    """The fast top-K loop (one graph replay per step ending in cs_beam_decode_step, one
+    device->host copy) and the general host loop (cs_vocab_topk + cs_beam_step per step)
+    on the SAME fused decode state: identical candidates, min-rewards and kept beams at
+    every step, and the same statement (both restate beam_search.py:439-667)."""
+    R = importlib.import_module(PKG + ".runtime")
+    T = importlib.import_module(PKG + ".tokenizer")
+    methods = importlib.import_module(PKG + ".methods")
+    eng = _tiny(family, dev, seed=7)
+    tok = T.CharTokenizer(family, vocab_size=eng.model.cfg.vocab)
+    R.register_engine("test/fused-tiny", eng, tok)
+    try:
+        ops_ = {"Agent 1": "We should fund public transit.", "Agent 2": "Lower taxes first.",
+                "Agent 3": "Protect the environment above all."}
+        cfg = {"beam_width": 3, "max_tokens": 9, "proposer": "topk", "top_k": 6}
+        gf = methods.get_method_generator("beam_search", dict(cfg), "test/fused-tiny")
+        sf = gf.generate_statement("How should the city spend its budget?", ops_)
+        gh = methods.get_method_generator("beam_search", dict(cfg, fast_topk=False), "test/fused-tiny")
+        sh = gh.generate_statement("How should the city spend its budget?", ops_)
+        assert gf.decode_path == "fused-topk" and gh.decode_path == "fused"
+        assert gf.step_log == gh.step_log
+        assert sf == sh
+    finally:
+        R.clear_engines()
