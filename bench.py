@@ -1,23 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark of the agent x candidate scoring + welfare hot path on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): Best-of-N, N = 64 candidates x A = 8
-agents per GPU, T = 150 scored tokens per candidate, Llama-3.1-8B vocabulary
-(128,256) in bf16, egalitarian welfare.  One step = one full N x A scoring pass:
+Headline (`value`, BASELINE.json configs[1], "C2"): Best-of-N scoring, N = 64 candidates x
+A = 8 agents per GPU, T = 150 scored tokens per candidate, Llama-3.1-8B (random-init,
+bf16), egalitarian welfare, END TO END: one step = one full N x A scoring pass,
 
-    logits [A*N*T, V] (resident in HBM)  --cs_logsoftmax_gather-->  token log-probs
-      --cs_segment_reduce--> per-(agent, candidate) mean log-prob utility
-      --cs_welfare_reduce(MIN)--> [RCCL MIN all-reduce across ranks]
-      --cs_segmented_topk(k=1)--> selected candidate
+    prefill the A agent prompts (prefix K/V) -> forward of every (agent, candidate) stream
+    over its agent's shared prefix (cs_rope_place + cs_prefix_attention per layer,
+    hipBLASLt GEMMs) -> LM head -> cs_logsoftmax_gather -> cs_segment_reduce -> mean
+    log-prob utilities -> cs_welfare_reduce(MIN) [-> RCCL MIN all-reduce] ->
+    cs_segmented_topk(k=1)
 
-Multi-GPU: agents shard across ranks (8 per GPU, weak scaling); the only exchange
-is the MIN all-reduce of the N per-candidate welfare values.
+i.e. what one reference `_calculate_candidate_rewards` + `_calculate_egalitarian_welfare`
+(src/methods/best_of_n.py:240-418) costs with every get_prompt_logprobs call
+(src/utils.py:201-281) served locally.  `value` = agent x candidate scorings/s of the
+whole job.  The same line carries:
+  kernel_only     the post-LM-head path alone on resident logits (76,800 x 128,256 bf16 =
+                  19.7 GB per pass); `roofline` prices its dominant kernel
+                  (lsg_stream_kernel of cs_logsoftmax_gather) against 8 TB/s from HIP
+                  events on its launch stream, `traffic` from rocprofv3 PMC counters;
+  method_decode   BASELINE C1 / C3 / C5 as beam_search generator runs (proposer "topk",
+                  random-init Llama-3.2-1B / Gemma-2-9B / Llama-3.3-70B bf16): decode steps/s
+                  WITH the forward (one graph replay + one host walk per step);
+  beam_kernel     the same decode steps' post-LM-head launch alone on resident logits;
+  cpu_baseline    the reference's per-call scoring restated on the host cores (a full
+                  forward of prompt + candidate per (agent, candidate), as
+                  get_prompt_logprobs re-encodes the prompt every call), plus the fp64 C
+                  oracle and torch.log_softmax + gather on a C2 logits sample.
 
-Prints ONE JSON line (rank 0).  `value` = agent x candidate scorings per second of
-the whole job; `roofline` prices the dominant kernel (cs_logsoftmax_gather)
-against the 8 TB/s HBM peak from HIP-event timing on its own stream;
-`cpu_baseline` times the CPU oracle (a port of the reference's fp64 scoring
-arithmetic) on a bounded sample of the same workload.
+Multi-GPU: `--gpus N` without a torchrun environment relaunches itself under
+torch.distributed.run with N ranks (before touching the GPU) and every rank checks the
+world size.  Agents shard across ranks (C2: 8 per GPU, weak scaling; C3 / C5: the
+config's agents split over the ranks); the only exchange is the MIN all-reduce of the
+per-candidate welfare.
 """
 from __future__ import annotations
 
@@ -25,6 +40,8 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,7 +52,12 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 PKG_DIR = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# byte-level BPE trained on the reference's texts (tests/golden/make_bpe_fixture.py): real
+# prompt token counts (~4 characters per token) for the method-level runs
+BPE_FIXTURE = os.path.join(REPO, "tests", "golden", "bpe_fixture")
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_DENSE_TFLOPS = 2500.0   # MI355X dense bf16 MFMA peak (no sparsity)
+METRIC = "agent×candidate scorings/sec + decode steps/sec at 1/2/4/8 MI355X; % HBM roofline"
 
 CONFIGS = {
     # name: (agents per GPU, candidates, scored tokens per candidate, vocab, welfare, description)
@@ -53,6 +75,49 @@ CONFIGS = {
                "340 nodes) x A=32 agents per GPU, Llama-3.1-8B vocab 128256 bf16 logits, "
                "Nash welfare"),
 }
+
+# method-level beam search runs (BASELINE configs[0], [2], [4]); agents are the config's
+# total, split over the ranks by the generator itself (parallel.method_shard)
+METHOD_CONFIGS = {
+    "c1": dict(preset="llama-3.2-1b", agents=4, beam_width=4, top_k=10, max_tokens=50,
+               desc="C1 beam_search: scenario 1, 4 agents, beam 4, top-10, 50 tokens, "
+                    "Llama-3.2-1B (random init, bf16)"),
+    "c3": dict(preset="gemma-2-9b", agents=16, beam_width=16, top_k=50, max_tokens=50,
+               desc="C3 beam_search: 16 agents, beam 16 x top-50, 50 tokens, Gemma-2-9B "
+                    "(random init, bf16; soft-caps 50 / 30)"),
+    "c5": dict(preset="llama-3.3-70b", agents=64, beam_width=8, top_k=32, max_tokens=50,
+               desc="C5 beam_search: 64 agents, beam 8 x top-32, 50 tokens, Llama-3.3-70B "
+                    "(random init, bf16, full replica per GPU)"),
+}
+
+# scenario 1 of the reference's appendix configs (configs/appendix/llama/scenario_1/
+# beam_search.yaml:20-25): the prompt texts of the synthetic agents
+SCENARIO_ISSUE = "Should a person's genetic code be considered private information?"
+SCENARIO_OPINIONS = [
+    "I'd like to think it should be considered private information and for the persons privacy "
+    "to be respected. However, it may be important for research or for the biological family. If "
+    "the person is open for it, then their opinion should be respected",
+    "A persons genetic code should be considered private information for the sole reason it "
+    "belongs to them. I can only think of medical case use scenarios when it may be useful to "
+    "someone else in the case of faulty genes etc being eradicated by using someone else's stem "
+    "cells or dna to help in this.",
+    "The majority of all the genetic code is identical between people. I am undecided on the "
+    "matter, the differences make us different. But by sharing all the genetic code, this may "
+    "help prevent and cure illnesses so I would be slightly in favour if used appropriately.",
+    "I believe that a person's genetic code should be considered private information, the same "
+    "way you wouldn't give out your address or personal information to strangers, it should "
+    "cover your genetic makeup as well as it could be used to screen out people with specific "
+    "genetic markers and for discrimination in the future. Having access to your genetic "
+    "information also has the added risk of being potentially harmful to any offspring in the "
+    "future and I believe that precaution should be taken to ensure that your genetic code is "
+    "safe from abuse by others.",
+]
+
+
+def synthetic_opinions(n):
+    """n agent opinions: the scenario's 4 texts cycled, each tagged with its participant
+    number so that every agent prompt is distinct (SURVEY.md §8(d) synthetic inputs)."""
+    return {f"Agent {i + 1}": f"{SCENARIO_OPINIONS[i % 4]} (participant {i + 1})" for i in range(n)}
 
 
 def tree_layout(bf, depth, A, dev):
@@ -94,30 +159,63 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="workload of the kernel-only leg")
+    ap.add_argument("--e2e", default=1, type=int,
+                    help="1: the headline value is the forward-included C2 pass (default); "
+                         "0: kernel-only (the headline then reports the kernel leg, labelled)")
+    ap.add_argument("--method", default="c1,c3,c5",
+                    help="method-level beam_search decode configs ('' disables)")
+    ap.add_argument("--method-statements", type=int, default=1,
+                    help="timed generate_statement calls per method config")
     ap.add_argument("--beam", default="c1,c3,c5",
-                    help="beam-search decode-step configs reported under 'beam' ('' disables)")
+                    help="kernel-level beam decode configs on resident logits ('' disables)")
     ap.add_argument("--beam-steps", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="target CPU time for the oracle baseline sample (0 disables)")
+                    help="target CPU time per CPU-baseline sample (0 disables)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
-                         "the multi-rank path with several ranks on one GPU)")
-    ap.add_argument("--e2e", action="store_true",
-                    help="also time the full scoring pass INCLUDING the transformer forward "
-                         "(random-init Llama-3.1-8B bf16, per-agent prefix K/V) and report it "
-                         "under 'end_to_end'")
+                         "the multi-rank path)")
+    ap.add_argument("--selftest-launch", action="store_true",
+                    help="only launch the ranks, check the world size and print the agent split "
+                         "(no GPU work; CPU-testable with --backend gloo)")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per launch (optional)")
     return ap.parse_args()
 
 
-def init_dist(n_gpus, backend="nccl"):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args) -> int:
+    """--gpus N outside torchrun: run N ranks under torch.distributed.run as a CHILD
+    process (this process never touches the GPU) and exit with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and os.environ.get("CS_BENCH_FORCE_SHARDED") != "1":
+        sys.exit(f"bench: world size {world} != --gpus {args.gpus}; run under torchrun with "
+                 f"--nproc-per-node {args.gpus} or let bench.py launch the ranks itself")
+    if args.selftest_launch:
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo" if args.backend == "gloo" else args.backend)
+        return world, rank, local
     if world > 1 or os.environ.get("CS_BENCH_FORCE_SHARDED") == "1":
-        if backend == "gloo":   # rehearsal: every rank on the one visible GPU
+        if args.backend == "gloo":   # rehearsal: every rank on the one visible GPU
             torch.cuda.set_device(0)
             torch.distributed.init_process_group("gloo")
         else:
@@ -126,6 +224,49 @@ def init_dist(n_gpus, backend="nccl"):
     else:
         torch.cuda.set_device(0)
     return world, rank, local
+
+
+def selftest_launch(world, rank, local):
+    """The launch contract without GPU work: every rank reports itself and its agent share."""
+    par = importlib.import_module(PKG_DIR + ".parallel")
+    me = {"rank": rank, "local_rank": local,
+          "c2_agents": par.AgentShard(8 * world, rank, world).local,
+          "c3_agents": par.AgentShard(16, rank, world).local,
+          "c5_agents": par.AgentShard(64, rank, world).local}
+    if world > 1:
+        allm = [None] * world
+        torch.distributed.all_gather_object(allm, me)
+        torch.distributed.barrier()
+    else:
+        allm = [me]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "selftest_launch": True, "n_gpus": world,
+                          "ranks": allm}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def _barrier_sync(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
+def _max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _free(*_objs):
+    R = importlib.import_module(PKG_DIR + ".runtime")
+    R.clear_engines()
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
 
 
 def make_inputs(A, N, T, V, seed, dev):
@@ -141,79 +282,339 @@ def make_inputs(A, N, T, V, seed, dev):
     return logits, tgt, offsets
 
 
-def cpu_baseline(A, N, T, V, welfare_kind, seconds):
-    """Time the CPU oracle on a bounded sample: 2 agents x 8 candidates of the workload."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as orc
+def c2_kernel_leg(args, world, rank, dev):
+    """The post-LM-head path alone on resident logits (BASELINE C2 / C4 shapes):
+    cs_logsoftmax_gather -> cs_segment_reduce -> mean -> welfare -> [all-reduce] -> top-1."""
+    ops = importlib.import_module(PKG_DIR + ".ops")
+    par = importlib.import_module(PKG_DIR + ".parallel")
+    A, N, T, V, wkind, desc = CONFIGS[args.config]
+    tree = args.config.endswith("tree")
+    flat = None
+    if tree:   # rows = tree nodes; each path's log-probs are gathered from its nodes
+        n_nodes, flat = tree_layout(4, T, A, dev)
+        rows = A * n_nodes
+        logits, tgt, _ = make_inputs(A, n_nodes, 1, V, 1234 + rank, dev)
+        offsets = torch.arange(0, A * N * T + 1, T, dtype=torch.int32, device=dev)
+    else:
+        rows = A * N * T
+        logits, tgt, offsets = make_inputs(A, N, T, V, 1234 + rank, dev)
+    ws = ops.Workspace()
+    stream = torch.cuda.current_stream()
+    shard = par.AgentShard(A * world, rank, world)   # A agents per GPU, round-robin
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    orc.set_threads(threads)
-    a_s, n_s = 2, 8
-    rows = a_s * n_s * T
-    rng = np.random.default_rng(99)
-    logits = orc.bf16_bits((rng.standard_normal((rows, V), dtype=np.float32) * 3.0))
-    tgt = rng.integers(0, V, size=(rows, 1)).astype(np.int32)
-    off = np.arange(0, rows + 1, T, dtype=np.int32)
-    kind = {"min": orc.MIN, "sumlog": orc.SUMLOG}[welfare_kind]
-    iters, t0 = 0, time.perf_counter()
-    while True:
-        tok, _ = orc.logsoftmax_gather(logits, tgt, bf16=True)
-        seg = orc.segment_reduce(tok, off)
-        U = (seg["sum_lp"] / seg["count"]).reshape(a_s, n_s)
-        W = orc.welfare(U, kind)
-        orc.topk(W, 1)
-        iters += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": a_s * n_s * iters / el, "unit": "scorings/s", "cores": threads, "kind": "port",
-            "sample": f"{a_s} agents x {n_s} candidates x T={T} rows of V={V} bf16 "
-                      f"(oracle/cs_oracle.c fp64, OpenMP {threads} threads), {iters} passes "
-                      f"in {el:.1f} s"}
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        tok, _ = ops.logsoftmax_gather(logits, tgt, workspace=ws)
+        if ev is not None:
+            ev[1].record(stream)
+        if flat is not None:
+            tok = tok.view(-1).index_select(0, flat)
+        seg = ops.segment_reduce(tok, offsets)
+        U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N)
+        if wkind == "sumlog":
+            U = torch.exp(U)  # Nash over geometric-mean token probability
+        if ev is not None:
+            ev[2].record(stream)
+        W = par.combine_welfare(U, wkind, shard, eps=1e-30)
+        if ev is not None:
+            ev[3].record(stream)
+        idx, _ = ops.topk(W, 1)
+        return idx
+
+    for _ in range(args.warmup):
+        step()
+    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
+              for _ in range(args.steps)]
+    _barrier_sync(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    _barrier_sync(world)
+    elapsed = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    coll_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in events]))
+    ms = elapsed * 1000.0 / args.steps
+    alg_bytes = rows * V * 2 + rows * 4 * 2  # logits read once + targets in + lp out
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    del logits
+    return {
+        "workload": desc, "timing": "eager launches, resident bf16 logits",
+        "scorings_per_s": A * N * world * args.steps / elapsed, "ms_per_step": ms,
+        "passes_per_s": 1000.0 / ms, "rows_per_gpu": rows, "steps": args.steps,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": read_traffic(args.pmc_json, args.config, rows, V),
+                     "kernel": "lsg_stream_kernel (cs_logsoftmax_gather)",
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
+        "collective": {"op": ("all_reduce(MIN) of W" if wkind == "min" else
+                              "all_gather of [A_local, C] + ordered fold") if world > 1
+                       else "none (1 GPU: local fold)",
+                       "bytes": N * 4 if wkind == "min" else A * world * N * 4,
+                       "ms_per_step": coll_ms},
+    }
 
 
-def end_to_end(A, N, T, V, wkind, dev, steps=2, prefix_len=200, seed=0):
-    """Full C2 scoring pass incl. the transformer forward: Llama-3.1-8B (random init, bf16)
-    prefills A agent prefixes of `prefix_len` tokens once, then scores N candidates x T
-    tokens under every agent (prefix K/V reused by all candidates), LM head, HIP kernels,
-    welfare, selection."""
+def _model_flops_per_token(cfg):
+    """2 x the parameters one token multiplies (projections, MLP, LM head)."""
+    d, L = cfg.d_model, cfg.n_layers
+    per_layer = d * (cfg.n_heads + 2 * cfg.n_kv_heads) * cfg.head_dim + cfg.n_heads * cfg.head_dim * d \
+        + 3 * d * cfg.d_ff
+    return 2.0 * (L * per_layer + cfg.vocab * d)
+
+
+def c2_e2e_leg(args, world, rank, dev, prefix_len=200, seed=0):
+    """BASELINE C2 end to end: Llama-3.1-8B (random init, bf16) prefills the A agent prefixes,
+    scores N candidates x T tokens under every agent (shared prefix K/V on the stream
+    kernels), LM head, HIP kernels, welfare (+ RCCL MIN all-reduce), selection."""
     M = importlib.import_module(PKG_DIR + ".model")
     E = importlib.import_module(PKG_DIR + ".engine")
     ops = importlib.import_module(PKG_DIR + ".ops")
+    par = importlib.import_module(PKG_DIR + ".parallel")
+    A, N, T, V, wkind, desc = CONFIGS["c2"]
     cfg = M.preset("llama-3.1-8b")
     t0 = time.perf_counter()
     model = M.Model(cfg, dev, torch.bfloat16, seed=seed)
     torch.cuda.synchronize()
     init_s = time.perf_counter() - t0
-    # every pass re-encodes the prefixes in full (no reuse of the previous pass's K/V)
-    eng = E.ScoringEngine(model, max_rows_per_chunk=16384, reuse_caches=0)
-    g = torch.Generator().manual_seed(11)
+    # every pass re-encodes its prefixes (no reuse of the previous pass's K/V)
+    eng = E.ScoringEngine(model, reuse_caches=0)
+    g = torch.Generator().manual_seed(11 + rank)
     prefixes = [torch.randint(300, V, (prefix_len,), generator=g).tolist() for _ in range(A)]
     cands = [torch.randint(300, V, (T,), generator=g).tolist() for _ in range(N)]
     owner = [a for a in range(A) for _ in range(N)]
     conts = [cands[c] for _ in range(A) for c in range(N)]
     offs = eng.offsets(conts, dev)
+    shard = par.AgentShard(A * world, rank, world)
 
     def one_pass():
         cache = eng.prefill(prefixes)
         lp = eng.score(cache, owner, conts)
         seg = ops.segment_reduce(lp, offs)
         U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N).contiguous()
-        W = ops.welfare(U, wkind)
+        W = par.combine_welfare(U, wkind, shard, nonfinite="replace")
         return ops.topk(W, 1)[0]
 
-    one_pass()
+    for _ in range(args.warmup):
+        one_pass()
+    _barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_pass()
+    _barrier_sync(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    dt = el / args.steps
+    tokens = A * N * T + A * prefix_len
+    flops = _model_flops_per_token(cfg) * tokens
+    out = {"workload": desc + "; forward included (Llama-3.1-8B random init, bf16, "
+                              f"{prefix_len}-token agent prefixes re-encoded every pass)",
+           "scorings_per_s": world * A * N / dt, "s_per_pass": dt, "passes": args.steps,
+           "scored_tokens_per_gpu": A * N * T, "prefix_tokens_per_gpu": A * prefix_len,
+           "tokens_per_s": world * A * N * T / dt, "model_init_s": init_s,
+           "path": "ScoringEngine.score -> _score_fused (cs_rope_place + cs_prefix_attention per "
+                   "layer; GEMMs hipBLASLt) -> cs_logsoftmax_gather -> folds",
+           "model_tflops_per_s": flops / dt / 1e12,
+           "mfma_frac": flops / dt / 1e12 / BF16_DENSE_TFLOPS}
+    del eng, model
+    _free()
+    return out
+
+
+def method_leg(name, args, world, rank, dev):
+    """A BASELINE beam configuration as the product's beam_search generator on a random-init
+    model: decode steps/s with the forward included (one captured graph replay + one
+    device->host copy + the reference's host walk per step)."""
+    R = importlib.import_module(PKG_DIR + ".runtime")
+    E = importlib.import_module(PKG_DIR + ".engine")
+    methods = importlib.import_module(PKG_DIR + ".methods")
+    mc = METHOD_CONFIGS[name]
+    t0 = time.perf_counter()
+    eng, tok = R.random_engine(mc["preset"], dev, reuse_caches=0, tokenizer_dir=BPE_FIXTURE)
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    model_id = "random:" + mc["preset"]
+    R.register_engine(model_id, eng, tok)
+    opinions = synthetic_opinions(mc["agents"])
+    gcfg = {"beam_width": mc["beam_width"], "max_tokens": mc["max_tokens"], "proposer": "topk",
+            "top_k": mc["top_k"], "seed": 1}
+    warm = methods.get_method_generator("beam_search", dict(gcfg, max_tokens=4), model_id)
+    warm.generate_statement(SCENARIO_ISSUE, opinions)
+    runs = []
+    for _ in range(max(1, args.method_statements)):
+        gen = methods.get_method_generator("beam_search", dict(gcfg), model_id)
+        _barrier_sync(world)
+        t0 = time.perf_counter()
+        gen.generate_statement(SCENARIO_ISSUE, opinions)
+        _barrier_sync(world)
+        el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+        st = np.asarray(gen.step_times)
+        d = np.diff(st)
+        steady = d[2:] if d.size > 4 else d           # past the two graph captures
+        step_s = _max_over_ranks(float(np.median(steady)) if steady.size else el, world, dev)
+        runs.append({"statement_s": el, "steps": gen.steps_run, "step_s": step_s,
+                     "path": gen.decode_path})
+    step_s = float(np.median([r["step_s"] for r in runs]))
+    steps = runs[-1]["steps"]
+    A, B, K = mc["agents"], mc["beam_width"], mc["top_k"]
+    # the step alone: the same graph (advance + LM head + cs_beam_decode_step) replayed with
+    # no host walk in between -> what the host adds per step
+    graph_ms = None
+    if world == 1:
+        graph_ms = _graph_step_ms(eng, tok, opinions, mc, dev)
+    out = {"workload": mc["desc"], "agents": A, "beams": B, "top_k": K,
+           "agents_per_gpu": len(range(rank, A, world)),
+           "decode_steps_per_s": 1.0 / step_s, "ms_per_step": step_s * 1e3,
+           "scorings_per_s": A * B * K / step_s,
+           "statement_s": float(np.median([r["statement_s"] for r in runs])),
+           "steps_per_statement": steps, "statements": len(runs), "model_init_s": init_s,
+           "decode_path": runs[-1]["path"],
+           "timing": "median host step time of the generator's loop (forward + LM head + "
+                     "cs_beam_decode_step graph replay, device->host copy, reference walk), "
+                     "max over ranks; statement_s includes prefill and the graph captures"}
+    if graph_ms is not None:
+        out["graph_step_ms"] = graph_ms
+        out["host_overhead_frac"] = step_s * 1e3 / graph_ms - 1.0
+    del eng
+    _free()
+    return out
+
+
+def _graph_step_ms(eng, tok, opinions, mc, dev, reps=20):
+    """Replays of one decode step's graph (parents' history gather, forward of the new
+    tokens, LM head, cs_beam_decode_step) back to back: the GPU cost of a step."""
+    E = importlib.import_module(PKG_DIR + ".engine")
+    ops = importlib.import_module(PKG_DIR + ".ops")
+    P = importlib.import_module(PKG_DIR + ".methods.prompts")
+    A, B, K = mc["agents"], mc["beam_width"], mc["top_k"]
+    agent_prefixes = [tok.chat_prefix(P.BEAM["agent_system"],
+                                      P.BEAM["agent_user"].format(issue=SCENARIO_ISSUE, opinion=o))
+                      for o in opinions.values()]
+    ref_user = P.BEAM["ref_user"].format(issue=SCENARIO_ISSUE,
+                                         opinions_text=P.opinions_text(opinions))
+    cache = eng.prefill_streams(agent_prefixes +
+                                [tok.render_raw(f"{P.BEAM['ref_system']}\n\n{ref_user}")])
+    st = E.DecodeState(eng, cache, n_prefix=A + 1, n_beams=B, max_steps=reps + 3)
+    m = eng.model
+    U = torch.empty(A, B * K, dtype=torch.float32, device=dev)
+    W = torch.empty(B * K, dtype=torch.float32, device=dev)
+    rw = torch.zeros(A, B, dtype=torch.float32, device=dev)
+    ids = torch.empty(B, K, dtype=torch.int32, device=dev)
+    order = torch.empty(B * K, dtype=torch.int32, device=dev)
+    ws = ops.Workspace(zeroed=True)
+
+    def post():
+        lg = m.lm_head(st.hidden)
+        ops.beam_decode_step(lg[A * B:], lg[:A * B], rw, K, "min", n_order=B * K,
+                             softcap=eng.softcap, workspace=ws, out_U=U, out_W=W, out_ids=ids,
+                             out_order=order)
+
+    par = list(range(B))
+    for _ in range(3):                       # eager step + the two captures
+        st.advance(par, [5] * B, post=post)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        one_pass()
+    for _ in range(reps):
+        st.advance(par, [5] * B, post=post)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    return {"model": "llama-3.1-8b (random init, bf16)", "prefix_tokens": prefix_len,
-            "scored_tokens": A * N * T, "s_per_pass": dt, "scorings_per_s": A * N / dt,
-            "tokens_per_s": A * N * T / dt, "model_init_s": init_s, "passes": steps,
-            "note": "forward = PyTorch/hipBLASLt (plumbing); logits -> HIP C-ABI kernels"}
+    return (time.perf_counter() - t0) * 1e3 / reps
+
+
+def _host_cores():
+    """The host cores this process may use: its affinity mask, capped by OMP_NUM_THREADS
+    (the GPU box sets it to its CPU share; the mask shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def cpu_baseline(seconds, V=128_256, T=150):
+    """The reference's scoring path restated on the host cores.
+
+    Headline (`value`): the reference scores every (agent, candidate) with a
+    get_prompt_logprobs call that re-encodes the whole prompt (src/utils.py:249-259): here
+    one CPU forward of prompt + candidate through Llama-3.2-1B in fp32 (BASELINE configs[0]:
+    "Llama-3.2-1B logprobs on CPU"), log-softmax over the vocabulary at every candidate
+    position and the gather, per scoring, on all host cores.  Also reported: the fp64 C
+    oracle (the scoring arithmetic after the LM head) and torch.log_softmax + gather on a
+    C2 logits sample, both on the same cores."""
+    M = importlib.import_module(PKG_DIR + ".model")
+    cores = _host_cores()
+    torch.set_num_threads(cores)
+    out = {"unit": "scorings/s", "cores": cores, "kind": "port"}
+    # (1) forward-included per-call scoring, 1B fp32
+    cfg = M.preset("llama-3.2-1b")
+    t0 = time.perf_counter()
+    # constant-filled fp32 weights of the exact shapes: a CPU forward's time does not
+    # depend on the values, and filling is seconds where sampling 1.2 G normals is minutes
+    model = M.Model.__new__(M.Model)
+    model.cfg = cfg
+    w = {n: torch.full(shp, 1.0 if "norm" in n else 0.01, dtype=torch.float32)
+         for n, shp in model.shapes().items()}
+    model = M.Model(cfg, "cpu", torch.float32, weights=w)
+    init_s = time.perf_counter() - t0
+    g = torch.Generator().manual_seed(3)
+    P, Tc = 200, 10
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            ids = torch.randint(300, cfg.vocab, (1, P + Tc), generator=g)
+            kv, h, _ = model.prefill(ids, torch.tensor([P + Tc]))
+            lg = model.lm_head(h[0, P - 1:P + Tc - 1]).float()
+            lp = torch.log_softmax(lg, dim=-1).gather(1, ids[0, P:P + Tc, None])
+            float(lp.mean())
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    out["value"] = n / el
+    out["sample"] = (f"{n} scorings in {el:.1f} s: Llama-3.2-1B fp32 (constant weights) forward of a "
+                     f"{P}-token prompt + {Tc}-token candidate, log-softmax over {cfg.vocab} + "
+                     f"gather at the candidate tokens, per (agent, candidate) as "
+                     f"get_prompt_logprobs re-encodes every call; torch {cores} threads "
+                     f"(model init {init_s:.1f} s, not timed)")
+    del model
+    # (2) the post-LM-head arithmetic: fp64 C oracle and torch fp32, C2 rows
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+    orc.set_threads(cores)
+    a_s, n_s = 2, 8
+    rows = a_s * n_s * T
+    rng = np.random.default_rng(99)
+    x32 = rng.standard_normal((rows, V), dtype=np.float32) * 3.0
+    logits = orc.bf16_bits(x32)
+    tgt = rng.integers(0, V, size=(rows, 1)).astype(np.int32)
+    off = np.arange(0, rows + 1, T, dtype=np.int32)
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        tok, _ = orc.logsoftmax_gather(logits, tgt, bf16=True)
+        seg = orc.segment_reduce(tok, off)
+        U = (seg["sum_lp"] / seg["count"]).reshape(a_s, n_s)
+        orc.topk(orc.welfare(U, orc.MIN), 1)
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds / 2:
+            break
+    out["oracle_post_lm_head"] = {"value": a_s * n_s * iters / el, "unit": "scorings/s",
+                                  "sample": f"{a_s} agents x {n_s} candidates x T={T} rows of "
+                                            f"V={V} bf16, oracle/cs_oracle.c fp64, {iters} passes"}
+    xt = torch.from_numpy(x32).to(torch.bfloat16)
+    tt = torch.from_numpy(tgt.astype(np.int64))
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        lp = torch.log_softmax(xt.float(), dim=-1).gather(1, tt)
+        float(lp.sum())
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds / 2:
+            break
+    out["torch_log_softmax_gather"] = {
+        "value": a_s * n_s * iters / el, "unit": "scorings/s",
+        "gb_per_s": rows * V * 2 * iters / el / 1e9,
+        "sample": f"torch.log_softmax(x.float()).gather on [{rows}, {V}] bf16, {iters} passes"}
+    return out
 
 
 def gpu_busy(stream, ms=20.0):
@@ -421,115 +822,30 @@ def read_traffic(path, config, rows, V):
 
 def main():
     args = parse()
-    world, rank, local = init_dist(args.gpus, args.backend)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
+    world, rank, local = init_dist(args)
+    if args.selftest_launch:
+        selftest_launch(world, rank, local)
+        return
     dev = torch.device("cuda", torch.cuda.current_device())
-    ops = importlib.import_module(PKG_DIR + ".ops")
     par = importlib.import_module(PKG_DIR + ".parallel")
 
-    A, N, T, V, wkind, desc = CONFIGS[args.config]
-    tree = args.config.endswith("tree")
-    flat = None
-    if tree:   # rows = tree nodes; each path's log-probs are gathered from its nodes
-        n_nodes, flat = tree_layout(4, T, A, dev)
-        rows = A * n_nodes
-        logits, tgt, _ = make_inputs(A, n_nodes, 1, V, 1234 + rank, dev)
-        offsets = torch.arange(0, A * N * T + 1, T, dtype=torch.int32, device=dev)
-    else:
-        rows = A * N * T
-        logits, tgt, offsets = make_inputs(A, N, T, V, 1234 + rank, dev)
-    ws = ops.Workspace()
-    stream = torch.cuda.current_stream()
-    shard = par.AgentShard(A * world, rank, world)   # A agents per GPU, round-robin
+    errors = {}
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        tok, _ = ops.logsoftmax_gather(logits, tgt, workspace=ws)
-        if ev is not None:
-            ev[1].record(stream)
-        if flat is not None:
-            tok = tok.view(-1).index_select(0, flat)
-        seg = ops.segment_reduce(tok, offsets)
-        U = (seg["sum_lp"] / seg["count"].to(torch.float32)).view(A, N)
-        if wkind == "sumlog":
-            U = torch.exp(U)  # Nash over geometric-mean token probability
-        # agents sharded over ranks: MIN all-reduce (egalitarian) or gather + ordered fold
-        if ev is not None:
-            ev[2].record(stream)
-        W = par.combine_welfare(U, wkind, shard, eps=1e-30)
-        if ev is not None:
-            ev[3].record(stream)
-        idx, _ = ops.topk(W, 1)
-        return idx
+    def guarded(name, fn, *a):
+        """A failing leg is reported in the line (and on stderr), not a lost line."""
+        try:
+            return fn(*a)
+        except Exception as e:   # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            errors[name] = f"{type(e).__name__}: {e}"[:500]
+            _free()
+            return None
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
-              for _ in range(args.steps)]
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(events[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    # the welfare exchange (RCCL MIN all-reduce, or all-gather + ordered fold) broken out
-    coll_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in events]))
-    ms_per_step = elapsed * 1000.0 / args.steps
-
-    line = None
-    if rank == 0:
-        scorings = A * N * world
-        alg_bytes = rows * V * 2 + rows * 4 * 2  # logits read once + targets in + lp out
-        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        cpu = None
-        if world == 1 and args.cpu_seconds > 0 and not tree:
-            cpu = cpu_baseline(A, N, T, V, wkind, args.cpu_seconds)
-        e2e = None
-        if args.e2e and world == 1 and not tree:
-            del logits
-            torch.cuda.empty_cache()
-            e2e = end_to_end(A, N, T, V, wkind, dev)
-        line = {
-            "metric": "agent×candidate scorings/sec + decode steps/sec at 1/2/4/8 MI355X; % HBM roofline",
-            "value": scorings * args.steps / elapsed,
-            "unit": "scorings/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "decode_steps_per_s": 1000.0 / ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic",
-            "config": {"workload": desc, "agents_per_gpu": A, "candidates": N,
-                       "tokens_per_candidate": T, "vocab": V, "rows_per_gpu": rows,
-                       "welfare": wkind, "parallelism": f"agents sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": read_traffic(args.pmc_json, args.config, rows, V),
-                         "kernel": "lsg_stream_kernel (cs_logsoftmax_gather)",
-                         "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
-            "cpu_baseline": cpu,
-            "collective": {"op": ("all_reduce(MIN) of W" if wkind == "min" else
-                                  "all_gather of [A_local, C] + ordered fold") if world > 1
-                           else "none (1 GPU: local fold)",
-                           "bytes": N * 4 if wkind == "min" else A * world * N * 4,
-                           "ms_per_step": coll_ms},
-        }
-        if e2e is not None:
-            line["end_to_end"] = e2e
+    kern = c2_kernel_leg(args, world, rank, dev)
+    _free()
     beam = {}
     beams = [b for b in args.beam.split(",") if b]
     comm = None
@@ -540,12 +856,63 @@ def main():
             print(f"bench: direct RCCL communicator unavailable ({e}); using the ProcessGroup",
                   file=sys.stderr, flush=True)
     for name in beams:
-        beam[name] = run_beam(name, world, rank, dev, args.beam_steps, 20, comm, args.pmc_json)
+        r = guarded("beam_kernel." + name, run_beam, name, world, rank, dev, args.beam_steps, 20,
+                    comm, args.pmc_json)
+        if r is not None:
+            beam[name] = r
     if comm is not None:
         comm.close()
+    _free()
+    e2e = (guarded("end_to_end", c2_e2e_leg, args, world, rank, dev)
+           if args.e2e and args.config == "c2" else None)
+    method = {}
+    for name in [m for m in args.method.split(",") if m]:
+        r = guarded("method_decode." + name, method_leg, name, args, world, rank, dev)
+        if r is not None:
+            method[name] = r
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = guarded("cpu_baseline", cpu_baseline, args.cpu_seconds)
+
     if rank == 0:
+        A, N, T, V, wkind, desc = CONFIGS[args.config]
+        if e2e is not None:
+            value, ms, note = e2e["scorings_per_s"], e2e["s_per_pass"] * 1e3, "end_to_end"
+        else:
+            value, ms, note = kern["scorings_per_s"], kern["ms_per_step"], "kernel_only"
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "scorings/s",
+            "value_is": note,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "decode_steps_per_s": 1000.0 / ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights of the named architectures, synthetic token "
+                    "ids / scenario-1 prompt texts)",
+            "config": {"workload": desc + ("; forward included" if e2e is not None else
+                                           "; post-LM-head kernels on resident logits"),
+                       "agents_per_gpu": A, "candidates": N, "tokens_per_candidate": T,
+                       "vocab": V, "welfare": wkind,
+                       "parallelism": f"agents sharded over {world} GPU(s)"},
+            "roofline": kern["roofline"],
+            "cpu_baseline": cpu,
+            "kernel_only": {k: v for k, v in kern.items() if k != "roofline"},
+        }
+        if e2e is not None:
+            line["end_to_end"] = e2e
+        if method:
+            line["method_decode"] = method
         if beam:
-            line["beam"] = beam
+            line["beam_kernel"] = beam
+        if errors:
+            line["errors"] = errors
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

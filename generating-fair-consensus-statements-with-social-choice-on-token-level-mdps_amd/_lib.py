@@ -26,7 +26,7 @@ EXPORTED = (
     "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_workspace_size",
-    "cs_prefix_attention", "cs_rope_place",
+    "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
 )
 
 
@@ -53,6 +53,12 @@ def load():
         raise CSError(
             f"{LIB_NAME} is not built ({path} missing). Build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` from the repo root.")
+    from . import build as _build
+    if _build.built_hash() != _build.source_hash():
+        # a library older than its sources would be called with the new signatures
+        raise CSError(f"{LIB_NAME} is stale (built from other sources than csrc/ and "
+                      "include/ now hold). Rebuild it with "
+                      "`python -c 'import __graft_entry__ as g; g.build()'`.")
     try:
         L = ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover - environment dependent
@@ -95,14 +101,22 @@ def load():
     L.cs_beam_decode_step.restype = ctypes.c_int
     L.cs_beam_select.argtypes = [vp, i32, ctypes.c_int, vp, i32, i32, vp, vp, vp, vp, vp]
     L.cs_beam_select.restype = ctypes.c_int
-    L.cs_prefix_attention_workspace_size.argtypes = [i32, i32, i32, i32, i32, i32, i64]
+    L.cs_prefix_attention_workspace_size.argtypes = [i32, i32, i32, i32, i32, i32, i32, i64]
     L.cs_prefix_attention_workspace_size.restype = ctypes.c_size_t
-    L.cs_prefix_attention.argtypes = [vp, vp, vp, i64, vp, vp, i32, vp, vp, i64, vp, i32, i32, i32,
-                                      i32, i32, f32, f32, vp, vp, ctypes.c_size_t, vp]
+    L.cs_prefix_attention.argtypes = [vp, vp, vp, i64, vp, vp, i32, vp, i32, vp, vp, i64, vp, i32,
+                                      i32, i32, i32, i32, f32, f32, i32, vp, vp, ctypes.c_size_t,
+                                      vp]
     L.cs_prefix_attention.restype = ctypes.c_int
     L.cs_rope_place.argtypes = [vp, i64, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp,
                                 i64, vp]
     L.cs_rope_place.restype = ctypes.c_int
+    L.cs_add_rms_norm.argtypes = [vp, i64, vp, i64, vp, i64, vp, i64, i64, f32, ctypes.c_int, vp,
+                                  i64, vp]
+    L.cs_add_rms_norm.restype = ctypes.c_int
+    L.cs_gated_act.argtypes = [vp, i64, vp, i64, i64, i64, ctypes.c_int, vp, i64, vp]
+    L.cs_gated_act.restype = ctypes.c_int
+    L.cs_hist_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, vp]
+    L.cs_hist_gather.restype = ctypes.c_int
     _lib = L
     return L
 

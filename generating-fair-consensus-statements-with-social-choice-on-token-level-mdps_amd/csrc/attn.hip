@@ -19,7 +19,8 @@
 //
 // Layouts (all bf16, D = head_dim in {64, 128, 256}):
 //   q       [n_tok, H, D], token tok = s*T + t of stream s = grp*n_str + b
-//   k_pfx   [n_prefix, Hkv, ldp, D]     vt_pfx [n_prefix, Hkv, D, ldp]   (ldp % 32 == 0)
+//   k_pfx   [Hkv, Lp, D]                vt_pfx [Hkv, D, Lp]     (ragged prefixes: prefix p's
+//           keys are rows off[p] .. off[p] + len[p], off[p] % 32 == 0, padded to 32 keys)
 //   k_hist  [S, Hkv, ldh, D]            vt_hist [S, Hkv, D, ldh]         (ldh % 32 == 0)
 //   out     [n_tok, H, D]
 // Query token t of stream s sees prefix keys [0, plen[pfx]) and history keys
@@ -45,11 +46,13 @@ constexpr int kAttnThreads = 256;   // 4 waves
 constexpr int kGroupRows = 64;      // query rows per workgroup (4 tiles of 16)
 constexpr int kKeyBlock = 32;
 constexpr int kMaxSplit = 32;
+constexpr int kItemsPerWave = 4;   // key blocks a wave walks before the work is split further
 
 struct AttnParams {
   const __bf16* q;
   const __bf16* kp;
   const __bf16* vtp;
+  const int64_t* poff;
   const int32_t* plen;
   const int32_t* gpfx;      // group -> prefix index (nullable: identity)
   const __bf16* kh;
@@ -60,6 +63,7 @@ struct AttnParams {
   int64_t ldp, ldh;
   int32_t n_grp, n_str, T, H, Hkv, rep, n_qg, n_split;
   float scale, softcap, inv_softcap;
+  int32_t window;           // > 0: keys more than window - 1 positions back are masked
   int32_t swizzle;
 };
 
@@ -71,6 +75,29 @@ __device__ __forceinline__ int logical_block(int swz) {
   if (!swz) return b;
   const int per = gridDim.x >> 3;
   return (b & 7) * per + (b >> 3);
+}
+
+// key blocks ("items") a 16-row query tile visits: the prefix blocks plus the history blocks
+// of every stream with rows in the tile
+__device__ __forceinline__ int tile_items(const AttnParams& a, int M, int rt0, int nbp, int hb) {
+  const int rt1 = min(rt0 + 15, M - 1);
+  const int b_lo = (rt0 / a.rep) / a.T, b_hi = (rt1 / a.rep) / a.T;
+  const int t_hi = b_lo == b_hi ? (rt1 / a.rep) % a.T : a.T - 1;
+  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
+  return nbp + (b_hi - b_lo + 1) * nbh;
+}
+
+// splits a (group, head, query group) uses: enough that no wave walks more than
+// kItemsPerWave blocks, at most the grid's n_split (device-side, from the actual prefix
+// length and history size; the merge recomputes the same number)
+__device__ __forceinline__ int splits_used(const AttnParams& a, int M, int r0, int nbp, int hb) {
+  const int nrows = min(kGroupRows, M - r0);
+  const int n_qt = (nrows + 15) >> 4;
+  const int kw = n_qt == 1 ? 4 : (n_qt == 2 ? 2 : 1);
+  int items = 0;
+  for (int q = 0; q < n_qt; ++q) items = max(items, tile_items(a, M, r0 + 16 * q, nbp, hb));
+  const int per = kItemsPerWave * kw;
+  return max(1, min(a.n_split, (items + per - 1) / per));
 }
 
 template <int D>
@@ -108,6 +135,9 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   const int hb = *a.hist_base;
   const int pl = a.plen[p];
   const int hv = min(hb + t + 1, static_cast<int>(a.ldh));
+  // sliding window (Gemma-2 even layers): key position > qpos - window; prefix key j sits at
+  // position j, history slot j at pl + j, the query at pl + hb + t
+  const int kmin_pos = a.window > 0 ? pl + hb + t - a.window + 1 : INT32_MIN;
 
   // the tile's streams (wave-uniform)
   const int rt0 = r0 + qt * 16, rt1 = min(rt0 + 15, M - 1);
@@ -116,6 +146,8 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
   const int nbp = (pl + kKeyBlock - 1) / kKeyBlock;
   const int n_items = nbp + (b_hi - b_lo + 1) * nbh;
+  const int n_used = a.n_split == 1 ? 1 : splits_used(a, M, r0, nbp, hb);
+  if (split >= n_used) return;                       // whole workgroup: uniform
 
   bf16x8 qf[NDS];
   {
@@ -137,19 +169,20 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   float m = -INFINITY, l = 0.0f;
 
   if (active) {
-    const int nslot = a.n_split * kw;
+    const int nslot = n_used * kw;
     for (int it = split * kw + ks; it < n_items; it += nslot) {
       const __bf16* kbase;
       const __bf16* vbase;
       int64_t ldv;
-      int kb, lim;
+      int kb, lim, pos0;
       if (it < nbp) {
         kb = it * kKeyBlock;
-        const int64_t ph = static_cast<int64_t>(p) * a.Hkv + g;
-        kbase = a.kp + ph * a.ldp * D;
-        vbase = a.vtp + ph * D * a.ldp;
+        const int64_t po = a.poff[p];
+        kbase = a.kp + (static_cast<int64_t>(g) * a.ldp + po) * D;
+        vbase = a.vtp + static_cast<int64_t>(g) * D * a.ldp + po;
         ldv = a.ldp;
         lim = vrow ? pl : 0;
+        pos0 = 0;
       } else {
         const int ih = it - nbp;
         const int bb = b_lo + ih / nbh;
@@ -159,6 +192,7 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
         vbase = a.vth + sh * D * a.ldh;
         ldv = a.ldh;
         lim = (vrow && bb == b) ? hv : 0;
+        pos0 = pl;
       }
       // S^T tiles: keys kb + [0, 16) and kb + [16, 32)
       f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
@@ -184,7 +218,7 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
         float x = y[i] * a.scale;
         if (a.softcap > 0.0f) x = softcap_fn(x, a.softcap, a.inv_softcap);
         x *= kLog2e;
-        y[i] = key < lim ? x : -INFINITY;
+        y[i] = (key < lim && pos0 + key >= kmin_pos) ? x : -INFINITY;
         bm = fmaxf(bm, y[i]);
       }
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
@@ -287,15 +321,18 @@ __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) 
   const int M = a.n_str * a.T * a.rep;
   const int r0 = qg * kGroupRows;
   const int nrows = min(kGroupRows, M - r0);
+  const int p = a.gpfx ? a.gpfx[gi] : gi;
+  const int nbp = (a.plen[p] + kKeyBlock - 1) / kKeyBlock;
+  const int n_used = splits_used(a, M, r0, nbp, *a.hist_base);
   const float* base = a.part + (static_cast<int64_t>(pg) * a.n_qg + qg) * a.n_split * kGroupRows * LDSW;
   for (int item = threadIdx.x; item < nrows * NC; item += kAttnThreads) {
     const int rl = item / NC, c4 = item % NC;
     float mt = -INFINITY;
-    for (int sp = 0; sp < a.n_split; ++sp) mt = fmaxf(mt, base[(sp * kGroupRows + rl) * LDSW + D]);
+    for (int sp = 0; sp < n_used; ++sp) mt = fmaxf(mt, base[(sp * kGroupRows + rl) * LDSW + D]);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     float l = 0.0f;
     if (mt != -INFINITY) {
-      for (int sp = 0; sp < a.n_split; ++sp) {
+      for (int sp = 0; sp < n_used; ++sp) {
         const float* pr = base + (sp * kGroupRows + rl) * LDSW;
         const float c = __builtin_amdgcn_exp2f(pr[D] - mt);
         l = fmaf(pr[D + 1], c, l);
@@ -371,18 +408,51 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
   dst[i + half] = static_cast<__bf16>(y2);
 }
 
-int attn_plan(int32_t n_grp, int32_t n_str, int32_t T, int32_t Hkv, int32_t rep, int64_t ldp,
-              int32_t* n_qg, int32_t* n_split) {
+// Beam reordering of the per-stream history: dst[l][s] = src[l][parent[s]] for the filled
+// slots only (j < *hist_base; V rows rounded up to 8 slots).  One workgroup per (layer,
+// stream), 16-byte vectors; the unfilled capacity is never moved.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void hist_gather_kernel(
+    const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
+    __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
+    int64_t S, int32_t Hkv, int32_t ldh, int32_t D) {
+  const int64_t l = blockIdx.x / S, s = blockIdx.x % S;
+  const int hb = min(*hist_base, ldh);
+  if (hb <= 0) return;
+  const int64_t p = parent[s];
+  const int64_t per = static_cast<int64_t>(Hkv) * ldh * D;         // elements per (l, s)
+  const int64_t so = (l * S + p) * per, dn = (l * S + s) * per;
+  // K: per head hb * D contiguous elements
+  const int kv = hb * D / 8;                                        // vectors per head
+  for (int i = threadIdx.x; i < Hkv * kv; i += 256) {
+    const int g = i / kv, v = i % kv;
+    const int64_t o = static_cast<int64_t>(g) * ldh * D + 8 * static_cast<int64_t>(v);
+    *reinterpret_cast<u32x4_t*>(dst_k + dn + o) = *reinterpret_cast<const u32x4_t*>(src_k + so + o);
+  }
+  // V^T: per (head, d) row the first ceil8(hb) slots
+  const int vv = (hb + 7) / 8;
+  for (int i = threadIdx.x; i < Hkv * D * vv; i += 256) {
+    const int row = i / vv, v = i % vv;
+    const int64_t o = static_cast<int64_t>(row) * ldh + 8 * v;
+    *reinterpret_cast<u32x4_t*>(dst_v + dn + o) = *reinterpret_cast<const u32x4_t*>(src_v + so + o);
+  }
+}
+
+int attn_plan(int32_t n_grp, int32_t n_str, int32_t T, int32_t Hkv, int32_t rep, int64_t max_plen,
+              int64_t ldh, int32_t* n_qg, int32_t* n_split) {
   const int64_t M = static_cast<int64_t>(n_str) * T * rep;
   const int64_t qg = (M + kGroupRows - 1) / kGroupRows;
   const int64_t base = static_cast<int64_t>(n_grp) * Hkv * qg;
   if (qg > 0x7fffffff || base > 0x7fffffff) return -1;
   *n_qg = static_cast<int32_t>(qg);
   int64_t ns = 1;
-  if (base < 512) {
-    const int64_t want = (512 + base - 1) / base;
-    const int64_t blocks = std::max<int64_t>(1, ldp / kKeyBlock / 2);
-    ns = std::min<int64_t>(std::min<int64_t>(want, blocks), kMaxSplit);
+  if (base < 1024) {
+    // an upper bound of the splits any (group, head, query group) uses: every prefix
+    // block plus the history blocks of the <= 16 streams of a tile, kItemsPerWave per wave
+    const int64_t streams = std::min<int64_t>(16, std::max<int64_t>(1, 16 / std::max<int64_t>(1, static_cast<int64_t>(T) * rep)));
+    const int64_t items = (max_plen + kKeyBlock - 1) / kKeyBlock + streams * (ldh / kKeyBlock);
+    ns = std::min<int64_t>((items + kItemsPerWave - 1) / kItemsPerWave, kMaxSplit);
   }
   *n_split = static_cast<int32_t>(std::max<int64_t>(ns, 1));
   return 0;
@@ -393,19 +463,22 @@ int attn_plan(int32_t n_grp, int32_t n_str, int32_t T, int32_t Hkv, int32_t rep,
 extern "C" {
 
 size_t cs_prefix_attention_workspace_size(int32_t n_groups, int32_t n_str, int32_t T, int32_t H,
-                                          int32_t Hkv, int32_t D, int64_t ld_prefix) {
+                                          int32_t Hkv, int32_t D, int32_t max_prefix_len,
+                                          int64_t ld_hist) {
   if (n_groups <= 0 || n_str <= 0 || T <= 0 || Hkv <= 0 || H % Hkv != 0) return 0;
   int32_t nqg = 0, ns = 0;
-  if (attn_plan(n_groups, n_str, T, Hkv, H / Hkv, ld_prefix, &nqg, &ns) != 0 || ns == 1) return 0;
+  if (attn_plan(n_groups, n_str, T, Hkv, H / Hkv, max_prefix_len, ld_hist, &nqg, &ns) != 0 || ns == 1)
+    return 0;
   return static_cast<size_t>(n_groups) * Hkv * nqg * ns * kGroupRows * (D + 2) * sizeof(float);
 }
 
 int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
-                        int64_t ld_prefix, const int32_t* prefix_len, const int32_t* group_prefix,
-                        int32_t n_groups, const void* k_hist, const void* vt_hist, int64_t ld_hist,
+                        int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
+                        int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                        const void* k_hist, const void* vt_hist, int64_t ld_hist,
                         const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
-                        int32_t D, float scale, float softcap, void* out, void* workspace,
-                        size_t workspace_bytes, cs_stream_t stream) {
+                        int32_t D, float scale, float softcap, int32_t window, void* out,
+                        void* workspace, size_t workspace_bytes, cs_stream_t stream) {
   if (n_groups < 0 || n_str < 0 || T < 0) return fail(CS_ERR_INVALID, "cs_prefix_attention: negative size");
   if (n_groups == 0 || n_str == 0 || T == 0) return CS_OK;
   if (Hkv <= 0 || H <= 0 || H % Hkv != 0 || H / Hkv > 64)
@@ -414,13 +487,17 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
     return fail(CS_ERR_INVALID, "cs_prefix_attention: head_dim must be 64, 128 or 256");
   if (ld_prefix <= 0 || ld_prefix % kKeyBlock != 0 || ld_hist <= 0 || ld_hist % kKeyBlock != 0)
     return fail(CS_ERR_INVALID, "cs_prefix_attention: ld_prefix / ld_hist must be positive multiples of 32");
-  if (!q || !k_prefix || !vt_prefix || !prefix_len || !k_hist || !vt_hist || !hist_base || !out)
+  if (max_prefix_len < 0 || max_prefix_len > ld_prefix)
+    return fail(CS_ERR_INVALID, "cs_prefix_attention: max_prefix_len outside [0, ld_prefix]");
+  if (!q || !k_prefix || !vt_prefix || !prefix_off || !prefix_len || !k_hist || !vt_hist ||
+      !hist_base || !out)
     return fail(CS_ERR_INVALID, "cs_prefix_attention: NULL pointer");
   if (!(scale > 0.0f) || softcap < 0.0f) return fail(CS_ERR_INVALID, "cs_prefix_attention: bad scale / softcap");
   AttnParams a;
   a.q = static_cast<const __bf16*>(q);
   a.kp = static_cast<const __bf16*>(k_prefix);
   a.vtp = static_cast<const __bf16*>(vt_prefix);
+  a.poff = prefix_off;
   a.plen = prefix_len;
   a.gpfx = group_prefix;
   a.kh = static_cast<const __bf16*>(k_hist);
@@ -438,13 +515,15 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   a.scale = scale;
   a.softcap = softcap;
   a.inv_softcap = softcap > 0.0f ? 1.0f / softcap : 0.0f;
-  if (attn_plan(n_groups, n_str, T, Hkv, a.rep, ld_prefix, &a.n_qg, &a.n_split) != 0)
+  a.window = window > 0 ? window : 0;
+  if (attn_plan(n_groups, n_str, T, Hkv, a.rep, max_prefix_len, ld_hist, &a.n_qg, &a.n_split) != 0)
     return fail(CS_ERR_INVALID, "cs_prefix_attention: too many query rows");
   const int64_t nwg = static_cast<int64_t>(n_groups) * Hkv * a.n_qg * a.n_split;
   if (nwg > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_prefix_attention: grid too large");
   a.part = nullptr;
   if (a.n_split > 1) {
-    const size_t need = cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, ld_prefix);
+    const size_t need =
+        cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, max_prefix_len, ld_hist);
     if (!workspace || workspace_bytes < need)
       return fail(CS_ERR_WORKSPACE, "cs_prefix_attention: workspace smaller than "
                                     "cs_prefix_attention_workspace_size()");
@@ -469,6 +548,25 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   }
 #undef CS_ATTN_LAUNCH
   return check_launch("cs_prefix_attention");
+}
+
+int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
+                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S,
+                   int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream) {
+  if (L < 0 || S < 0 || Hkv <= 0 || D <= 0) return fail(CS_ERR_INVALID, "cs_hist_gather: bad shape");
+  if (L == 0 || S == 0) return CS_OK;
+  if (!src_k || !dst_k || !src_vt || !dst_vt || !parent || !hist_base)
+    return fail(CS_ERR_INVALID, "cs_hist_gather: NULL pointer");
+  if (ld_hist <= 0 || ld_hist % 8 || D % 8)
+    return fail(CS_ERR_INVALID, "cs_hist_gather: ld_hist and D must be positive multiples of 8");
+  if (src_k == dst_k || src_vt == dst_vt)
+    return fail(CS_ERR_INVALID, "cs_hist_gather: source and destination must differ (ping-pong)");
+  if (L * S > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_hist_gather: grid too large");
+  hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const __bf16*>(src_k),
+                     static_cast<__bf16*>(dst_k), static_cast<const __bf16*>(src_vt),
+                     static_cast<__bf16*>(dst_vt), parent, hist_base, S, Hkv, ld_hist, D);
+  return check_launch("cs_hist_gather");
 }
 
 int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const int32_t* prefix_len,

@@ -1,0 +1,167 @@
+// norm.hip — the per-token elementwise work of the stream forward, fused:
+//
+//   add_rms_kernel    residual add + RMSNorm in one pass over a row: s = a + b (rounded to
+//                     bf16, the residual stream), y = s * rsqrt(mean(s^2) + eps) * w
+//                     (Llama-3) or * (1 + w) (Gemma-2), fp32 statistics.  Replaces the
+//                     add + 1 (Llama) / 7 (Gemma: cast, pow, mean, add, rsqrt, mul, mul,
+//                     cast) launches of the PyTorch layer.
+//   gated_act_kernel  act(gate) * up for the gated MLP (SiLU for Llama-3, tanh-GeLU for
+//                     Gemma-2) in one pass; the activation is rounded to bf16 before the
+//                     product, as the PyTorch pair of launches does.
+//
+// Both are HBM-streaming (16-byte vector loads, one workgroup per row / per row slice);
+// on decode-sized batches what they save is launches (each costs ~4-5 us of GPU time
+// even inside a captured graph).
+#include "cs_kernels.cuh"
+
+namespace {
+
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+
+// fp32 -> bf16, round to nearest even (NaN kept quiet)
+__device__ __forceinline__ uint16_t to_bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40);
+  return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+constexpr int kNormThreads = 256;
+
+// one workgroup per row; VPT 16-byte vectors per thread (d <= 256 * 8 * VPT).  s_out may
+// alias a (the residual stream updated in place): every element is loaded before the
+// barrier and stored after it by the same thread.
+template <int VPT>
+__global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
+    const uint16_t* a, int64_t lda, const uint16_t* __restrict__ b, int64_t ldb,
+    uint16_t* s_out, int64_t lds, const uint16_t* __restrict__ w, int64_t d,
+    float eps, int plus_one, uint16_t* __restrict__ y, int64_t ldy) {
+  const int64_t r = blockIdx.x;
+  const int nv = static_cast<int>(d >> 3);
+  u16x8 sv[VPT];
+  float ss = 0.0f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = threadIdx.x + k * kNormThreads;
+    if (v < nv) {
+      u16x8 x = *reinterpret_cast<const u16x8*>(a + r * lda + 8 * v);
+      if (b) {
+        const u16x8 o = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = to_bf(bf(x[e]) + bf(o[e]));
+      }
+      sv[k] = x;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss = fmaf(bf(x[e]), bf(x[e]), ss);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  __shared__ float red[kNormThreads / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  float tot = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kNormThreads / 64; ++i) tot += red[i];
+  const float inv = 1.0f / sqrtf(tot / static_cast<float>(d) + eps);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = threadIdx.x + k * kNormThreads;
+    if (v < nv) {
+      if (s_out) *reinterpret_cast<u16x8*>(s_out + r * lds + 8 * v) = sv[k];
+      const u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * v);
+      u16x8 out;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = plus_one ? 1.0f + bf(wv[e]) : bf(wv[e]);
+        // Llama (F.rms_norm): x * inv * w, one rounding; Gemma: (x * inv) * (1 + w)
+        out[e] = to_bf((bf(sv[k][e]) * inv) * g);
+      }
+      *reinterpret_cast<u16x8*>(y + r * ldy + 8 * v) = out;
+    }
+  }
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+// grid rows * nb (nb = ceil(F / (8 * 256)) blocks per row): 8 outputs per thread
+__global__ __launch_bounds__(kNormThreads) void gated_act_kernel(
+    const uint16_t* __restrict__ gate, int64_t ldg, const uint16_t* __restrict__ up, int64_t ldu,
+    int64_t F, int nb, int act, uint16_t* __restrict__ out, int64_t ldo) {
+  const int64_t r = blockIdx.x / nb;
+  const int64_t j = (static_cast<int64_t>(blockIdx.x % nb) * kNormThreads + threadIdx.x) * 8;
+  if (j >= F) return;
+  const u16x8 g = *reinterpret_cast<const u16x8*>(gate + r * ldg + j);
+  const u16x8 u = *reinterpret_cast<const u16x8*>(up + r * ldu + j);
+  u16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = bf(g[e]);
+    const uint16_t a = to_bf(act ? gelu_tanh_f(x) : silu_f(x));
+    o[e] = to_bf(bf(a) * bf(u[e]));
+  }
+  *reinterpret_cast<u16x8*>(out + r * ldo + j) = o;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, void* s_out,
+                    int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
+                    int plus_one, void* y, int64_t ldy, cs_stream_t stream) {
+  if (rows < 0 || d <= 0) return fail(CS_ERR_INVALID, "cs_add_rms_norm: bad shape");
+  if (rows == 0) return CS_OK;
+  if (!a || !weight || !y) return fail(CS_ERR_INVALID, "cs_add_rms_norm: NULL pointer");
+  if (d % 8 != 0 || d > 16 * 8 * kNormThreads)
+    return fail(CS_ERR_INVALID, "cs_add_rms_norm: d must be a multiple of 8 and <= 32768");
+  if (lda < d || ldy < d || (b && ldb < d) || (s_out && lds < d) || lda % 8 || ldy % 8 ||
+      (b && ldb % 8) || (s_out && lds % 8))
+    return fail(CS_ERR_INVALID, "cs_add_rms_norm: leading dimensions must be >= d and multiples of 8");
+  const uint16_t* A = static_cast<const uint16_t*>(a);
+  const uint16_t* B = static_cast<const uint16_t*>(b);
+  uint16_t* S = static_cast<uint16_t*>(s_out);
+  const uint16_t* W = static_cast<const uint16_t*>(weight);
+  uint16_t* Y = static_cast<uint16_t*>(y);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nv = static_cast<int>(d / 8);
+  const dim3 grid(static_cast<uint32_t>(rows));
+  if (nv <= kNormThreads) {
+    hipLaunchKernelGGL(add_rms_kernel<1>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
+                       d, eps, plus_one, Y, ldy);
+  } else if (nv <= 2 * kNormThreads) {
+    hipLaunchKernelGGL(add_rms_kernel<2>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
+                       d, eps, plus_one, Y, ldy);
+  } else if (nv <= 4 * kNormThreads) {
+    hipLaunchKernelGGL(add_rms_kernel<4>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
+                       d, eps, plus_one, Y, ldy);
+  } else {
+    hipLaunchKernelGGL(add_rms_kernel<16>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
+                       d, eps, plus_one, Y, ldy);
+  }
+  return check_launch("cs_add_rms_norm");
+}
+
+int cs_gated_act(const void* gate, int64_t ld_gate, const void* up, int64_t ld_up, int64_t rows,
+                 int64_t F, int act, void* out, int64_t ld_out, cs_stream_t stream) {
+  if (rows < 0 || F <= 0) return fail(CS_ERR_INVALID, "cs_gated_act: bad shape");
+  if (rows == 0) return CS_OK;
+  if (!gate || !up || !out) return fail(CS_ERR_INVALID, "cs_gated_act: NULL pointer");
+  if (act != 0 && act != 1) return fail(CS_ERR_INVALID, "cs_gated_act: act must be 0 (SiLU) or 1 (tanh-GeLU)");
+  if (F % 8 || ld_gate % 8 || ld_up % 8 || ld_out % 8 || ld_gate < F || ld_up < F || ld_out < F)
+    return fail(CS_ERR_INVALID, "cs_gated_act: F and leading dimensions must be multiples of 8, >= F");
+  const int64_t nb = (F / 8 + kNormThreads - 1) / kNormThreads;
+  if (rows * nb > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gated_act: grid too large");
+  hipLaunchKernelGGL(gated_act_kernel, dim3(static_cast<uint32_t>(rows * nb)), dim3(kNormThreads), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(gate), ld_gate,
+                     static_cast<const uint16_t*>(up), ld_up, F, static_cast<int>(nb), act,
+                     static_cast<uint16_t*>(out), ld_out);
+  return check_launch("cs_gated_act");
+}
+
+}  // extern "C"

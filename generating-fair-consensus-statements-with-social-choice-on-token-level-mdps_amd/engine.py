@@ -55,6 +55,25 @@ def _pad(seqs: Sequence[Sequence[int]], device, fill: int = 0):
     return out.to(device, non_blocking=True), lens.to(device, non_blocking=True)
 
 
+def _uniform_groups(owner: Sequence[int]):
+    """(prefix index of each group, streams per group) when ``owner`` is contiguous runs of
+    equal length (agent-major agent x candidate batches), else None."""
+    R = len(owner)
+    if R == 0:
+        return None
+    n = 1
+    while n < R and owner[n] == owner[0]:
+        n += 1
+    if R % n:
+        return None
+    groups = [int(owner[i]) for i in range(0, R, n)]
+    for gi, g in enumerate(groups):
+        base = gi * n
+        if any(owner[base + j] != g for j in range(n)):
+            return None
+    return groups, n
+
+
 def _id_matrix(rows) -> np.ndarray:
     """Token ids of stored rows as one [n, width] array, right-padded with -1 (never a
     token id, so it ends every common run)."""
@@ -91,8 +110,14 @@ class ScoringEngine:
 
     def __init__(self, model: Model, max_rows_per_chunk: int = 32768,
                  max_streams_per_chunk: int = 1024, reuse_caches: Optional[int] = None,
-                 reuse_min_tokens: int = 16, reuse_max_tokens: int = 1 << 18):
+                 reuse_min_tokens: int = 16, reuse_max_tokens: int = 1 << 18,
+                 fused_scoring: bool = True, fused_max_rows: int = 1 << 17):
         self.model = model
+        # bf16 models score agent x candidate batches on the stream kernels
+        # (_score_fused); fused_max_rows bounds a chunk's logits block (2^17 rows of the
+        # 128,256 Llama-3 vocab = 34 GB of bf16 logits, an eighth of the HBM)
+        self.fused_scoring = bool(fused_scoring)
+        self.fused_max_rows = int(fused_max_rows)
         self.device = model.device
         self.softcap = model.cfg.final_softcap
         self.max_rows = max_rows_per_chunk
@@ -138,6 +163,67 @@ class ScoringEngine:
                 while sum(c.ids.numel() for c, _ in self._store) > self.reuse_max_tokens:
                     del self._store[0]
         return cache
+
+    @torch.no_grad()
+    def prefill_streams(self, prefixes: Sequence[Sequence[int]], bucket_ratio: float = 1.25,
+                        bucket_tokens: int = 1 << 16) -> StreamPrefix:
+        """Prefill for the stream decode (bf16 models): prompts of very different lengths
+        (64 agent prompts of ~200 tokens and a reference prompt listing every opinion)
+        are prefilled in length buckets (padding <= bucket_ratio, <= bucket_tokens padded
+        tokens per forward) and their K/V written straight into the ragged FusedPrefix
+        buffers — nothing is padded to the longest prompt."""
+        if any(len(p) == 0 for p in prefixes):
+            raise ValueError("every prefix needs at least one token (BOS)")
+        m = self.model
+        c = m.cfg
+        dev = self.device
+        lens = [len(p) for p in prefixes]
+        n = len(prefixes)
+        off = _offsets32(lens)
+        Lp = off[-1]
+        ks = [torch.zeros(c.n_kv_heads, Lp, c.head_dim, dtype=m.dtype, device=dev)
+              for _ in range(c.n_layers)]
+        vts = [torch.zeros(c.n_kv_heads, c.head_dim, Lp, dtype=m.dtype, device=dev)
+               for _ in range(c.n_layers)]
+        last = torch.empty(n, c.d_model, dtype=m.dtype, device=dev)
+        order = sorted(range(n), key=lambda i: lens[i])
+        j = 0
+        while j < n:
+            b = [order[j]]
+            j += 1
+            while (j < n and lens[order[j]] <= bucket_ratio * lens[b[0]]
+                   and (len(b) + 1) * lens[order[j]] <= bucket_tokens):
+                b.append(order[j])
+                j += 1
+            ids, lt = _pad([prefixes[i] for i in b], dev)
+            nb, Pb = ids.shape
+            if m.fused_ok():
+                # the prompts as streams over an empty prefix: causal attention over their
+                # own tokens on cs_prefix_attention (O(T) memory; no T x T score matrix
+                # for a several-thousand-token reference prompt)
+                ldh = _ceil32(Pb)
+                hk = [torch.zeros(nb, c.n_kv_heads, ldh, c.head_dim, dtype=m.dtype, device=dev)
+                      for _ in range(c.n_layers)]
+                hv = [torch.zeros(nb, c.n_kv_heads, c.head_dim, ldh, dtype=m.dtype, device=dev)
+                      for _ in range(c.n_layers)]
+                h = m.forward_streams(ids.reshape(-1), _empty_prefix(m), hk, hv,
+                                      torch.zeros(1, dtype=torch.int32, device=dev), 1, Pb,
+                                      group_prefix=torch.zeros(nb, dtype=torch.int32, device=dev))
+                h = h.view(nb, Pb, -1)
+                kv = [(k, v.transpose(2, 3)) for k, v in zip(hk, hv)]
+            else:
+                kv, h, _ = m.prefill(ids, lt)
+            last[torch.as_tensor(b, device=dev)] = h[torch.arange(nb, device=dev), lt - 1]
+            for li, (k, v) in enumerate(kv):
+                for r, i in enumerate(b):
+                    ks[li][:, off[i]:off[i] + lens[i]] = k[r, :, :lens[i]]
+                    vts[li][:, :, off[i]:off[i] + lens[i]] = v[r, :, :lens[i]].transpose(1, 2)
+            del kv, h
+        fp = FusedPrefix(k=ks, vt=vts, off=torch.as_tensor(off[:-1], dtype=torch.int64, device=dev),
+                         lengths=torch.as_tensor(lens, dtype=torch.int32, device=dev),
+                         max_len=max(lens))
+        return StreamPrefix(fused=fp, last_hidden=last,
+                            lengths=torch.as_tensor(lens, dtype=torch.long, device=dev), lens=lens)
 
     def reset_prefix_store(self) -> None:
         with self._store_lock:
@@ -260,6 +346,11 @@ class ScoringEngine:
         R = len(conts)
         lens = [len(c) for c in conts]
         out = torch.empty(sum(lens), dtype=torch.float32, device=self.device)
+        grouping = _uniform_groups(owner)
+        if (grouping is not None and self.fused_scoring and R and max(lens) > 1 and
+                self.model.fused_ok(int(cache.ids.shape[1]) + max(lens))):
+            self._score_fused(cache, grouping, conts, lens, out)
+            return out
         # chunk streams so that the logits block stays bounded
         r0, o0 = 0, 0
         while r0 < R:
@@ -271,6 +362,55 @@ class ScoringEngine:
             self._score_chunk(cache, owner[r0:r1], conts[r0:r1], out[o0:o0 + rows])
             r0, o0 = r1, o0 + rows
         return out
+
+    def _score_fused(self, cache, grouping, conts, lens, out):
+        """Scoring over shared prefixes on the stream kernels: every chunk is whole groups
+        (all n_str continuations of some prefixes), padded to the longest continuation;
+        continuation tokens 0..T-2 run through forward_streams (each stream's own tokens
+        in one reusable history buffer, the prefix K/V read once per (prefix, head) per
+        layer), token 0 is scored from the prefix's last hidden, rows -> LM head ->
+        cs_logsoftmax_gather.  Replaces the per-stream gathered [prefix | tokens] contexts
+        of _score_chunk (one copy of each prefix per candidate per layer)."""
+        dev = self.device
+        m = self.model
+        c = m.cfg
+        groups, n_str = grouping
+        pfx = fused_prefix(cache)          # once per call, shared by the chunks
+        T = max(lens)
+        per_group = n_str * T
+        g_per_chunk = max(1, self.fused_max_rows // max(per_group, 1))
+        o0 = 0
+        for g0 in range(0, len(groups), g_per_chunk):
+            gs = groups[g0:g0 + g_per_chunk]
+            S = len(gs) * n_str
+            cs = conts[g0 * n_str:g0 * n_str + S]
+            ls = lens[g0 * n_str:g0 * n_str + S]
+            toks, lens_t = _pad(cs, dev)
+            Tc = toks.shape[1]
+            own = torch.as_tensor(gs, dtype=torch.long, device=dev).repeat_interleave(n_str)
+            last = cache.last_hidden[own]
+            if Tc > 1:
+                ldh = _ceil32(Tc - 1)
+                hk = torch.zeros(S, c.n_kv_heads, ldh, c.head_dim, dtype=m.dtype, device=dev)
+                hv = torch.zeros(S, c.n_kv_heads, c.head_dim, ldh, dtype=m.dtype, device=dev)
+                hb = torch.zeros(1, dtype=torch.int32, device=dev)
+                gp = torch.as_tensor(gs, dtype=torch.int32, device=dev)
+                # one history buffer serves every layer: a chunk's K/V are not kept
+                h = m.forward_streams(toks[:, :Tc - 1].reshape(-1), pfx, [hk] * c.n_layers,
+                                      [hv] * c.n_layers, hb, n_str, Tc - 1, group_prefix=gp)
+                hpad = torch.cat([last[:, None, :], h.view(S, Tc - 1, -1)], dim=1)   # [S, Tc, d]
+                del h, hk, hv
+            else:
+                hpad = last[:, None, :]
+            rows = sum(ls)
+            if all(L == Tc for L in ls):
+                rows_h, rows_t = hpad.reshape(S * Tc, -1), toks.reshape(-1, 1)
+            else:
+                idx_r = torch.repeat_interleave(torch.arange(S, device=dev), lens_t)
+                idx_t = torch.cat([torch.arange(L, device=dev) for L in ls])
+                rows_h, rows_t = hpad[idx_r, idx_t], toks[idx_r, idx_t][:, None]
+            out[o0:o0 + rows].copy_(self.rows_logprobs(rows_h, rows_t).view(-1))
+            o0 += rows
 
     def _score_chunk(self, cache, owner, conts, out):
         dev = self.device
@@ -452,27 +592,61 @@ def _ceil32(n: int) -> int:
 
 @dataclass
 class FusedPrefix:
-    """Prefix K/V in the cs_prefix_attention layouts (include/consensus_scoring.h)."""
-    k: list                     # per layer [n_prefix, Hkv, ldp, D]
-    vt: list                    # per layer [n_prefix, Hkv, D, ldp] (V transposed)
+    """Prefix K/V in the cs_prefix_attention layouts (include/consensus_scoring.h): all
+    prefixes of one prefill in one ragged buffer per layer, prefix p's keys at rows
+    off[p] .. off[p] + lengths[p] (off[p] % 32 == 0, each prefix padded to 32 keys)."""
+    k: list                     # per layer [Hkv, Lp, D]
+    vt: list                    # per layer [Hkv, D, Lp] (V transposed: key-contiguous rows)
+    off: torch.Tensor           # [n_prefix] int64 (device)
     lengths: torch.Tensor       # [n_prefix] int32 (device)
-    ldp: int
+    max_len: int                # host copy of max(lengths)
+
+
+@dataclass
+class StreamPrefix:
+    """What the stream decode needs of a prefill (engine.prefill_streams): the ragged
+    prefix K/V, each prefix's last final-norm hidden and its length."""
+    fused: FusedPrefix
+    last_hidden: torch.Tensor   # [n_prefix, d]
+    lengths: torch.Tensor       # [n_prefix] int64 (device)
+    lens: List[int]             # host copy
+
+
+def _empty_prefix(m: Model) -> FusedPrefix:
+    """One prefix of length 0 (prefill of prompts as streams of their own tokens)."""
+    c = m.cfg
+    dev = m.device
+    return FusedPrefix(
+        k=[torch.zeros(c.n_kv_heads, 32, c.head_dim, dtype=m.dtype, device=dev)] * c.n_layers,
+        vt=[torch.zeros(c.n_kv_heads, c.head_dim, 32, dtype=m.dtype, device=dev)] * c.n_layers,
+        off=torch.zeros(1, dtype=torch.int64, device=dev),
+        lengths=torch.zeros(1, dtype=torch.int32, device=dev), max_len=0)
+
+
+def _offsets32(lens: Sequence[int]) -> List[int]:
+    off, o = [], 0
+    for n in lens:
+        off.append(o)
+        o += _ceil32(n)
+    return off + [o]
 
 
 def fused_prefix(cache: PrefixCache) -> FusedPrefix:
-    """The prefill's K/V re-laid for the stream kernels: key capacity rounded up to 32
-    (zero-filled), V transposed so its rows are key-contiguous.  One copy per prefill."""
+    """A padded prefill's K/V re-laid for the stream kernels (prefix p at rows p * ldp,
+    ldp = the padded length rounded up to 32, zero-filled; V transposed).  One copy."""
     n, Hkv, P, D = cache.kv[0][0].shape
     ldp = _ceil32(P)
     ks, vts = [], []
     for k, v in cache.kv:
-        kp = torch.zeros(n, Hkv, ldp, D, dtype=k.dtype, device=k.device)
-        kp[:, :, :P] = k
-        vt = torch.zeros(n, Hkv, D, ldp, dtype=v.dtype, device=v.device)
-        vt[..., :P] = v.transpose(2, 3)
-        ks.append(kp)
-        vts.append(vt)
-    return FusedPrefix(k=ks, vt=vts, lengths=cache.lengths.to(torch.int32), ldp=ldp)
+        kp = torch.zeros(Hkv, n, ldp, D, dtype=k.dtype, device=k.device)
+        kp[:, :, :P] = k.transpose(0, 1)
+        vt = torch.zeros(Hkv, D, n, ldp, dtype=v.dtype, device=v.device)
+        vt[..., :P] = v.permute(1, 3, 0, 2)
+        ks.append(kp.view(Hkv, n * ldp, D))
+        vts.append(vt.view(Hkv, D, n * ldp))
+    dev = cache.lengths.device
+    return FusedPrefix(k=ks, vt=vts, off=torch.arange(n, device=dev, dtype=torch.int64) * ldp,
+                       lengths=cache.lengths.to(torch.int32), max_len=P)
 
 
 class DecodeState:
@@ -484,7 +658,7 @@ class DecodeState:
     generated K/V lives in a preallocated history buffer [S, Hkv, ldh, D] (V transposed),
     slot t = the token of step t; the prefix K/V is shared by the stream's n_beams
     siblings through cs_prefix_attention.  ``advance`` = gather the parents' histories
-    (one index_select per buffer into the other half of a ping-pong pair), forward the new
+    (cs_hist_gather: the filled slots only, into the other half of a ping-pong pair), forward the new
     tokens with hist_base = t read from device memory, keep the final-norm hidden.  After
     the first (eager) advance each parity's step is captured once in a hipGraph and
     replayed, so a decode step costs one graph launch plus its inputs' copies; ``post``
@@ -495,23 +669,25 @@ class DecodeState:
     (src/methods/beam_search.py:491-538 through src/utils.py:249-259) as one token per
     stream per step."""
 
-    def __init__(self, engine: "ScoringEngine", cache: PrefixCache, n_prefix: int, n_beams: int,
+    def __init__(self, engine: "ScoringEngine", cache, n_prefix: int, n_beams: int,
                  max_steps: int, use_graphs: bool = True):
+        """cache: a StreamPrefix (engine.prefill_streams) or a PrefixCache (re-laid)."""
         self.e = engine
         m = engine.model
         c = m.cfg
         self.P, self.B = int(n_prefix), int(n_beams)
         self.S = self.P * self.B
         dev = engine.device
-        self.pfx = fused_prefix(cache)
+        self.pfx = cache.fused if isinstance(cache, StreamPrefix) else fused_prefix(cache)
         self.ldh = _ceil32(max_steps)
         self.max_steps = int(max_steps)
 
         def buffers():
-            return ([torch.zeros(self.S, c.n_kv_heads, self.ldh, c.head_dim, dtype=m.dtype, device=dev)
-                     for _ in range(c.n_layers)],
-                    [torch.zeros(self.S, c.n_kv_heads, c.head_dim, self.ldh, dtype=m.dtype, device=dev)
-                     for _ in range(c.n_layers)])
+            # all layers in one tensor each, so a step's parent gather is 2 launches, not 2L
+            return (torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
+                                dtype=m.dtype, device=dev),
+                    torch.zeros(c.n_layers, self.S, c.n_kv_heads, c.head_dim, self.ldh,
+                                dtype=m.dtype, device=dev))
 
         self.hist = [buffers(), buffers()]
         self.cur = 0
@@ -532,10 +708,9 @@ class DecodeState:
         m = self.e.model
         old_k, old_v = self.hist[self.cur]
         new_k, new_v = self.hist[1 - self.cur]
-        for i in range(len(old_k)):
-            torch.index_select(old_k[i], 0, self.src, out=new_k[i])
-            torch.index_select(old_v[i], 0, self.src, out=new_v[i])
-        h = m.forward_streams(self.tok, self.pfx, new_k, new_v, self.hist_base, self.B, 1)
+        ops.hist_gather(old_k, new_k, old_v, new_v, self.src, self.hist_base)
+        h = m.forward_streams(self.tok, self.pfx, list(new_k.unbind(0)), list(new_v.unbind(0)),
+                              self.hist_base, self.B, 1)
         self.hidden.copy_(h)
         self.hist_base += 1
         if post is not None:

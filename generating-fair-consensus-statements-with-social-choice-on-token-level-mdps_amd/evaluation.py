@@ -52,6 +52,7 @@ class StatementEvaluator:
         self._judge_requested = include_llm_judge
 
     # --- batched core ---------------------------------------------------------------
+    @runtime.serialized("evaluation_model")
     def agent_utilities(self, statements: List[str], issue: str, agent_opinions: Dict[str, str]):
         """Per (agent, statement): mean log-prob and mean prob, as [A, S] device tensors."""
         engine, tok = runtime.get_engine(self.evaluation_model)

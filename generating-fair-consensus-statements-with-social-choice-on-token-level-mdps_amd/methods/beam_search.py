@@ -30,6 +30,7 @@ order on every rank; rank 0's proposals are used everywhere.
 from __future__ import annotations
 
 import logging
+import time
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -108,6 +109,8 @@ class BeamSearchGenerator(BaseGenerator):
         self.step_log: List[dict] = []
         self.decode_path = None
         self.steps_run = 0
+        self.step_times: List[float] = []     # perf_counter at the start of every step
+        self.prefill_s = 0.0
 
     # --- candidate proposal ------------------------------------------------------
     def _propose(self, st, ref_idx: int, bias: List[int], step_base_seed: Optional[int],
@@ -186,12 +189,16 @@ class BeamSearchGenerator(BaseGenerator):
         ref_user = BEAM["ref_user"].format(issue=issue, opinions_text=opinions_text(agent_opinions))
         ref_prefix = tok.render_raw(f"{BEAM['ref_system']}\n\n{ref_user}")
         all_prefixes = agent_prefixes + [ref_prefix]
-        cache = engine.prefill(all_prefixes)
         bias = (runtime.bias_token_ids(tok, self.bias_against_tokens)
                 if self.use_token_biasing and self.bias_against_tokens else [])
-        max_ctx = max(len(p) for p in all_prefixes) + int(self.max_tokens)
         fused = (self.fused_decode and int(self.max_tokens) > 0 and int(self.beam_width) > 0
-                 and engine.model.fused_ok(max_ctx))
+                 and engine.model.fused_ok())
+        t0 = time.perf_counter()
+        # the stream decode prefills in length buckets into ragged K/V (the reference prompt
+        # lists every opinion and is many times longer than an agent prompt)
+        cache = engine.prefill_streams(all_prefixes) if fused else engine.prefill(all_prefixes)
+        self.prefill_s = time.perf_counter() - t0     # host-side (asynchronous launches)
+        self.step_times = []
         self.step_log = []
         self.steps_run = 0
         if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk:
@@ -221,6 +228,7 @@ class BeamSearchGenerator(BaseGenerator):
             if not beams:
                 break
             self.steps_run += 1
+            self.step_times.append(time.perf_counter())
             step_base_seed = (self.seed + step * self.max_sampling_attempts * len(beams) * (A + 1)
                               if self.seed is not None else None)
             n_live = getattr(st, "n_live", st.n_beams)
@@ -327,6 +335,7 @@ class BeamSearchGenerator(BaseGenerator):
         for step in range(self.max_tokens):
             self.steps_run += 1
             ids_h, order_h, W_h, U_h = host.fetch(ids_buf, order_buf, W_buf, U_buf)
+            self.step_times.append(time.perf_counter())   # this step's results are on the host
             ids_f = ids_h.reshape(-1)
             live = order_h[order_h < n_live * K]                          # beams b < n_live
             tstr = {}

@@ -58,6 +58,7 @@ class BestOfNGenerator(BaseGenerator):
         self.last_agent_rewards: Dict[str, List[float]] = {}
         self.last_welfare: List[float] = []
 
+    @runtime.serialized()
     def generate_statement(self, issue: str, agent_opinions: dict) -> str:
         cfg = self.config
         n = cfg.get("num_best_of_n", cfg.get("n", 3))

@@ -176,6 +176,7 @@ class FiniteLookaheadGenerator(BaseGenerator):
                     cnt[:, p] += e
         return (sums / cnt).to(torch.float32).contiguous()
 
+    @runtime.serialized()
     def generate_statement(self, issue: str, agent_opinions: dict) -> str:
         cfg = self.config
         bf = cfg.get("branching_factor", 2)

@@ -250,6 +250,7 @@ class MCTSGenerator(BaseGenerator):
         return sorted(node.children.values(), key=lambda c: c.visits, reverse=True)[0]
 
     # --- main loop (mcts.py:932-1044) ---------------------------------------------------
+    @runtime.serialized()
     def generate_statement(self, issue: str, agent_opinions: dict) -> str:
         A = len(agent_opinions)
         self.trace = []

@@ -366,21 +366,22 @@ class Model:
 
     def fused_ok(self, max_ctx: int = 0) -> bool:
         """Whether forward_streams (cs_rope_place + cs_prefix_attention) serves this model:
-        bf16 weights on a HIP device, head_dim in {64, 128, 256}, and every context within
-        Gemma-2's sliding window (the kernel attends the whole visible range)."""
+        bf16 weights on a HIP device, head_dim in {64, 128, 256} (Gemma-2's sliding window
+        and attention soft-cap are applied in the kernel).  ``max_ctx`` is kept for callers
+        that size contexts; every length is served."""
         c = self.cfg
         return (self.device.type == "cuda" and self.dtype == torch.bfloat16
                 and c.head_dim in (64, 128, 256) and c.n_heads % c.n_kv_heads == 0
-                and (not c.sliding_window or max_ctx <= c.sliding_window))
+                and c.n_heads // c.n_kv_heads <= 64)
 
     @torch.no_grad()
     def forward_streams(self, tokens: torch.Tensor, pfx, hist_k: List[torch.Tensor],
                         hist_vt: List[torch.Tensor], hist_base: torch.Tensor, n_str: int, T: int,
                         group_prefix: Optional[torch.Tensor] = None) -> torch.Tensor:
         """T new tokens for each of S = n_groups * n_str streams (tokens [S*T], stream-major):
-        stream s = i * n_str + b attends to its group's prefix (pfx.k / pfx.vt / pfx.lengths,
-        the layouts of include/consensus_scoring.h cs_prefix_attention; group i uses prefix
-        group_prefix[i] or i) and to its own history slots [0, hist_base + t] in
+        stream s = i * n_str + b attends to its group's prefix (pfx: engine.FusedPrefix, the
+        ragged layouts of include/consensus_scoring.h cs_prefix_attention; group i uses
+        prefix group_prefix[i] or i) and to its own history slots [0, hist_base + t] in
         hist_k[layer] [S, Hkv, ldh, D] / hist_vt[layer] [S, Hkv, D, ldh]; the new tokens'
         K / V are written to slots hist_base + t.  Per layer: one fused q|k|v GEMM,
         cs_rope_place, cs_prefix_attention, output GEMM, MLP.  No host synchronisation and
@@ -391,27 +392,34 @@ class Model:
         H, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
         n_tok = tokens.shape[0]
         scale = self.attn_scale()
-        h = self._embed(tokens)
+        g2 = c.family == "gemma2"
+        act = "gelu_tanh" if g2 else "silu"
+        eps = c.rms_eps
+        h = self._embed(tokens).contiguous()                 # the residual stream [n_tok, d]
+        # every residual add + RMSNorm is one cs_add_rms_norm launch; h is updated in place
+        x = ops.add_rms_norm(h, self.w["l0.attn_norm"], eps, plus_one=g2)
         for i in range(c.n_layers):
             p = f"l{i}."
-            x = self._rms(h, self.w[p + "attn_norm"])
             qkv = x @ self.wf[p + "qkv"].t()
             q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
             ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
                            hist_k[i], hist_vt[i], group_prefix=group_prefix)
-            o = ops.prefix_attention(q, pfx.k[i], pfx.vt[i], pfx.lengths, hist_k[i], hist_vt[i],
-                                     hist_base, n_str, T, scale=scale, softcap=c.attn_softcap,
+            o = ops.prefix_attention(q, pfx.k[i], pfx.vt[i], pfx.off, pfx.lengths, pfx.max_len,
+                                     hist_k[i], hist_vt[i], hist_base, n_str, T, scale=scale,
+                                     softcap=c.attn_softcap,
+                                     window=c.sliding_window if i % 2 == 0 else 0,
                                      group_prefix=group_prefix)
             o = o.view(n_tok, H * D) @ self.w[p + "wo"].t()
-            if c.family == "gemma2":
-                o = self._rms(o, self.w[p + "post_attn_norm"])
-            h = h + o
-            x = self._rms(h, self.w[p + "mlp_norm"])
-            y = self._mlp(i, x)
-            if c.family == "gemma2":
-                y = self._rms(y, self.w[p + "post_mlp_norm"])
-            h = h + y
-        return self._rms(h, self.w["norm"])
+            if g2:
+                o = ops.add_rms_norm(o, self.w[p + "post_attn_norm"], eps, plus_one=True)
+            x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2)
+            gu = x @ self.wf[p + "gate_up"].t()
+            y = ops.gated_act(gu[:, :c.d_ff], gu[:, c.d_ff:], act) @ self.w[p + "w_down"].t()
+            if g2:
+                y = ops.add_rms_norm(y, self.w[p + "post_mlp_norm"], eps, plus_one=True)
+            nxt = self.w[f"l{i + 1}.attn_norm"] if i + 1 < c.n_layers else self.w["norm"]
+            x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2)
+        return x
 
 
 def hf_state_dict(model: Model) -> Dict[str, torch.Tensor]:

@@ -444,54 +444,61 @@ _attn_ws: dict = {}
 
 
 def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.Tensor,
-                     prefix_len: torch.Tensor, k_hist: torch.Tensor, vt_hist: torch.Tensor,
-                     hist_base: torch.Tensor, n_str: int, T: int, *, scale: float,
-                     softcap: float = 0.0, group_prefix: Optional[torch.Tensor] = None,
+                     prefix_off: torch.Tensor, prefix_len: torch.Tensor, max_prefix_len: int,
+                     k_hist: torch.Tensor, vt_hist: torch.Tensor, hist_base: torch.Tensor,
+                     n_str: int, T: int, *, scale: float, softcap: float = 0.0, window: int = 0,
+                     group_prefix: Optional[torch.Tensor] = None,
                      out: Optional[torch.Tensor] = None, workspace: Optional[Workspace] = None):
     """Cascade attention of candidate streams over shared per-agent prefix K/V
     (cs_prefix_attention; layouts in include/consensus_scoring.h).
 
-    q [n_groups*n_str*T, H, D] bf16; k_prefix [n_prefix, Hkv, ldp, D], vt_prefix
-    [n_prefix, Hkv, D, ldp]; prefix_len [n_prefix] int32; k_hist [S, Hkv, ldh, D], vt_hist
-    [S, Hkv, D, ldh] (S = n_groups*n_str); hist_base [1] int32 (device).  Returns out
-    [n_tok, H, D] bf16.  Replaces the per-call prompt re-encoding of src/utils.py:249-259."""
+    q [n_groups*n_str*T, H, D] bf16; k_prefix [Hkv, Lp, D], vt_prefix [Hkv, D, Lp] (ragged
+    prefixes: prefix p's keys are rows prefix_off[p] ..); prefix_off [n_prefix] int64,
+    prefix_len [n_prefix] int32 (device), max_prefix_len >= every prefix_len (host);
+    k_hist [S, Hkv, ldh, D], vt_hist [S, Hkv, D, ldh] (S = n_groups*n_str); hist_base [1]
+    int32 (device).  Returns out [n_tok, H, D] bf16.  Replaces the per-call prompt
+    re-encoding of src/utils.py:249-259."""
     L = _lib.load()
     if q.dim() != 3 or q.dtype != torch.bfloat16 or not q.is_contiguous():
         raise CSError("q must be a contiguous [n_tok, H, D] bfloat16 tensor")
     n_tok, H, D = q.shape
-    n_prefix, Hkv, ldp, Dk = k_prefix.shape
+    Hkv, Lp, Dk = k_prefix.shape
     S, Hkv2, ldh, Dh = k_hist.shape
     if Dk != D or Dh != D or Hkv2 != Hkv:
         raise CSError("head layout mismatch between q, k_prefix and k_hist")
-    if tuple(vt_prefix.shape) != (n_prefix, Hkv, D, ldp) or tuple(vt_hist.shape) != (S, Hkv, D, ldh):
-        raise CSError("vt_prefix / vt_hist must be the transposed [.., Hkv, D, ld] layouts")
+    if tuple(vt_prefix.shape) != (Hkv, D, Lp) or tuple(vt_hist.shape) != (S, Hkv, D, ldh):
+        raise CSError("vt_prefix [Hkv, D, Lp] / vt_hist [S, Hkv, D, ldh] layouts expected")
     for t in (k_prefix, vt_prefix, k_hist, vt_hist):
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise CSError("K/V buffers must be contiguous bfloat16")
     if n_str <= 0 or T <= 0 or S % n_str != 0 or n_tok != S * T:
         raise CSError(f"n_tok {n_tok} != streams {S} x T {T} (n_str {n_str})")
     n_groups = S // n_str
+    n_prefix = prefix_len.numel()
     if group_prefix is None and n_groups != n_prefix:
         raise CSError("n_groups must equal n_prefix without group_prefix")
     if group_prefix is not None and (group_prefix.dtype != torch.int32 or group_prefix.numel() != n_groups):
         raise CSError("group_prefix must be int32 [n_groups]")
-    if prefix_len.dtype != torch.int32 or prefix_len.numel() != n_prefix:
-        raise CSError("prefix_len must be int32 [n_prefix]")
+    if prefix_len.dtype != torch.int32 or prefix_off.dtype != torch.int64 or \
+            prefix_off.numel() != n_prefix:
+        raise CSError("prefix_len must be int32 [n_prefix] and prefix_off int64 [n_prefix]")
     if hist_base.dtype != torch.int32 or hist_base.numel() != 1:
         raise CSError("hist_base must be a one-element int32 device tensor")
-    _require_cuda(q, k_prefix, vt_prefix, prefix_len, k_hist, vt_hist, hist_base, group_prefix, out)
+    _require_cuda(q, k_prefix, vt_prefix, prefix_off, prefix_len, k_hist, vt_hist, hist_base,
+                  group_prefix, out)
     if out is None:
         out = torch.empty_like(q)
-    nbytes = int(L.cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, ldp))
+    mpl = int(max_prefix_len)
+    nbytes = int(L.cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, mpl, ldh))
     if workspace is None:
         workspace = _attn_ws.setdefault(q.device, Workspace())
     ws = workspace.get(nbytes, q.device)
-    rc = L.cs_prefix_attention(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), ldp,
-                               prefix_len.data_ptr(),
+    rc = L.cs_prefix_attention(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), Lp,
+                               prefix_off.data_ptr(), prefix_len.data_ptr(), mpl,
                                group_prefix.data_ptr() if group_prefix is not None else None,
                                n_groups, k_hist.data_ptr(), vt_hist.data_ptr(), ldh,
                                hist_base.data_ptr(), n_str, T, H, Hkv, D, float(scale),
-                               float(softcap), out.data_ptr(),
+                               float(softcap), int(window), out.data_ptr(),
                                ws.data_ptr() if ws is not None else None,
                                ws.numel() if ws is not None else 0, _stream())
     _lib.check(rc, "cs_prefix_attention")
@@ -524,3 +531,74 @@ def rope_place(qkv: torch.Tensor, inv_freq: torch.Tensor, prefix_len: torch.Tens
                          k_hist.data_ptr(), vt_hist.data_ptr(), ldh, _stream())
     _lib.check(rc, "cs_rope_place")
     return q_out
+
+
+def _rows2d(t: torch.Tensor, name: str):
+    if t.dim() != 2 or t.dtype != torch.bfloat16 or t.stride(1) != 1:
+        raise CSError(f"{name} must be a 2-D bfloat16 tensor with unit column stride")
+    return t.stride(0) if t.shape[0] > 1 else t.shape[1]
+
+
+def add_rms_norm(a: torch.Tensor, weight: torch.Tensor, eps: float, *, b: Optional[torch.Tensor] = None,
+                 plus_one: bool = False, s_out: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = RMSNorm(a + b) (cs_add_rms_norm); the bf16 sum a + b is also written to s_out.
+    a, b, s_out, out [rows, d] bf16; weight [d] bf16 (Gemma-2: plus_one, 1 + weight)."""
+    L = _lib.load()
+    lda = _rows2d(a, "a")
+    rows, d = a.shape
+    ldb = _rows2d(b, "b") if b is not None else 0
+    lds = _rows2d(s_out, "s_out") if s_out is not None else 0
+    if (b is not None and b.shape != a.shape) or (s_out is not None and s_out.shape != a.shape):
+        raise CSError("a, b and s_out must share one shape")
+    if weight.dtype != torch.bfloat16 or weight.numel() != d or not weight.is_contiguous():
+        raise CSError("weight must be a contiguous bfloat16 [d] tensor")
+    if out is None:
+        out = torch.empty_like(a, memory_format=torch.contiguous_format)
+    ldy = _rows2d(out, "out")
+    _require_cuda(a, b, s_out, weight, out)
+    rc = L.cs_add_rms_norm(a.data_ptr(), lda, b.data_ptr() if b is not None else None, ldb,
+                           s_out.data_ptr() if s_out is not None else None, lds, weight.data_ptr(),
+                           rows, d, float(eps), int(bool(plus_one)), out.data_ptr(), ldy, _stream())
+    _lib.check(rc, "cs_add_rms_norm")
+    return out
+
+
+def gated_act(gate: torch.Tensor, up: torch.Tensor, act: str = "silu",
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(gate) * up (cs_gated_act): SiLU (Llama-3) or tanh-GeLU (Gemma-2); [rows, F] bf16."""
+    L = _lib.load()
+    ldg = _rows2d(gate, "gate")
+    ldu = _rows2d(up, "up")
+    if gate.shape != up.shape:
+        raise CSError("gate and up must share one shape")
+    rows, F = gate.shape
+    if out is None:
+        out = torch.empty(rows, F, dtype=torch.bfloat16, device=gate.device)
+    ldo = _rows2d(out, "out")
+    _require_cuda(gate, up, out)
+    rc = L.cs_gated_act(gate.data_ptr(), ldg, up.data_ptr(), ldu, rows, F,
+                        {"silu": 0, "gelu_tanh": 1}[act], out.data_ptr(), ldo, _stream())
+    _lib.check(rc, "cs_gated_act")
+    return out
+
+
+def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
+                dst_vt: torch.Tensor, parent: torch.Tensor, hist_base: torch.Tensor) -> None:
+    """dst[l][s] = src[l][parent[s]] over the filled history slots (cs_hist_gather);
+    K [L, S, Hkv, ldh, D], V^T [L, S, Hkv, D, ldh] bf16, parent [S] int64."""
+    L_ = _lib.load()
+    if src_k.dim() != 5 or src_k.shape != dst_k.shape or src_vt.shape != dst_vt.shape:
+        raise CSError("history buffers must be matching [L, S, Hkv, ldh, D] / [L, S, Hkv, D, ldh]")
+    Ln, S, Hkv, ldh, D = src_k.shape
+    if tuple(src_vt.shape) != (Ln, S, Hkv, D, ldh):
+        raise CSError("V^T history layout mismatch")
+    for t in (src_k, dst_k, src_vt, dst_vt):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise CSError("history buffers must be contiguous bfloat16")
+    if parent.dtype != torch.int64 or parent.numel() != S or hist_base.dtype != torch.int32:
+        raise CSError("parent must be int64 [S], hist_base int32 [1]")
+    _require_cuda(src_k, dst_k, src_vt, dst_vt, parent, hist_base)
+    rc = L_.cs_hist_gather(src_k.data_ptr(), dst_k.data_ptr(), src_vt.data_ptr(), dst_vt.data_ptr(),
+                           parent.data_ptr(), hist_base.data_ptr(), Ln, S, Hkv, ldh, D, _stream())
+    _lib.check(rc, "cs_hist_gather")

@@ -82,6 +82,21 @@ def device_lock(device) -> threading.RLock:
         return lk
 
 
+def serialized(attr: str = "model_identifier"):
+    """Method decorator: run under the device lock of ``getattr(self, attr)``'s engine
+    (the reference's runner calls generators from threads, src/experiment.py:283-322)."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrap(self, *a, **k):
+            eng, _ = get_engine(getattr(self, attr))
+            with device_lock(eng.device):
+                return fn(self, *a, **k)
+        return wrap
+    return deco
+
+
 def register_engine(model_identifier: str, engine: ScoringEngine, tokenizer: CharTokenizer) -> None:
     with _lock:
         _ENGINES[model_identifier] = (engine, tokenizer)
@@ -94,13 +109,21 @@ def register_model_dir(model_identifier: str, path: str) -> None:
 
 
 def random_engine(preset_name: str, device=None, dtype=torch.bfloat16, seed: int = 0,
-                  **engine_kw) -> Tuple[ScoringEngine, CharTokenizer]:
-    """Architecture-exact random-init model + full-vocabulary synthetic tokenizer."""
+                  tokenizer_dir: Optional[str] = None, **engine_kw):
+    """Architecture-exact random-init model + a full-vocabulary tokenizer: the
+    character tokenizer, or the BPE of ``tokenizer_dir`` (tokenizer.json; ids past its
+    table are synthetic single characters) for realistic prompt token counts."""
     cfg = preset(preset_name)
     dev = torch.device(device) if device is not None else \
         torch.device("cuda", torch.cuda.current_device())
     model = Model(cfg, dev, dtype, seed=seed)
-    tok = CharTokenizer("gemma2" if cfg.family == "gemma2" else "llama3", vocab_size=cfg.vocab)
+    fam = "gemma2" if cfg.family == "gemma2" else "llama3"
+    if tokenizer_dir:
+        from .tokenizer import BPETokenizer
+        # the fixture's chat template is Llama-3's: other families use their own layout
+        tok = BPETokenizer(tokenizer_dir, fam, vocab_size=cfg.vocab, use_config=fam == "llama3")
+    else:
+        tok = CharTokenizer(fam, vocab_size=cfg.vocab)
     return ScoringEngine(model, **engine_kw), tok
 
 

@@ -158,3 +158,171 @@ class CharTokenizer:
         prefix are exactly the tokens the text path would produce for user_prefix+cont."""
         ids, (start, end) = self.render_chat(system, user_prefix, add_generation_prompt=False)
         return ids[:end]
+
+
+FAMILY_SPECIALS = {
+    # family: (bos, eos, end-of-sequence strings)
+    "llama3": ("<|begin_of_text|>", "<|eot_id|>", ("<|eot_id|>", "<|end_of_text|>")),
+    "gemma2": ("<bos>", "<end_of_turn>", ("<end_of_turn>", "<eos>")),
+}
+_SENTINEL = "⁣⁣cs-prefix-end⁣⁣"   # never in prompt text; cut point of chat_prefix
+
+
+class BPETokenizer:
+    """A checkpoint's own tokenizer: ``tokenizer.json`` (Hugging Face `tokenizers` format,
+    e.g. Llama-3's byte-level BPE or Gemma-2's) and, from ``tokenizer_config.json``, its
+    chat template (jinja, rendered as transformers' apply_chat_template renders it) —
+    the text the hosted API of the reference renders and tokenizes server side
+    (src/utils.py:249-259).  Same interface as CharTokenizer.
+
+    Unlike a character tokenizer a BPE is NOT merge-free: the ids of ``prompt + token``
+    need not be the prompt's ids plus the token's (the reference re-tokenizes the string,
+    src/methods/beam_search.py:358-390).  ``merge_free`` is False and ``append_stable``
+    tells the callers when an id-level continuation equals the re-tokenized text."""
+
+    merge_free = False
+
+    def __init__(self, path: str, family: str = "llama3", vocab_size: int = 0,
+                 chat_template: "str | None" = None, use_config: bool = True) -> None:
+        import json
+        import os
+
+        from tokenizers import Tokenizer
+
+        tdir = path if os.path.isdir(path) else os.path.dirname(path)
+        tfile = os.path.join(path, "tokenizer.json") if os.path.isdir(path) else path
+        self.tk = Tokenizer.from_file(tfile)
+        self.family = family
+        conf = {}
+        cpath = os.path.join(tdir, "tokenizer_config.json")
+        if use_config and os.path.exists(cpath):
+            with open(cpath) as f:
+                conf = json.load(f)
+        self.chat_template = chat_template if chat_template is not None else conf.get("chat_template")
+        bos, eos, eos_strings = FAMILY_SPECIALS[family]
+
+        def tok_text(v, default):
+            if isinstance(v, dict):
+                v = v.get("content")
+            return v or default
+
+        self.bos = tok_text(conf.get("bos_token"), bos)
+        self.eos = tok_text(conf.get("eos_token"), eos)
+        self.eos_strings = tuple(s for s in dict.fromkeys((self.eos,) + eos_strings))
+        self.special_ids: Dict[str, int] = {}
+        for s in LLAMA3_SPECIALS + GEMMA2_SPECIALS + [self.bos, self.eos]:
+            i = self.tk.token_to_id(s)
+            if i is not None:
+                self.special_ids[s] = i
+        if self.bos not in self.special_ids or self.eos not in self.special_ids:
+            raise ValueError(f"tokenizer {tfile} lacks the {family} special tokens {self.bos!r} / "
+                             f"{self.eos!r}")
+        self.bos_id = self.special_ids[self.bos]
+        self.eos_id = self.special_ids[self.eos]
+        self.eos_ids = tuple(self.special_ids[s] for s in self.eos_strings if s in self.special_ids)
+        self.n_table = self.tk.get_vocab_size(with_added_tokens=True)
+        self.full_vocab = max(int(vocab_size), self.n_table)
+        self._strs: Dict[int, str] = {}
+        self._jinja = None
+
+    @property
+    def vocab_size(self) -> int:
+        return self.full_vocab
+
+    # --- plain text ---------------------------------------------------------------
+    def encode(self, text: str) -> List[int]:
+        return self.tk.encode(text, add_special_tokens=False).ids
+
+    def encode_offsets(self, text: str):
+        e = self.tk.encode(text, add_special_tokens=False)
+        return e.ids, e.offsets
+
+    def token_str(self, i: int) -> str:
+        s = self._strs.get(i)
+        if s is None:
+            if 0 <= i < self.n_table:
+                s = self.tk.decode([i], skip_special_tokens=False)
+            elif self.n_table <= i < self.full_vocab:
+                s = chr(SYNTH_BASE + i)
+            else:
+                s = UNK
+            self._strs[i] = s
+        return s
+
+    def tokens(self, ids: Sequence[int]) -> List[str]:
+        return [self.token_str(i) for i in ids]
+
+    def decode(self, ids: Iterable[int]) -> str:
+        ids = list(ids)
+        if all(0 <= i < self.n_table for i in ids):
+            return self.tk.decode(ids, skip_special_tokens=False)
+        return "".join(self.token_str(i) for i in ids)
+
+    def append_stable(self, prefix_text: str, prefix_ids: Sequence[int], piece: str,
+                      piece_ids: Sequence[int]) -> bool:
+        """Whether encode(prefix_text + piece) == prefix_ids + piece_ids (the id-level
+        continuation is what the reference's re-tokenized string gives)."""
+        return self.encode(prefix_text + piece) == list(prefix_ids) + list(piece_ids)
+
+    # --- prompt layouts -----------------------------------------------------------
+    def render_raw(self, text: str, add_bos: bool = True) -> List[int]:
+        return ([self.bos_id] if add_bos else []) + self.encode(text)
+
+    def _messages(self, system, user):
+        if self.family == "gemma2":          # no system role: prefixed to the user turn
+            return [{"role": "user", "content": (system + "\n\n" + user) if system else user}]
+        msgs = [{"role": "system", "content": system}] if system else []
+        return msgs + [{"role": "user", "content": user}]
+
+    def chat_text(self, system: "str | None", user: str, add_generation_prompt: bool = True) -> str:
+        """The rendered chat prompt string (the checkpoint's template, or the family's
+        standard layout when it has none)."""
+        if self.chat_template:
+            if self._jinja is None:
+                from jinja2.sandbox import ImmutableSandboxedEnvironment
+
+                def raise_exception(msg):
+                    raise ValueError(msg)
+
+                env = ImmutableSandboxedEnvironment(trim_blocks=True, lstrip_blocks=True)
+                env.globals["raise_exception"] = raise_exception
+                self._jinja = env.from_string(self.chat_template)
+            return self._jinja.render(messages=self._messages(system, user), bos_token=self.bos,
+                                      eos_token=self.eos,
+                                      add_generation_prompt=add_generation_prompt)
+        if self.family == "llama3":
+            t = "<|begin_of_text|>"
+            if system:
+                t += f"<|start_header_id|>system<|end_header_id|>\n\n{system}<|eot_id|>"
+            t += f"<|start_header_id|>user<|end_header_id|>\n\n{user}<|eot_id|>"
+            if add_generation_prompt:
+                t += "<|start_header_id|>assistant<|end_header_id|>\n\n"
+            return t
+        u = (system + "\n\n" + user) if system else user
+        t = f"<bos><start_of_turn>user\n{u}<end_of_turn>\n"
+        return t + ("<start_of_turn>model\n" if add_generation_prompt else "")
+
+    def render_chat(self, system: "str | None", user: str, add_generation_prompt: bool = True):
+        """(ids, (start, end)): the chat prompt's ids and the token span of the user content
+        (tokens whose characters overlap it, src/utils.py:321-363)."""
+        text = self.chat_text(system, user, add_generation_prompt)
+        ids, offs = self.encode_offsets(text)
+        key = user.strip()
+        c0 = text.rfind(key) if key else -1
+        if c0 < 0:
+            return ids, (len(ids), len(ids))
+        c1 = c0 + len(key)
+        span = [i for i, (a, b) in enumerate(offs) if a < c1 and b > c0]
+        return ids, ((span[0], span[-1] + 1) if span else (len(ids), len(ids)))
+
+    def chat_prefix(self, system: "str | None", user_prefix: str) -> List[int]:
+        """Ids of the chat prompt up to the end of ``user_prefix`` (the part of the user
+        turn shared by every candidate), with nothing of the template after it: the
+        prompt is rendered with a sentinel after the prefix (so the template's trim does
+        not eat the prefix's trailing whitespace) and cut there."""
+        text = self.chat_text(system, user_prefix + _SENTINEL, add_generation_prompt=False)
+        return self.encode(text[:text.index(_SENTINEL)])
+
+
+def load_tokenizer(path: str, family: str, vocab_size: int = 0) -> BPETokenizer:
+    return BPETokenizer(path, family=family, vocab_size=vocab_size)

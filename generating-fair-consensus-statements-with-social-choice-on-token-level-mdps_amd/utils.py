@@ -59,11 +59,12 @@ def prompt_logprobs_ids(model: str, ids: Sequence[int]) -> List[Optional[float]]
     engine, _ = runtime.get_engine(model)
     if len(ids) < 2:
         return [None] * len(ids)
-    t = torch.as_tensor(list(ids), dtype=torch.long, device=engine.device)[None]
-    h = engine.prefill([list(ids)]).hidden          # reuses a stored common prefix
-    rows = h[0, :-1]
-    tgt = t[0, 1:].to(torch.int32)[:, None]
-    lp = engine.rows_logprobs(rows, tgt).view(-1).double().cpu().tolist()
+    with runtime.device_lock(engine.device):
+        t = torch.as_tensor(list(ids), dtype=torch.long, device=engine.device)[None]
+        h = engine.prefill([list(ids)]).hidden          # reuses a stored common prefix
+        rows = h[0, :-1]
+        tgt = t[0, 1:].to(torch.int32)[:, None]
+        lp = engine.rows_logprobs(rows, tgt).view(-1).double().cpu().tolist()
     return [None] + lp
 
 
@@ -147,6 +148,11 @@ def user_span_sums(model, systems: Sequence[Optional[str]], users: Sequence[str]
     where the reference's call yields no usable log-probs (empty span, a None entry).
     """
     engine, tok = runtime.get_engine(model)
+    with runtime.device_lock(engine.device):
+        return _user_span_sums(engine, tok, systems, users, device_out)
+
+
+def _user_span_sums(engine, tok, systems, users, device_out):
     n = len(users)
     out = torch.full((n,), float("nan"), dtype=torch.float64)
     fast = [i for i in range(n) if users[i] and span_found_at_user(tok, systems[i], users[i])]
@@ -246,8 +252,9 @@ def generate_text(model, user_prompt, system_prompt=None, max_tokens=4096, tempe
             full = f"{system_prompt}\n\n{user_prompt}" if system_prompt else f"{user_prompt}"
             ids = tok.render_raw(full)
         bias = runtime.bias_token_ids(tok, bias_against_tokens)
-        out = runtime.generate(engine, tok, ids, [seed], max_tokens, float(temperature),
-                               bias_ids=bias, bias_value=float(bias_value))[0]
+        with runtime.device_lock(engine.device):
+            out = runtime.generate(engine, tok, ids, [seed], max_tokens, float(temperature),
+                                   bias_ids=bias, bias_value=float(bias_value))[0]
         text = tok.decode(out)
         for term in terminators or ():
             cut = text.find(term)

@@ -269,19 +269,25 @@ int cs_vocab_sample(const void* logits, int dtype, int64_t rows, int64_t vocab, 
  * n_groups groups of n_str streams each; group i uses prefix group_prefix[i] (NULL =
  * identity).  Stream s = i*n_str + b carries T query tokens; token t of stream s is
  * q[(s*T + t)][H][D] and sees
- *     prefix keys  [0, prefix_len[pfx])       k_prefix [n_prefix][Hkv][ld_prefix][D],
- *                                             vt_prefix [n_prefix][Hkv][D][ld_prefix]
+ *     prefix keys  [0, prefix_len[pfx])       k_prefix [Hkv][ld_prefix][D],
+ *                                             vt_prefix [Hkv][D][ld_prefix]: prefix p's key
+ *                                             j is row prefix_off[p] + j (ragged prefixes
+ *                                             in one buffer; prefix_off[p] % 32 == 0 and
+ *                                             rows up to the next multiple of 32 readable)
  *     its history  [0, *hist_base + t]        k_hist  [S][Hkv][ld_hist][D],
  *                                             vt_hist [S][Hkv][D][ld_hist]
  * (V transposed: key-contiguous rows; ld_prefix, ld_hist multiples of 32; key slots past
  * the visible range must hold finite values).  out [(s*T + t)][H][D].  Query head h uses
  * K/V head h / (H / Hkv).  scores = q.k * scale, then softcap * tanh(./softcap) when
- * softcap > 0 (Gemma-2 attention soft-cap), softmax over the visible keys.  D in
+ * softcap > 0 (Gemma-2 attention soft-cap), softmax over the visible keys; window > 0
+ * also hides keys more than window - 1 positions behind the query (Gemma-2's sliding
+ * window; prefix key j sits at position j, history slot j at prefix_len + j).  D in
  * {64, 128, 256}.  hist_base lives in device memory so that a captured decode step
- * replays with a growing history.  One workgroup holds all query rows of (group, K/V
- * head) (64 per workgroup), so a prefix key block is read once for every candidate of
- * that agent.  Workspace: cs_prefix_attention_workspace_size() bytes (0 = none needed);
- * results are deterministic (fixed-order split merge).
+ * replays with a growing history.  max_prefix_len (host) bounds prefix_len and sizes the
+ * key split.  One workgroup holds all query rows of (group, K/V head) (64 per
+ * workgroup), so a prefix key block is read once for every candidate of that agent.
+ * Workspace: cs_prefix_attention_workspace_size() bytes (0 = none needed); results are
+ * deterministic (fixed-order split merge).
  *
  * Replaces: the per-(agent, candidate) re-encoding of the agent's whole prompt behind
  *   every get_prompt_logprobs call (src/utils.py:249-259; driven per candidate at
@@ -289,13 +295,15 @@ int cs_vocab_sample(const void* logits, int dtype, int64_t rows, int64_t vocab, 
  *   finite_lookahead.py:464-524, src/evaluation.py:177-230).
  */
 size_t cs_prefix_attention_workspace_size(int32_t n_groups, int32_t n_str, int32_t T, int32_t H,
-                                          int32_t Hkv, int32_t D, int64_t ld_prefix);
+                                          int32_t Hkv, int32_t D, int32_t max_prefix_len,
+                                          int64_t ld_hist);
 int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
-                        int64_t ld_prefix, const int32_t* prefix_len, const int32_t* group_prefix,
-                        int32_t n_groups, const void* k_hist, const void* vt_hist, int64_t ld_hist,
+                        int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
+                        int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                        const void* k_hist, const void* vt_hist, int64_t ld_hist,
                         const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
-                        int32_t D, float scale, float softcap, void* out, void* workspace,
-                        size_t workspace_bytes, cs_stream_t stream);
+                        int32_t D, float scale, float softcap, int32_t window, void* out,
+                        void* workspace, size_t workspace_bytes, cs_stream_t stream);
 
 /*
  * cs_rope_place — rotary embedding (half-rotation convention, angle = position *
@@ -312,6 +320,48 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
                   const int32_t* group_prefix, int32_t n_groups, const int32_t* hist_base,
                   int32_t n_str, int32_t T, int32_t H, int32_t Hkv, int32_t D, void* q_out,
                   void* k_hist, void* vt_hist, int64_t ld_hist, cs_stream_t stream);
+
+/*
+ * cs_hist_gather — beam reordering of the per-stream K/V history (the cs_prefix_attention
+ * layouts, all L layers in one buffer): for every layer l and stream s, the filled slots
+ * j < *hist_base of stream parent[s] are copied,
+ *     dst_k [l][s][g][j][:] = src_k [l][parent[s]][g][j][:]     ([L][S][Hkv][ld_hist][D])
+ *     dst_vt[l][s][g][:][j] = src_vt[l][parent[s]][g][:][j]     ([L][S][Hkv][D][ld_hist],
+ *                                                               slots rounded up to 8)
+ * src and dst distinct (a ping-pong pair).  hist_base in device memory (graph replays).
+ *
+ * Replaces: the reference's beams are strings re-encoded in full by every call
+ *   (src/methods/beam_search.py:491-538 through src/utils.py:249-259); here a kept beam
+ *   inherits its parent's K/V.
+ */
+int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
+                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S,
+                   int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
+
+/*
+ * cs_add_rms_norm — residual add + RMSNorm of bf16 rows in one pass:
+ *     s = a + b (rounded to bf16; b NULL = none), written to s_out when non-NULL (may alias a)
+ *     y = s * rsqrt(mean(s^2) + eps) * g,  g = weight (plus_one = 0, Llama-3) or
+ *         1 + weight (plus_one = 1, Gemma-2); fp32 statistics, one rounding.
+ * d a multiple of 8 (<= 32768), leading dimensions multiples of 8.
+ *
+ * Replaces: part of the remote forward behind every get_prompt_logprobs call
+ *   (src/utils.py:249-259) — the per-layer residual + normalisation of each new token.
+ */
+int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, void* s_out,
+                    int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
+                    int plus_one, void* y, int64_t ldy, cs_stream_t stream);
+
+/*
+ * cs_gated_act — the gated MLP activation of bf16 rows: out = act(gate) * up with act =
+ * SiLU (act = 0, Llama-3) or tanh-GeLU (act = 1, Gemma-2), the activation rounded to bf16
+ * before the product.  F and leading dimensions multiples of 8.
+ *
+ * Replaces: part of the remote forward behind every get_prompt_logprobs call
+ *   (src/utils.py:249-259).
+ */
+int cs_gated_act(const void* gate, int64_t ld_gate, const void* up, int64_t ld_up, int64_t rows,
+                 int64_t F, int act, void* out, int64_t ld_out, cs_stream_t stream);
 
 #ifdef __cplusplus
 }

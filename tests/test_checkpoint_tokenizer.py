@@ -1,0 +1,115 @@
+"""The real-model path offline (CPU): a checkpoint directory in the published Hugging Face
+layout (config.json + model.safetensors + tokenizer.json / tokenizer_config.json) loads
+into the engine, and
+
+  * the engine's forward equals transformers' independent LlamaForCausalLM /
+    Gemma2ForCausalLM on the same directory (next-token log-probs, fp32, 1e-4);
+  * BPETokenizer renders the chat prompt to the same ids as transformers'
+    apply_chat_template with the checkpoint's template;
+  * an unregistered real model id raises instead of silently building random weights.
+
+The checkpoint is synthesized here (random tiny weights + the BPE fixture of
+tests/golden/make_bpe_fixture.py); no pretrained file exists offline."""
+import importlib
+import json
+import os
+
+import pytest
+import torch
+
+from conftest import REPO
+
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+FIXTURE = os.path.join(REPO, "tests", "golden", "bpe_fixture")
+
+
+def _ckpt(tmp_path, family):
+    M = importlib.import_module(PKG + ".model")
+    C = importlib.import_module(PKG + ".checkpoint")
+    T = importlib.import_module(PKG + ".tokenizer")
+    tok = T.BPETokenizer(FIXTURE, "llama3")
+    V = tok.n_table
+    if family == "llama3":
+        cfg = M.preset("tiny-llama", vocab=V, init_std=0.05)
+    else:
+        cfg = M.preset("tiny-gemma", vocab=V, init_std=0.05)
+    model = M.Model(cfg, "cpu", torch.float32, seed=4)
+    d = os.path.join(str(tmp_path), family)
+    C.save_checkpoint(model, d, tokenizer_dir=FIXTURE)
+    return d, model
+
+
+@pytest.mark.parametrize("family", ["llama3", "gemma2"])
+def test_loaded_checkpoint_matches_transformers(tmp_path, family):
+    C = importlib.import_module(PKG + ".checkpoint")
+    transformers = pytest.importorskip("transformers")
+    d, ref_model = _ckpt(tmp_path, family)
+    eng, tok = C.load_engine(d, device="cpu", dtype=torch.float32, reuse_caches=0)
+    assert eng.model.cfg.family == family
+    # the loaded weights are the saved ones
+    for k, v in ref_model.w.items():
+        assert torch.equal(eng.model.w[k], v), k
+    cls = transformers.LlamaForCausalLM if family == "llama3" else transformers.Gemma2ForCausalLM
+    hf = cls.from_pretrained(d, torch_dtype=torch.float32, attn_implementation="eager").eval()
+    text = "Issue: Should a person's genetic code be considered private information?"
+    ids = [tok.bos_id] + tok.encode(text)
+    with torch.no_grad():
+        ref = torch.log_softmax(hf(torch.tensor([ids])).logits[0].float(), dim=-1)
+        kv, h, _ = eng.model.prefill(torch.tensor([ids]), torch.tensor([len(ids)]))
+        lg = eng.model.lm_head(h[0]).float()
+        if eng.model.cfg.final_softcap:
+            c = eng.model.cfg.final_softcap
+            lg = c * torch.tanh(lg / c)
+        ours = torch.log_softmax(lg, dim=-1)
+    tgt = torch.tensor(ids[1:])
+    a = ours[:-1].gather(1, tgt[:, None])
+    b = ref[:-1].gather(1, tgt[:, None])
+    assert float((a - b).abs().max()) < 1e-4
+
+
+def test_bpe_chat_template_matches_transformers():
+    transformers = pytest.importorskip("transformers")
+    T = importlib.import_module(PKG + ".tokenizer")
+    tok = T.BPETokenizer(FIXTURE, "llama3")
+    conf = json.load(open(os.path.join(FIXTURE, "tokenizer_config.json")))
+    hf = transformers.PreTrainedTokenizerFast(tokenizer_file=os.path.join(FIXTURE, "tokenizer.json"),
+                                              bos_token=conf["bos_token"], eos_token=conf["eos_token"])
+    hf.chat_template = conf["chat_template"]
+    cases = [("You are generating a statement.", "Issue:\nGenes?\n\nStatement:\n"),
+             (None, "  leading and trailing  "), ("S", "A"), ("sys", "a​")]
+    for system, user in cases:
+        msgs = ([{"role": "system", "content": system}] if system else []) + \
+               [{"role": "user", "content": user}]
+        r = hf.apply_chat_template(msgs, tokenize=True, add_generation_prompt=True)
+        ids_hf = r["input_ids"] if hasattr(r, "keys") else r
+        ids, (a, b) = tok.render_chat(system, user)
+        assert ids == list(ids_hf), (system, user)
+        if user.strip():
+            assert user.strip() in tok.decode(ids[a:b])
+
+
+def test_chat_prefix_and_append_stability():
+    T = importlib.import_module(PKG + ".tokenizer")
+    tok = T.BPETokenizer(FIXTURE, "llama3")
+    system, user = "You are generating a statement.", "Issue:\nGenes?\n\nStatement:\n"
+    pre = tok.chat_prefix(system, user)
+    text = tok.chat_text(system, user + "X", add_generation_prompt=False)
+    assert tok.decode(pre) == text[:text.index("X")]
+    # a continuation after the prefix: stable when no BPE merge crosses the boundary
+    cont = "We agree that privacy matters."
+    full = tok.encode(tok.decode(pre) + cont)
+    assert tok.append_stable(tok.decode(pre), pre, cont, tok.encode(cont)) == (
+        full == pre + tok.encode(cont))
+    # a word split across the boundary re-tokenizes differently
+    assert not tok.append_stable("We agree th", tok.encode("We agree th"), "at", tok.encode("at"))
+    assert tok.vocab_size >= tok.n_table and tok.bos_id == tok.special_ids["<|begin_of_text|>"]
+
+
+def test_unregistered_real_model_id_raises(monkeypatch):
+    R = importlib.import_module(PKG + ".runtime")
+    ops = importlib.import_module(PKG + ".ops")
+    monkeypatch.delenv("CS_ALLOW_RANDOM_INIT", raising=False)
+    monkeypatch.delenv("CS_MODEL_ROOT", raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    with pytest.raises(ops.CSError, match="no weights for model"):
+        R.get_engine("meta-llama/Meta-Llama-3.1-8B-Instruct-Turbo")

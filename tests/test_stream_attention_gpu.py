@@ -24,7 +24,8 @@ def _ceil32(n):
     return max(32, (n + 31) // 32 * 32)
 
 
-def ref_attention(q, kp, vp, plen, kh, vh, hist_base, n_str, T, scale, softcap, gpfx=None):
+def ref_attention(q, kp, vp, plen, kh, vh, hist_base, n_str, T, scale, softcap, gpfx=None,
+                  window=0):
     """fp32 reference.  q [n_tok, H, D]; kp/vp [n_prefix, Hkv, ldp, D]; kh/vh [S, Hkv, ldh, D]."""
     n_tok, H, D = q.shape
     S, Hkv = kh.shape[0], kh.shape[1]
@@ -43,6 +44,10 @@ def ref_attention(q, kp, vp, plen, kh, vh, hist_base, n_str, T, scale, softcap, 
             sc = torch.einsum("grd,gnd->grn", qq, K) * scale
             if softcap > 0:
                 sc = softcap * torch.tanh(sc / softcap)
+            if window > 0:     # key positions: prefix j -> j, history j -> P + j
+                kpos = torch.cat([torch.arange(P), P + torch.arange(n_h)]).to(q.device)
+                qpos = P + hist_base + t
+                sc = sc.masked_fill((qpos - kpos >= window)[None, None], float("-inf"))
             pr = torch.softmax(sc, dim=-1)
             out[s * T + t] = torch.einsum("grn,gnd->grd", pr, Vv).reshape(H, D)
     return out
@@ -57,16 +62,31 @@ CASES = [
     (3, 2, 5, 8, 2, 64, [40, 64, 1], 2, 0.0, [2, 0, 0]),               # group -> prefix map
     (1, 64, 1, 32, 8, 128, [400], 9, 0.0, None),                       # one prefix, 64 streams
     (2, 3, 1, 4, 4, 64, [31, 33], 0, 0.0, None),                       # rep 1, first step
+    (2, 4, 3, 16, 8, 256, [300, 120], 40, 50.0, None, 64),             # Gemma sliding window
+    (3, 8, 1, 16, 8, 256, [500, 64, 250], 30, 50.0, None, 100),        # window, decode shape
 ]
+
+
+def _ragged(kp_list, Hkv, D):
+    """Per-prefix [Hkv, len_p, D] tensors -> (flat [Hkv, Lp, D], offsets): prefix p at rows
+    off[p] (multiples of 32), padding rows filled with finite garbage."""
+    off, o = [], 0
+    for k in kp_list:
+        off.append(o)
+        o += _ceil32(k.shape[1])
+    flat = torch.randn(Hkv, o, D).to(kp_list[0].dtype).to(kp_list[0].device) * 3.0
+    for k, o0 in zip(kp_list, off):
+        flat[:, o0:o0 + k.shape[1]] = k
+    return flat, off
 
 
 @pytest.mark.parametrize("case", CASES)
 def test_prefix_attention_matches_fp32_reference(ops, dev, case):
-    n_prefix, n_str, T, H, Hkv, D, plens, hb, cap, gmap = case
+    n_prefix, n_str, T, H, Hkv, D, plens, hb, cap, gmap = case[:10]
+    window = case[10] if len(case) > 10 else 0
     g = torch.Generator(device="cpu").manual_seed(zlib.crc32(repr(case).encode()))
     n_grp = len(gmap) if gmap is not None else n_prefix
     S = n_grp * n_str
-    ldp = _ceil32(max(plens))
     ldh = _ceil32(hb + T)
     bf = torch.bfloat16
 
@@ -74,25 +94,37 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
         return (torch.randn(*shape, generator=g) * s).to(bf).to(dev)
 
     q = rnd(S * T, H, D, s=1.0)
-    kp, vp = rnd(n_prefix, Hkv, ldp, D), rnd(n_prefix, Hkv, ldp, D)
+    kps = [rnd(Hkv, n, D) for n in plens]
+    vps = [rnd(Hkv, n, D) for n in plens]
+    kflat, off = _ragged(kps, Hkv, D)
+    vflat, _ = _ragged(vps, Hkv, D)
+    vtflat = vflat.transpose(1, 2).contiguous()
     kh, vh = rnd(S, Hkv, ldh, D), rnd(S, Hkv, ldh, D)
     plen = torch.tensor(plens, dtype=torch.int32, device=dev)
+    offt = torch.tensor(off, dtype=torch.int64, device=dev)
     hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
     gp = torch.tensor(gmap, dtype=torch.int32, device=dev) if gmap is not None else None
     scale = D ** -0.5 * (4.0 if cap else 1.0)      # the cap case drives scores into the cap
-    out = ops.prefix_attention(q, kp, vp.transpose(2, 3).contiguous(), plen, kh,
-                               vh.transpose(2, 3).contiguous(), hbt, n_str, T, scale=scale,
-                               softcap=cap, group_prefix=gp)
+
+    def run():
+        return ops.prefix_attention(q, kflat, vtflat, offt, plen, max(plens), kh,
+                                    vh.transpose(2, 3).contiguous(), hbt, n_str, T, scale=scale,
+                                    softcap=cap, window=window, group_prefix=gp)
+
+    out = run()
     torch.cuda.synchronize()
-    ref = ref_attention(q, kp, vp, plens, kh, vh, hb, n_str, T, scale, cap, gmap)
+    # reference on padded per-prefix tensors [n_prefix, Hkv, Pmax, D]
+    Pm = max(plens)
+    kp = torch.zeros(n_prefix, Hkv, Pm, D, dtype=bf, device=dev)
+    vp = torch.zeros(n_prefix, Hkv, Pm, D, dtype=bf, device=dev)
+    for i, (k, v) in enumerate(zip(kps, vps)):
+        kp[i, :, :k.shape[1]] = k
+        vp[i, :, :v.shape[1]] = v
+    ref = ref_attention(q, kp, vp, plens, kh, vh, hb, n_str, T, scale, cap, gmap, window)
     err = (out.float() - ref).abs()
     bound = 2e-2 + 2e-2 * ref.abs()
     assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}"
-    # deterministic: a second launch is bit-identical
-    out2 = ops.prefix_attention(q, kp, vp.transpose(2, 3).contiguous(), plen, kh,
-                                vh.transpose(2, 3).contiguous(), hbt, n_str, T, scale=scale,
-                                softcap=cap, group_prefix=gp)
-    assert torch.equal(out, out2)
+    assert torch.equal(out, run())          # deterministic: bit-identical relaunch
 
 
 @pytest.mark.parametrize("D,H,Hkv,T", [(64, 8, 2, 3), (128, 32, 8, 1), (256, 16, 8, 2)])
@@ -250,3 +282,69 @@ def test_beam_search_fast_topk_equals_host_loop(dev, family):
         assert sf == sh
     finally:
         R.clear_engines()
+
+
+@pytest.mark.parametrize("family", ["llama3", "gemma2"])
+def test_prefill_streams_matches_padded_prefill(dev, family):
+    """prefill_streams (length buckets, ragged K/V) and the padded prefill + fused_prefix
+    give the same prefix K/V (within bf16 rounding of differently padded forwards) and
+    DecodeStates over them the same next-token log-probs."""
+    E = importlib.import_module(PKG + ".engine")
+    eng = _tiny(family, dev, seed=9)
+    g = torch.Generator().manual_seed(4)
+    lens = (40, 23, 61, 300, 45)
+    prefixes = [torch.randint(5, 500, (n,), generator=g).tolist() for n in lens]
+    sp = eng.prefill_streams(prefixes)
+    pc = eng.prefill(prefixes)
+    fp = E.fused_prefix(pc)
+    for li in range(eng.model.cfg.n_layers):
+        for i, n in enumerate(lens):
+            a = sp.fused.k[li][:, int(sp.fused.off[i]):int(sp.fused.off[i]) + n].float()
+            b = fp.k[li][:, int(fp.off[i]):int(fp.off[i]) + n].float()
+            assert float((a - b).abs().max()) < 5e-2 * max(1.0, float(b.abs().max()))
+    assert torch.allclose(sp.last_hidden.float(), pc.last_hidden.float(), atol=5e-2, rtol=5e-2)
+    B = 3
+    s1 = E.DecodeState(eng, sp, n_prefix=5, n_beams=B, max_steps=4)
+    s2 = E.DecodeState(eng, pc, n_prefix=5, n_beams=B, max_steps=4)
+    tgt = torch.randint(0, eng.model.cfg.vocab, (5 * B, 8), generator=g).to(dev).to(torch.int32)
+    for step in range(3):
+        par = [0] * B if step == 0 else [1, 0, 2]
+        tk = torch.randint(5, 500, (B,), generator=g).tolist()
+        s1.advance(par, tk)
+        s2.advance(par, tk)
+        d = (eng.rows_logprobs(s1.hidden, tgt) - eng.rows_logprobs(s2.hidden, tgt)).abs().max()
+        assert float(d) < 5e-2, step
+
+
+@pytest.mark.parametrize("plus_one,d,with_b", [(False, 2048, True), (True, 3584, True),
+                                               (False, 8192, False), (True, 256, False)])
+def test_add_rms_norm_matches_torch(ops, dev, plus_one, d, with_b):
+    g = torch.Generator(device="cpu").manual_seed(d)
+    rows = 37
+    a = (torch.randn(rows, d, generator=g) * 2).to(torch.bfloat16).to(dev)
+    b = (torch.randn(rows, d, generator=g)).to(torch.bfloat16).to(dev) if with_b else None
+    w = (torch.randn(d, generator=g) * 0.1 + (0.0 if plus_one else 1.0)).to(torch.bfloat16).to(dev)
+    s_ref = (a + b) if with_b else a
+    sf = s_ref.float()
+    y_ref = sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + 1e-6)
+    y_ref = (y_ref * ((1.0 + w.float()) if plus_one else w.float())).to(torch.bfloat16)
+    a2 = a.clone()
+    y = ops.add_rms_norm(a2, w, 1e-6, b=b, s_out=a2, plus_one=plus_one)
+    torch.cuda.synchronize()
+    assert torch.equal(a2, s_ref)                    # the residual stream, bf16 add
+    diff = (y.float() - y_ref.float()).abs()
+    assert float(diff.max()) <= float(y_ref.float().abs().max()) * 2 ** -7
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+def test_gated_act_matches_torch(ops, dev, act):
+    import torch.nn.functional as F
+    g = torch.Generator(device="cpu").manual_seed(7)
+    gu = (torch.randn(29, 2 * 1536, generator=g) * 3).to(torch.bfloat16).to(dev)
+    gate, up = gu[:, :1536], gu[:, 1536:]
+    a = F.silu(gate) if act == "silu" else F.gelu(gate, approximate="tanh")
+    ref = a * up
+    out = ops.gated_act(gate, up, act)
+    torch.cuda.synchronize()
+    diff = (out.float() - ref.float()).abs()
+    assert float(diff.max()) <= 2 ** -6 * float(ref.float().abs().max())
