@@ -19,9 +19,13 @@
 //
 // Layouts (all bf16, D = head_dim in {64, 128, 256}):
 //   q       [n_tok, H, D], token tok = s*T + t of stream s = grp*n_str + b
-//   k_pfx   [Hkv, Lp, D]                vt_pfx [Hkv, D, Lp]     (ragged prefixes: prefix p's
+//   k_pfx   [Hkv, Lp, D]                vt_pfx [Hkv, Lp/32, D, 32] (ragged prefixes: prefix p's
 //           keys are rows off[p] .. off[p] + len[p], off[p] % 32 == 0, padded to 32 keys)
-//   k_hist  [S, Hkv, ldh, D]            vt_hist [S, Hkv, D, ldh]         (ldh % 32 == 0)
+//   k_hist  [S, Hkv, ldh, D]            vt_hist [S, Hkv, ldh/32, D, 32]  (ldh % 32 == 0)
+// V is stored TRANSPOSED IN 32-KEY TILES: the tile of keys 32c .. 32c+31 is D rows of 32
+// keys, contiguous (64 B per row): a key block's V^T is one 2-16 KB span, read as 16 rows
+// of 64 B per load instruction (a plain [D][keys] transpose puts the rows a whole key axis
+// apart — tens of KB — and the scattered 64-byte reads ran 10x below the HBM rate).
 //   out     [n_tok, H, D]
 // Query token t of stream s sees prefix keys [0, plen[pfx]) and history keys
 // [0, hist_base + t] (its own key is history slot hist_base + t).
@@ -179,8 +183,8 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
         kb = it * kKeyBlock;
         const int64_t po = a.poff[p];
         kbase = a.kp + (static_cast<int64_t>(g) * a.ldp + po) * D;
-        vbase = a.vtp + static_cast<int64_t>(g) * D * a.ldp + po;
-        ldv = a.ldp;
+        vbase = a.vtp + (static_cast<int64_t>(g) * a.ldp + po + kb) * D;   // the key block's tile
+        ldv = kKeyBlock;
         lim = vrow ? pl : 0;
         pos0 = 0;
       } else {
@@ -189,8 +193,8 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
         kb = (ih % nbh) * kKeyBlock;
         const int64_t sh = (static_cast<int64_t>(gi) * a.n_str + bb) * a.Hkv + g;
         kbase = a.kh + sh * a.ldh * D;
-        vbase = a.vth + sh * D * a.ldh;
-        ldv = a.ldh;
+        vbase = a.vth + (sh * a.ldh + kb) * D;                              // the key block's tile
+        ldv = kKeyBlock;
         lim = (vrow && bb == b) ? hv : 0;
         pos0 = pl;
       }
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
       }
       l = fmaf(l, alpha, ps);
       m = mn;
-      const __bf16* vrow0 = vbase + static_cast<int64_t>(col) * ldv + kb + 4 * h4;
+      const __bf16* vrow0 = vbase + static_cast<int64_t>(col) * ldv + 4 * h4;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const __bf16* vp = vrow0 + static_cast<int64_t>(dt * 16) * ldv;
@@ -310,11 +314,15 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   }
 }
 
-// one workgroup per (group, head, query group): rows x D/4 chunks, splits merged in order
+// one workgroup per (group, head, query group): first one thread per row folds the splits'
+// (m, l) into per-split weights (LDS), then every (row, 4-column chunk) sums the weighted
+// partial outputs — all loads of a phase independent, fixed split order (deterministic)
 template <int D>
 __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) {
   constexpr int LDSW = D + 2;
   constexpr int NC = D / 4;
+  __shared__ float wgt[kMaxSplit][kGroupRows];
+  __shared__ float inv_l[kGroupRows];
   const int qg = blockIdx.x % a.n_qg;
   const int pg = blockIdx.x / a.n_qg;
   const int gi = pg / a.Hkv, g = pg % a.Hkv;
@@ -325,22 +333,30 @@ __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) 
   const int nbp = (a.plen[p] + kKeyBlock - 1) / kKeyBlock;
   const int n_used = splits_used(a, M, r0, nbp, *a.hist_base);
   const float* base = a.part + (static_cast<int64_t>(pg) * a.n_qg + qg) * a.n_split * kGroupRows * LDSW;
+  for (int rl = threadIdx.x; rl < nrows; rl += kAttnThreads) {
+    float mt = -INFINITY;
+#pragma unroll 8
+    for (int sp = 0; sp < n_used; ++sp) mt = fmaxf(mt, base[(sp * kGroupRows + rl) * LDSW + D]);
+    float l = 0.0f;
+#pragma unroll 8
+    for (int sp = 0; sp < n_used; ++sp) {
+      const float m = base[(sp * kGroupRows + rl) * LDSW + D];
+      const float c = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m - mt);
+      wgt[sp][rl] = c;
+      l = fmaf(base[(sp * kGroupRows + rl) * LDSW + D + 1], c, l);
+    }
+    inv_l[rl] = l > 0.0f ? 1.0f / l : 0.0f;
+  }
+  __syncthreads();
   for (int item = threadIdx.x; item < nrows * NC; item += kAttnThreads) {
     const int rl = item / NC, c4 = item % NC;
-    float mt = -INFINITY;
-    for (int sp = 0; sp < n_used; ++sp) mt = fmaxf(mt, base[(sp * kGroupRows + rl) * LDSW + D]);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    float l = 0.0f;
-    if (mt != -INFINITY) {
-      for (int sp = 0; sp < n_used; ++sp) {
-        const float* pr = base + (sp * kGroupRows + rl) * LDSW;
-        const float c = __builtin_amdgcn_exp2f(pr[D] - mt);
-        l = fmaf(pr[D + 1], c, l);
-        const f32x4 v = *reinterpret_cast<const f32x4*>(pr + 4 * c4);
-        acc += v * c;
-      }
+#pragma unroll 8
+    for (int sp = 0; sp < n_used; ++sp) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(base + (sp * kGroupRows + rl) * LDSW + 4 * c4);
+      acc += v * wgt[sp][rl];
     }
-    const float inv = l > 0.0f ? 1.0f / l : 0.0f;
+    const float inv = inv_l[rl];
     const int row = r0 + rl;
     const int jh = row % a.rep, bt = row / a.rep;
     const int t = bt % a.T, b = bt / a.T;
@@ -368,48 +384,57 @@ struct RopeParams {
   int32_t n_str, T, H, Hkv, D;
 };
 
+// one thread per (token, 4 consecutive rotation pairs): the 4 angles' sincos once, then
+// every head of the token (q, k rotated; v placed) with 8-byte loads / stores
 __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
   const int half = r.D >> 1;
+  const int nq = half >> 2;                         // 4-pair quads per head
   const int nh = r.H + 2 * r.Hkv;
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (idx >= r.n_tok * nh * half) return;
-  const int i = static_cast<int>(idx % half);
-  const int hh = static_cast<int>((idx / half) % nh);
-  const int64_t tok = idx / (static_cast<int64_t>(half) * nh);
+  if (idx >= r.n_tok * nq) return;
+  const int i0 = 4 * static_cast<int>(idx % nq);
+  const int64_t tok = idx / nq;
   const int64_t s = tok / r.T;
   const int t = static_cast<int>(tok % r.T);
   const int gi = static_cast<int>(s / r.n_str);
   const int p = r.gpfx ? r.gpfx[gi] : gi;
-  const int hb = *r.hist_base;
-  const __bf16* src = r.qkv + tok * r.ldqkv + static_cast<int64_t>(hh) * r.D;
-  const float x1 = static_cast<float>(src[i]);
-  const float x2 = static_cast<float>(src[i + half]);
-  const int slot = hb + t;
-  if (hh >= r.H + r.Hkv) {           // v: transposed placement, no rotation
-    const int g = hh - r.H - r.Hkv;
-    __bf16* dst = r.vth + ((s * r.Hkv + g) * r.D) * r.ldh + slot;
-    dst[static_cast<int64_t>(i) * r.ldh] = src[i];
-    dst[static_cast<int64_t>(i + half) * r.ldh] = src[i + half];
-    return;
-  }
+  const int slot = *r.hist_base + t;
   const float pos = static_cast<float>(r.plen[p] + slot);
-  float sn, cs;
-  sincosf(pos * r.inv_freq[i], &sn, &cs);
-  const float y1 = fmaf(x1, cs, -x2 * sn);
-  const float y2 = fmaf(x2, cs, x1 * sn);
-  __bf16* dst;
-  if (hh < r.H) {
-    dst = r.q_out + (tok * r.H + hh) * r.D;
-  } else {
-    const int g = hh - r.H;
-    dst = r.kh + ((s * r.Hkv + g) * r.ldh + slot) * r.D;
+  float cs[4], sn[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sincosf(pos * r.inv_freq[i0 + e], &sn[e], &cs[e]);
+  const __bf16* row = r.qkv + tok * r.ldqkv;
+  for (int hh = 0; hh < nh; ++hh) {
+    const __bf16* src = row + static_cast<int64_t>(hh) * r.D + i0;
+    const bf16x4 a = *reinterpret_cast<const bf16x4*>(src);
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(src + half);
+    if (hh >= r.H + r.Hkv) {                         // v: transposed placement, no rotation
+      const int g = hh - r.H - r.Hkv;
+      __bf16* dst = r.vth + ((s * r.Hkv + g) * r.ldh + (slot & ~31)) * r.D +
+                    static_cast<int64_t>(i0) * 32 + (slot & 31);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dst[e * 32] = a[e];
+        dst[(half + e) * 32] = b[e];
+      }
+      continue;
+    }
+    bf16x4 y1, y2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x1 = static_cast<float>(a[e]), x2 = static_cast<float>(b[e]);
+      y1[e] = static_cast<__bf16>(fmaf(x1, cs[e], -x2 * sn[e]));
+      y2[e] = static_cast<__bf16>(fmaf(x2, cs[e], x1 * sn[e]));
+    }
+    __bf16* dst = hh < r.H ? r.q_out + (tok * r.H + hh) * r.D
+                           : r.kh + ((s * r.Hkv + (hh - r.H)) * r.ldh + slot) * r.D;
+    *reinterpret_cast<bf16x4*>(dst + i0) = y1;
+    *reinterpret_cast<bf16x4*>(dst + half + i0) = y2;
   }
-  dst[i] = static_cast<__bf16>(y1);
-  dst[i + half] = static_cast<__bf16>(y2);
 }
 
 // Beam reordering of the per-stream history: dst[l][s] = src[l][parent[s]] for the filled
-// slots only (j < *hist_base; V rows rounded up to 8 slots).  One workgroup per (layer,
+// slots only (j < *hist_base; V tiles rounded up to 32 slots).  One workgroup per (layer,
 // stream), 16-byte vectors; the unfilled capacity is never moved.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -417,26 +442,24 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
     const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
     __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
     int64_t S, int32_t Hkv, int32_t ldh, int32_t D) {
-  const int64_t l = blockIdx.x / S, s = blockIdx.x % S;
+  // one workgroup per (layer, stream, head)
+  const int64_t lsg = blockIdx.x;
+  const int g = static_cast<int>(lsg % Hkv);
+  const int64_t ls = lsg / Hkv;
+  const int64_t l = ls / S, s = ls % S;
   const int hb = min(*hist_base, ldh);
   if (hb <= 0) return;
   const int64_t p = parent[s];
-  const int64_t per = static_cast<int64_t>(Hkv) * ldh * D;         // elements per (l, s)
-  const int64_t so = (l * S + p) * per, dn = (l * S + s) * per;
-  // K: per head hb * D contiguous elements
-  const int kv = hb * D / 8;                                        // vectors per head
-  for (int i = threadIdx.x; i < Hkv * kv; i += 256) {
-    const int g = i / kv, v = i % kv;
-    const int64_t o = static_cast<int64_t>(g) * ldh * D + 8 * static_cast<int64_t>(v);
-    *reinterpret_cast<u32x4_t*>(dst_k + dn + o) = *reinterpret_cast<const u32x4_t*>(src_k + so + o);
-  }
-  // V^T: per (head, d) row the first ceil8(hb) slots
-  const int vv = (hb + 7) / 8;
-  for (int i = threadIdx.x; i < Hkv * D * vv; i += 256) {
-    const int row = i / vv, v = i % vv;
-    const int64_t o = static_cast<int64_t>(row) * ldh + 8 * v;
-    *reinterpret_cast<u32x4_t*>(dst_v + dn + o) = *reinterpret_cast<const u32x4_t*>(src_v + so + o);
-  }
+  const int64_t per = static_cast<int64_t>(ldh) * D;                 // elements per (l, s, g)
+  const int64_t so = ((l * S + p) * Hkv + g) * per, dn = ((l * S + s) * Hkv + g) * per;
+  // K: hb * D contiguous elements
+  const int kv = hb * D / 8;
+  for (int i = threadIdx.x; i < kv; i += 256)
+    reinterpret_cast<u32x4_t*>(dst_k + dn)[i] = reinterpret_cast<const u32x4_t*>(src_k + so)[i];
+  // V^T tiles: the first ceil32(hb) slots are ceil32(hb) * D contiguous elements
+  const int vv = ((hb + 31) & ~31) * D / 8;
+  for (int i = threadIdx.x; i < vv; i += 256)
+    reinterpret_cast<u32x4_t*>(dst_v + dn)[i] = reinterpret_cast<const u32x4_t*>(src_v + so)[i];
 }
 
 int attn_plan(int32_t n_grp, int32_t n_str, int32_t T, int32_t Hkv, int32_t rep, int64_t max_plen,
@@ -561,8 +584,8 @@ int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
     return fail(CS_ERR_INVALID, "cs_hist_gather: ld_hist and D must be positive multiples of 8");
   if (src_k == dst_k || src_vt == dst_vt)
     return fail(CS_ERR_INVALID, "cs_hist_gather: source and destination must differ (ping-pong)");
-  if (L * S > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_hist_gather: grid too large");
-  hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S)), dim3(256), 0,
+  if (L * S * Hkv > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_hist_gather: grid too large");
+  hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S * Hkv)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), static_cast<const __bf16*>(src_k),
                      static_cast<__bf16*>(dst_k), static_cast<const __bf16*>(src_vt),
                      static_cast<__bf16*>(dst_vt), parent, hist_base, S, Hkv, ld_hist, D);
@@ -597,7 +620,8 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
   r.H = H;
   r.Hkv = Hkv;
   r.D = D;
-  const int64_t total = r.n_tok * (H + 2 * Hkv) * (D / 2);
+  if (D % 8 != 0) return fail(CS_ERR_INVALID, "cs_rope_place: head_dim must be a multiple of 8");
+  const int64_t total = r.n_tok * (D / 8);
   const int64_t blocks = (total + 255) / 256;
   if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many elements");
   hipLaunchKernelGGL(rope_place_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,

@@ -111,6 +111,7 @@ class ScoringEngine:
     def __init__(self, model: Model, max_rows_per_chunk: int = 32768,
                  max_streams_per_chunk: int = 1024, reuse_caches: Optional[int] = None,
                  reuse_min_tokens: int = 16, reuse_max_tokens: int = 1 << 18,
+                 reuse_max_bytes: int = 8 << 30,
                  fused_scoring: bool = True, fused_max_rows: int = 1 << 17):
         self.model = model
         # bf16 models score agent x candidate batches on the stream kernels
@@ -129,6 +130,11 @@ class ScoringEngine:
         self.reuse_caches = int(reuse_caches)
         self.reuse_min_tokens = max(1, int(reuse_min_tokens))
         self.reuse_max_tokens = int(reuse_max_tokens)   # bound on stored rows x width
+        # ... and on the bytes the stored caches pin (K/V of every layer + final hidden)
+        c = model.cfg
+        esz = torch.finfo(model.dtype).bits // 8
+        self.bytes_per_cached_token = (c.n_layers * 2 * c.n_kv_heads * c.head_dim + c.d_model) * esz
+        self.reuse_max_bytes = int(reuse_max_bytes)
         self._store: List[tuple] = []     # (PrefixCache, [rows, width] ids, -1 padded), newest last
         self._store_lock = threading.Lock()
         self.reuse_stats = {"prefills": 0, "reused": 0, "tokens": 0, "tokens_run": 0}
@@ -156,11 +162,14 @@ class ScoringEngine:
             pos = torch.arange(P, device=self.device)[None].expand(ids.shape[0], P)
             cache = PrefixCache(kv=kv, lengths=lens, last_hidden=last, pos=pos, valid=valid,
                                 hidden=h, ids=ids)
-        if self.reuse_caches > 0 and cache.ids.numel() <= self.reuse_max_tokens:
+        if (self.reuse_caches > 0 and cache.ids.numel() <= self.reuse_max_tokens and
+                cache.ids.numel() * self.bytes_per_cached_token <= self.reuse_max_bytes):
             with self._store_lock:
                 self._store.append((cache, _id_matrix(rows)))
                 del self._store[:-self.reuse_caches]
-                while sum(c.ids.numel() for c, _ in self._store) > self.reuse_max_tokens:
+                while (sum(c.ids.numel() for c, _ in self._store) > self.reuse_max_tokens or
+                       sum(c.ids.numel() for c, _ in self._store) * self.bytes_per_cached_token
+                       > self.reuse_max_bytes):
                     del self._store[0]
         return cache
 
@@ -183,8 +192,8 @@ class ScoringEngine:
         Lp = off[-1]
         ks = [torch.zeros(c.n_kv_heads, Lp, c.head_dim, dtype=m.dtype, device=dev)
               for _ in range(c.n_layers)]
-        vts = [torch.zeros(c.n_kv_heads, c.head_dim, Lp, dtype=m.dtype, device=dev)
-               for _ in range(c.n_layers)]
+        vrs = [torch.zeros(c.n_kv_heads, Lp, c.head_dim, dtype=m.dtype, device=dev)
+               for _ in range(c.n_layers)]            # V rows; tiled (ops.blocked_vt) at the end
         last = torch.empty(n, c.d_model, dtype=m.dtype, device=dev)
         order = sorted(range(n), key=lambda i: lens[i])
         j = 0
@@ -204,21 +213,23 @@ class ScoringEngine:
                 ldh = _ceil32(Pb)
                 hk = [torch.zeros(nb, c.n_kv_heads, ldh, c.head_dim, dtype=m.dtype, device=dev)
                       for _ in range(c.n_layers)]
-                hv = [torch.zeros(nb, c.n_kv_heads, c.head_dim, ldh, dtype=m.dtype, device=dev)
-                      for _ in range(c.n_layers)]
+                hv = [torch.zeros(nb, c.n_kv_heads, ldh // 32, c.head_dim, 32, dtype=m.dtype,
+                                  device=dev) for _ in range(c.n_layers)]
                 h = m.forward_streams(ids.reshape(-1), _empty_prefix(m), hk, hv,
                                       torch.zeros(1, dtype=torch.int32, device=dev), 1, Pb,
                                       group_prefix=torch.zeros(nb, dtype=torch.int32, device=dev))
                 h = h.view(nb, Pb, -1)
-                kv = [(k, v.transpose(2, 3)) for k, v in zip(hk, hv)]
+                kv = [(k, ops.rows_from_blocked(v)) for k, v in zip(hk, hv)]
             else:
                 kv, h, _ = m.prefill(ids, lt)
             last[torch.as_tensor(b, device=dev)] = h[torch.arange(nb, device=dev), lt - 1]
             for li, (k, v) in enumerate(kv):
                 for r, i in enumerate(b):
                     ks[li][:, off[i]:off[i] + lens[i]] = k[r, :, :lens[i]]
-                    vts[li][:, :, off[i]:off[i] + lens[i]] = v[r, :, :lens[i]].transpose(1, 2)
+                    vrs[li][:, off[i]:off[i] + lens[i]] = v[r, :, :lens[i]]
             del kv, h
+        vts = [ops.blocked_vt(v) for v in vrs]
+        del vrs
         fp = FusedPrefix(k=ks, vt=vts, off=torch.as_tensor(off[:-1], dtype=torch.int64, device=dev),
                          lengths=torch.as_tensor(lens, dtype=torch.int32, device=dev),
                          max_len=max(lens))
@@ -392,7 +403,8 @@ class ScoringEngine:
             if Tc > 1:
                 ldh = _ceil32(Tc - 1)
                 hk = torch.zeros(S, c.n_kv_heads, ldh, c.head_dim, dtype=m.dtype, device=dev)
-                hv = torch.zeros(S, c.n_kv_heads, c.head_dim, ldh, dtype=m.dtype, device=dev)
+                hv = torch.zeros(S, c.n_kv_heads, ldh // 32, c.head_dim, 32, dtype=m.dtype,
+                                 device=dev)
                 hb = torch.zeros(1, dtype=torch.int32, device=dev)
                 gp = torch.as_tensor(gs, dtype=torch.int32, device=dev)
                 # one history buffer serves every layer: a chunk's K/V are not kept
@@ -596,7 +608,7 @@ class FusedPrefix:
     prefixes of one prefill in one ragged buffer per layer, prefix p's keys at rows
     off[p] .. off[p] + lengths[p] (off[p] % 32 == 0, each prefix padded to 32 keys)."""
     k: list                     # per layer [Hkv, Lp, D]
-    vt: list                    # per layer [Hkv, D, Lp] (V transposed: key-contiguous rows)
+    vt: list                    # per layer [Hkv, Lp/32, D, 32] (V^T in 32-key tiles)
     off: torch.Tensor           # [n_prefix] int64 (device)
     lengths: torch.Tensor       # [n_prefix] int32 (device)
     max_len: int                # host copy of max(lengths)
@@ -618,7 +630,7 @@ def _empty_prefix(m: Model) -> FusedPrefix:
     dev = m.device
     return FusedPrefix(
         k=[torch.zeros(c.n_kv_heads, 32, c.head_dim, dtype=m.dtype, device=dev)] * c.n_layers,
-        vt=[torch.zeros(c.n_kv_heads, c.head_dim, 32, dtype=m.dtype, device=dev)] * c.n_layers,
+        vt=[torch.zeros(c.n_kv_heads, 1, c.head_dim, 32, dtype=m.dtype, device=dev)] * c.n_layers,
         off=torch.zeros(1, dtype=torch.int64, device=dev),
         lengths=torch.zeros(1, dtype=torch.int32, device=dev), max_len=0)
 
@@ -633,17 +645,17 @@ def _offsets32(lens: Sequence[int]) -> List[int]:
 
 def fused_prefix(cache: PrefixCache) -> FusedPrefix:
     """A padded prefill's K/V re-laid for the stream kernels (prefix p at rows p * ldp,
-    ldp = the padded length rounded up to 32, zero-filled; V transposed).  One copy."""
+    ldp = the padded length rounded up to 32, zero-filled; V^T in 32-key tiles).  One copy."""
     n, Hkv, P, D = cache.kv[0][0].shape
     ldp = _ceil32(P)
     ks, vts = [], []
     for k, v in cache.kv:
         kp = torch.zeros(Hkv, n, ldp, D, dtype=k.dtype, device=k.device)
         kp[:, :, :P] = k.transpose(0, 1)
-        vt = torch.zeros(Hkv, D, n, ldp, dtype=v.dtype, device=v.device)
-        vt[..., :P] = v.permute(1, 3, 0, 2)
+        vr = torch.zeros(Hkv, n, ldp, D, dtype=v.dtype, device=v.device)
+        vr[:, :, :P] = v.transpose(0, 1)
         ks.append(kp.view(Hkv, n * ldp, D))
-        vts.append(vt.view(Hkv, D, n * ldp))
+        vts.append(ops.blocked_vt(vr.view(Hkv, n * ldp, D)))
     dev = cache.lengths.device
     return FusedPrefix(k=ks, vt=vts, off=torch.arange(n, device=dev, dtype=torch.int64) * ldp,
                        lengths=cache.lengths.to(torch.int32), max_len=P)
@@ -686,7 +698,7 @@ class DecodeState:
             # all layers in one tensor each, so a step's parent gather is 2 launches, not 2L
             return (torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
                                 dtype=m.dtype, device=dev),
-                    torch.zeros(c.n_layers, self.S, c.n_kv_heads, c.head_dim, self.ldh,
+                    torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh // 32, c.head_dim, 32,
                                 dtype=m.dtype, device=dev))
 
         self.hist = [buffers(), buffers()]

@@ -84,20 +84,26 @@ class StatementEvaluator:
         t0 = time.time()
         agents = list(agent_opinions)
         avg_lp, avg_p = self.agent_utilities(statements, issue, agent_opinions)
-        ppl = torch.exp(-avg_lp)
-        inv_ppl = 1.0 / torch.clamp(ppl, min=EPS)
         w = {
             "egalitarian_welfare_avg_prob": ops.welfare(avg_p, "min"),
             "utilitarian_welfare_avg_prob": ops.welfare(avg_p, "sum"),
             "log_nash_welfare_avg_prob": ops.welfare(avg_p, "sumlog", eps=EPS),
-            "egalitarian_welfare_perplexity": ops.welfare(ppl.contiguous(), "max"),
-            "utilitarian_welfare_perplexity": ops.welfare(ppl.contiguous(), "sum"),
-            "log_nash_welfare_perplexity": ops.welfare(inv_ppl.contiguous(), "sumlog",
-                                                       eps=1e-38),
         }
         w = {k: v.double().cpu().numpy() for k, v in w.items()}
         lp_h = avg_lp.double().cpu().numpy()
-        ppl_h = ppl.double().cpu().numpy()
+        # perplexity welfare in float64 on the host, exactly as src/evaluation.py:329-381
+        # (np.exp of the float64 log-prob: an average below -88.7 is a finite float64
+        # perplexity that an fp32 exp would turn into inf and drop from the fold)
+        with np.errstate(over="ignore"):
+            ppl_h = np.exp(-lp_h)
+        for kind in ("egalitarian", "utilitarian", "log_nash"):
+            w[f"{kind}_welfare_perplexity"] = np.full(len(statements), np.nan)
+        for s in range(len(statements)):
+            pp = [ppl_h[a, s] for a in range(lp_h.shape[0]) if np.isfinite(lp_h[a, s])]
+            if pp:
+                w["egalitarian_welfare_perplexity"][s] = max(pp)
+                w["utilitarian_welfare_perplexity"][s] = sum(pp)
+                w["log_nash_welfare_perplexity"][s] = sum(np.log([1.0 / max(x, EPS) for x in pp]))
         out = []
         for s in range(len(statements)):
             r: Dict[str, Any] = {"statement_embedding": None}

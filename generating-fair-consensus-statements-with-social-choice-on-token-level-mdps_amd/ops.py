@@ -452,10 +452,11 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     """Cascade attention of candidate streams over shared per-agent prefix K/V
     (cs_prefix_attention; layouts in include/consensus_scoring.h).
 
-    q [n_groups*n_str*T, H, D] bf16; k_prefix [Hkv, Lp, D], vt_prefix [Hkv, D, Lp] (ragged
-    prefixes: prefix p's keys are rows prefix_off[p] ..); prefix_off [n_prefix] int64,
-    prefix_len [n_prefix] int32 (device), max_prefix_len >= every prefix_len (host);
-    k_hist [S, Hkv, ldh, D], vt_hist [S, Hkv, D, ldh] (S = n_groups*n_str); hist_base [1]
+    q [n_groups*n_str*T, H, D] bf16; k_prefix [Hkv, Lp, D], vt_prefix [Hkv, Lp/32, D, 32]
+    (ragged prefixes: prefix p's keys are rows prefix_off[p] ..; V transposed in 32-key
+    tiles, see blocked_vt); prefix_off [n_prefix] int64, prefix_len [n_prefix] int32
+    (device), max_prefix_len >= every prefix_len (host); k_hist [S, Hkv, ldh, D], vt_hist
+    [S, Hkv, ldh/32, D, 32] (S = n_groups*n_str); hist_base [1]
     int32 (device).  Returns out [n_tok, H, D] bf16.  Replaces the per-call prompt
     re-encoding of src/utils.py:249-259."""
     L = _lib.load()
@@ -466,8 +467,10 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     S, Hkv2, ldh, Dh = k_hist.shape
     if Dk != D or Dh != D or Hkv2 != Hkv:
         raise CSError("head layout mismatch between q, k_prefix and k_hist")
-    if tuple(vt_prefix.shape) != (Hkv, D, Lp) or tuple(vt_hist.shape) != (S, Hkv, D, ldh):
-        raise CSError("vt_prefix [Hkv, D, Lp] / vt_hist [S, Hkv, D, ldh] layouts expected")
+    if tuple(vt_prefix.shape) != (Hkv, Lp // 32, D, 32) or \
+            tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32):
+        raise CSError("vt_prefix [Hkv, Lp/32, D, 32] / vt_hist [S, Hkv, ldh/32, D, 32] "
+                      "(V^T in 32-key tiles) expected")
     for t in (k_prefix, vt_prefix, k_hist, vt_hist):
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise CSError("K/V buffers must be contiguous bfloat16")
@@ -515,8 +518,8 @@ def rope_place(qkv: torch.Tensor, inv_freq: torch.Tensor, prefix_len: torch.Tens
         raise CSError("qkv must be a 2-D bfloat16 tensor with unit column stride")
     n_tok = qkv.shape[0]
     S, Hkv2, ldh, Dk = k_hist.shape
-    if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != (S, Hkv, D, ldh):
-        raise CSError("k_hist / vt_hist layout mismatch")
+    if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32):
+        raise CSError("k_hist [S, Hkv, ldh, D] / vt_hist [S, Hkv, ldh/32, D, 32] layout mismatch")
     if n_tok != S * T or S % n_str != 0:
         raise CSError("qkv rows must be streams x T")
     if tuple(q_out.shape) != (n_tok, H, D) or q_out.dtype != torch.bfloat16 or not q_out.is_contiguous():
@@ -586,12 +589,13 @@ def gated_act(gate: torch.Tensor, up: torch.Tensor, act: str = "silu",
 def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
                 dst_vt: torch.Tensor, parent: torch.Tensor, hist_base: torch.Tensor) -> None:
     """dst[l][s] = src[l][parent[s]] over the filled history slots (cs_hist_gather);
-    K [L, S, Hkv, ldh, D], V^T [L, S, Hkv, D, ldh] bf16, parent [S] int64."""
+    K [L, S, Hkv, ldh, D], V^T [L, S, Hkv, ldh/32, D, 32] bf16, parent [S] int64."""
     L_ = _lib.load()
     if src_k.dim() != 5 or src_k.shape != dst_k.shape or src_vt.shape != dst_vt.shape:
-        raise CSError("history buffers must be matching [L, S, Hkv, ldh, D] / [L, S, Hkv, D, ldh]")
+        raise CSError("history buffers must be matching [L, S, Hkv, ldh, D] / "
+                      "[L, S, Hkv, ldh/32, D, 32]")
     Ln, S, Hkv, ldh, D = src_k.shape
-    if tuple(src_vt.shape) != (Ln, S, Hkv, D, ldh):
+    if tuple(src_vt.shape) != (Ln, S, Hkv, ldh // 32, D, 32):
         raise CSError("V^T history layout mismatch")
     for t in (src_k, dst_k, src_vt, dst_vt):
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
@@ -602,3 +606,16 @@ def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
     rc = L_.cs_hist_gather(src_k.data_ptr(), dst_k.data_ptr(), src_vt.data_ptr(), dst_vt.data_ptr(),
                            parent.data_ptr(), hist_base.data_ptr(), Ln, S, Hkv, ldh, D, _stream())
     _lib.check(rc, "cs_hist_gather")
+
+
+def blocked_vt(v: torch.Tensor) -> torch.Tensor:
+    """V rows [..., keys, D] (keys a multiple of 32) -> the kernels' V^T in 32-key tiles
+    [..., keys/32, D, 32] (contiguous)."""
+    *lead, n, D = v.shape
+    return v.reshape(*lead, n // 32, 32, D).transpose(-1, -2).contiguous()
+
+
+def rows_from_blocked(vt: torch.Tensor) -> torch.Tensor:
+    """Inverse of blocked_vt: [..., nb, D, 32] -> [..., nb * 32, D]."""
+    *lead, nb, D, w = vt.shape
+    return vt.transpose(-1, -2).reshape(*lead, nb * w, D)

@@ -309,7 +309,7 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
  * cs_rope_place — rotary embedding (half-rotation convention, angle = position *
  * inv_freq[i]) of the fused projection qkv [(s*T + t)][ld_qkv] = [q (H*D) | k (Hkv*D) |
  * v (Hkv*D)] and placement into the cs_prefix_attention layouts: q_out [(s*T+t)][H][D],
- * k_hist[s][g][*hist_base + t][:] (rotated), vt_hist[s][g][:][*hist_base + t].  The
+ * k_hist[s][g][j][:] (rotated), vt_hist[s][g][j/32][:][j%32], j = *hist_base + t.  The
  * position of token t of stream s (group i) is prefix_len[group_prefix[i]] + *hist_base + t.
  * bf16 in / out, fp32 rotation.
  *
@@ -326,8 +326,8 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
  * layouts, all L layers in one buffer): for every layer l and stream s, the filled slots
  * j < *hist_base of stream parent[s] are copied,
  *     dst_k [l][s][g][j][:] = src_k [l][parent[s]][g][j][:]     ([L][S][Hkv][ld_hist][D])
- *     dst_vt[l][s][g][:][j] = src_vt[l][parent[s]][g][:][j]     ([L][S][Hkv][D][ld_hist],
- *                                                               slots rounded up to 8)
+ *     dst_vt[l][s][g][..]   = src_vt[l][parent[s]][g][..]      ([L][S][Hkv][ld_hist/32][D][32],
+ *                                                               the first ceil32(hist_base) slots)
  * src and dst distinct (a ping-pong pair).  hist_base in device memory (graph replays).
  *
  * Replaces: the reference's beams are strings re-encoded in full by every call

@@ -32,18 +32,42 @@ PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-md
 MODEL_ID = "tiny-llama-fixture"
 WEIGHT_SEED = 3
 FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
-            "gemma2": ("tiny-gemma-fixture", "method_traces_gemma.json")}
+            "gemma2": ("tiny-gemma-fixture", "method_traces_gemma.json"),
+            # BASELINE C1 shape: Llama-3.2-1B widths (d 2048, 32/8 heads of 64, vocab
+            # 128,256 -- the kernels' shapes) with 2 of its 16 layers, so that the
+            # reference's ~1,300 serial CPU calls finish in minutes
+            "c1": ("llama-3.2-1b-shaped-fixture", "method_traces_c1.json")}
+# untied LM head: with the random tied embedding a shallow model's residual stream makes
+# the last token's own logit ~45 sigma above the rest (every draw repeats it); an
+# independent head (std 0.02) gives logits of std ~1 and diverse samples
+C1_OVERRIDES = {"n_layers": 2, "tie_embeddings": False}
 
 
 def fixture_model(family: str = "llama3"):
     """The seeded fixture model (CPU fp32) and tokenizer shared by both sides."""
     Mm = importlib.import_module(PKG + ".model")
     T = importlib.import_module(PKG + ".tokenizer")
-    tok = T.CharTokenizer(family)
-    name = "tiny-llama" if family == "llama3" else "tiny-gemma"
-    cfg = Mm.preset(name, vocab=tok.vocab_size)
+    if family == "c1":
+        cfg = Mm.preset("llama-3.2-1b", **C1_OVERRIDES)
+        tok = T.CharTokenizer("llama3", vocab_size=cfg.vocab)
+    else:
+        tok = T.CharTokenizer(family)
+        name = "tiny-llama" if family == "llama3" else "tiny-gemma"
+        cfg = Mm.preset(name, vocab=tok.vocab_size)
     model = Mm.Model(cfg, "cpu", torch.float32, seed=WEIGHT_SEED)
     return cfg, model, tok
+
+
+# BASELINE C1 (configs/appendix/llama/scenario_1/beam_search.yaml:18-40: beam_width 4,
+# max_sampling_attempts 8), Best-of-N with N = 8, finite lookahead bf 3 / depth 2
+C1_RUNS = [
+    ("beam_search", {"beam_width": 4, "max_tokens": 10, "max_sampling_attempts": 8, "seed": 1,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+    ("best_of_n", {"n": 8, "max_tokens": 16, "seed": 7, "temperature": 1.0, "api_delay": 0,
+                   "log_level": "WARNING"}),
+    ("finite_lookahead", {"branching_factor": 3, "max_depth": 2, "max_tokens": 3, "seed": 11,
+                          "api_delay": 0, "log_level": "WARNING"}),
+]
 
 
 def install(reference: str, backend) -> None:
@@ -100,9 +124,12 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
-           "family": args.family,
+           "family": "llama3" if args.family == "c1" else args.family,
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
-    runs = [
+    if args.family == "c1":
+        out["preset_overrides"] = dict(C1_OVERRIDES)
+        out["tokenizer_vocab"] = cfg.vocab
+    runs = C1_RUNS if args.family == "c1" else [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,
                        "log_level": "WARNING"}),
         ("finite_lookahead", {"branching_factor": 2, "max_depth": 2, "max_tokens": 6, "seed": 11,

@@ -98,7 +98,7 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
     vps = [rnd(Hkv, n, D) for n in plens]
     kflat, off = _ragged(kps, Hkv, D)
     vflat, _ = _ragged(vps, Hkv, D)
-    vtflat = vflat.transpose(1, 2).contiguous()
+    vtflat = ops.blocked_vt(vflat)
     kh, vh = rnd(S, Hkv, ldh, D), rnd(S, Hkv, ldh, D)
     plen = torch.tensor(plens, dtype=torch.int32, device=dev)
     offt = torch.tensor(off, dtype=torch.int64, device=dev)
@@ -108,7 +108,7 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
 
     def run():
         return ops.prefix_attention(q, kflat, vtflat, offt, plen, max(plens), kh,
-                                    vh.transpose(2, 3).contiguous(), hbt, n_str, T, scale=scale,
+                                    ops.blocked_vt(vh), hbt, n_str, T, scale=scale,
                                     softcap=cap, window=window, group_prefix=gp)
 
     out = run()
@@ -143,8 +143,9 @@ def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
     hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
     q_out = torch.empty(S * T, H, D, dtype=torch.bfloat16, device=dev)
     kh = torch.zeros(S, Hkv, ldh, D, dtype=torch.bfloat16, device=dev)
-    vth = torch.zeros(S, Hkv, D, ldh, dtype=torch.bfloat16, device=dev)
+    vth = torch.zeros(S, Hkv, ldh // 32, D, 32, dtype=torch.bfloat16, device=dev)
     ops.rope_place(qkv, inv, plen, hbt, n_str, T, H, Hkv, D, q_out, kh, vth)
+    vrows = ops.rows_from_blocked(vth)              # [S, Hkv, ldh, D]
     torch.cuda.synchronize()
     # fp32 reference rotation
     pos = torch.tensor([plens[s // n_str] + hb + t for s in range(S) for t in range(T)],
@@ -159,8 +160,8 @@ def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
         for t in range(T):
             tok = s * T + t
             torch.testing.assert_close(kh[s, :, hb + t].float(), rot[tok, H:H + Hkv], atol=2e-2, rtol=1e-2)
-            assert torch.equal(vth[s, :, :, hb + t], qkv[tok].view(-1, D)[H + Hkv:])
-    assert kh[:, :, :hb].abs().sum() == 0 and vth[..., hb + T:].abs().sum() == 0
+            assert torch.equal(vrows[s, :, hb + t], qkv[tok].view(-1, D)[H + Hkv:])
+    assert kh[:, :, :hb].abs().sum() == 0 and vrows[:, :, hb + T:].abs().sum() == 0
 
 
 def _tiny(family, dev, seed=3, dtype=torch.bfloat16, weights=None):
@@ -246,7 +247,7 @@ def test_forward_streams_scoring_chunk_matches_fp32(dev):
     pfx = E.fused_prefix(cache)
     hk = [torch.zeros(2 * n_str, c.n_kv_heads, 32, c.head_dim, dtype=torch.bfloat16, device=dev)
           for _ in range(c.n_layers)]
-    hv = [torch.zeros(2 * n_str, c.n_kv_heads, c.head_dim, 32, dtype=torch.bfloat16, device=dev)
+    hv = [torch.zeros(2 * n_str, c.n_kv_heads, 1, c.head_dim, 32, dtype=torch.bfloat16, device=dev)
           for _ in range(c.n_layers)]
     hb = torch.zeros(1, dtype=torch.int32, device=dev)
     h = m.forward_streams(toks.reshape(-1), pfx, hk, hv, hb, n_str, T)
