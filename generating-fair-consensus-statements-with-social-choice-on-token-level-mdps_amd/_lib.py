@@ -25,7 +25,7 @@ EXPORTED = (
     "cs_segment_reduce", "cs_welfare_reduce", "cs_segmented_topk", "cs_vocab_topk_workspace_size",
     "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
-    "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_workspace_size",
+    "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
 )
 
@@ -101,11 +101,12 @@ def load():
     L.cs_beam_decode_step.restype = ctypes.c_int
     L.cs_beam_select.argtypes = [vp, i32, ctypes.c_int, vp, i32, i32, vp, vp, vp, vp, vp]
     L.cs_beam_select.restype = ctypes.c_int
-    L.cs_prefix_attention_workspace_size.argtypes = [i32, i32, i32, i32, i32, i32, i32, i64]
-    L.cs_prefix_attention_workspace_size.restype = ctypes.c_size_t
+    L.cs_prefix_attention_plan.argtypes = [vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, vp, i64,
+                                           vp, vp, vp]
+    L.cs_prefix_attention_plan.restype = i64
     L.cs_prefix_attention.argtypes = [vp, vp, vp, i64, vp, vp, i32, vp, i32, vp, vp, i64, vp, i32,
-                                      i32, i32, i32, i32, f32, f32, i32, vp, vp, ctypes.c_size_t,
-                                      vp]
+                                      i32, i32, i32, i32, f32, f32, i32, vp, i32, i32, vp, vp,
+                                      ctypes.c_size_t, vp]
     L.cs_prefix_attention.restype = ctypes.c_int
     L.cs_rope_place.argtypes = [vp, i64, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp,
                                 i64, vp]

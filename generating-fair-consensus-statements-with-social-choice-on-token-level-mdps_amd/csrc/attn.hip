@@ -40,6 +40,9 @@
 // xor-shuffles across the four lane groups.
 #include "cs_kernels.cuh"
 
+#include <algorithm>
+#include <vector>
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -49,9 +52,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAttnThreads = 256;   // 4 waves
 constexpr int kGroupRows = 64;      // query rows per workgroup (4 tiles of 16)
 constexpr int kKeyBlock = 32;
-constexpr int kMaxSplit = 32;
-constexpr int kItemsPerWave = 4;   // key blocks a wave walks before the work is split further
+constexpr int kMaxSplit = 32;       // key splits of one (group, head, query group)
+constexpr int kPlanMinBase = 1024;  // from this many (group, head, query group) workgroups on,
+                                    // the chip is full without key splits: no plan
+constexpr int kMergeRows = 8;       // query rows per merge workgroup (2 per wave)
+constexpr int kTargetWgsDefault = 1024;   // plan: split cells until about this many workgroups
+constexpr int kMinItemsDefault = 2;       // ... but never below this many key blocks per wave
 
+// Work plan entries (int32 x 4, device memory), attention entries first:
+//   attention  {pg = group * Hkv + head, query group, split | n_used << 8, partial slot}
+//   merge      {pg, query group, first partial slot, row chunk | n_used << 8}
 struct AttnParams {
   const __bf16* q;
   const __bf16* kp;
@@ -63,9 +73,10 @@ struct AttnParams {
   const __bf16* vth;
   const int32_t* hist_base;
   __bf16* out;
-  float* part;
+  float* part;              // [slot][kGroupRows][D + 2]: O (unnormalised), m, l
+  const int4* plan;         // nullable: one workgroup per (group, head, query group), no split
   int64_t ldp, ldh;
-  int32_t n_grp, n_str, T, H, Hkv, rep, n_qg, n_split;
+  int32_t n_grp, n_str, T, H, Hkv, rep, n_qg, n_attn;
   float scale, softcap, inv_softcap;
   int32_t window;           // > 0: keys more than window - 1 positions back are masked
   int32_t swizzle;
@@ -81,41 +92,141 @@ __device__ __forceinline__ int logical_block(int swz) {
   return (b & 7) * per + (b >> 3);
 }
 
-// key blocks ("items") a 16-row query tile visits: the prefix blocks plus the history blocks
-// of every stream with rows in the tile
-__device__ __forceinline__ int tile_items(const AttnParams& a, int M, int rt0, int nbp, int hb) {
-  const int rt1 = min(rt0 + 15, M - 1);
-  const int b_lo = (rt0 / a.rep) / a.T, b_hi = (rt1 / a.rep) / a.T;
-  const int t_hi = b_lo == b_hi ? (rt1 / a.rep) % a.T : a.T - 1;
-  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
-  return nbp + (b_hi - b_lo + 1) * nbh;
-}
-
-// splits a (group, head, query group) uses: enough that no wave walks more than
-// kItemsPerWave blocks, at most the grid's n_split (device-side, from the actual prefix
-// length and history size; the merge recomputes the same number)
-__device__ __forceinline__ int splits_used(const AttnParams& a, int M, int r0, int nbp, int hb) {
-  const int nrows = min(kGroupRows, M - r0);
-  const int n_qt = (nrows + 15) >> 4;
-  const int kw = n_qt == 1 ? 4 : (n_qt == 2 ? 2 : 1);
-  int items = 0;
-  for (int q = 0; q < n_qt; ++q) items = max(items, tile_items(a, M, r0 + 16 * q, nbp, hb));
-  const int per = kItemsPerWave * kw;
-  return max(1, min(a.n_split, (items + per - 1) / per));
-}
-
+// One 32-key block's operands for this lane: K rows kb + col and kb + 16 + col (8 bf16 of
+// each 32-wide d step), V^T rows (16-row d tiles) of the block's 32-key tile.
 template <int D>
-__global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a) {
+struct KeyBlock {
+  bf16x8 k0[D / 32], k1[D / 32];
+  bf16x4 vlo[D / 16], vhi[D / 16];
+};
+
+// where key block `it` of a query tile lives: the prefix blocks first, then the history
+// blocks of the tile's streams b_lo .. (nbh blocks each)
+struct ItemRef {
+  const __bf16* k;   // this lane's first K row
+  const __bf16* v;   // this lane's first V^T row
+  int kb, lim, pos0;
+};
+
+__device__ __forceinline__ ItemRef item_ref(const AttnParams& a, int it, int nbp, int nbh, int b_lo,
+                                            int b, int gi, int g, int64_t po, int pl, int hv,
+                                            bool vrow, int col, int h4, int D) {
+  ItemRef r;
+  if (it < nbp) {
+    r.kb = it * kKeyBlock;
+    const int64_t k0 = static_cast<int64_t>(g) * a.ldp + po;
+    r.k = a.kp + (k0 + r.kb + col) * D + 8 * h4;
+    r.v = a.vtp + (k0 + r.kb) * D + col * kKeyBlock + 4 * h4;
+    r.lim = vrow ? pl : 0;
+    r.pos0 = 0;
+  } else {
+    const int ih = it - nbp;
+    const int bb = b_lo + ih / nbh;
+    r.kb = (ih % nbh) * kKeyBlock;
+    const int64_t sh = (static_cast<int64_t>(gi) * a.n_str + bb) * a.Hkv + g;
+    r.k = a.kh + (sh * a.ldh + r.kb + col) * D + 8 * h4;
+    r.v = a.vth + (sh * a.ldh + r.kb) * D + col * kKeyBlock + 4 * h4;
+    r.lim = (vrow && bb == b) ? hv : 0;
+    r.pos0 = pl;
+  }
+  return r;
+}
+
+// all of a block's loads issued back to back (one memory round trip per block)
+template <int D>
+__device__ __forceinline__ void load_block(KeyBlock<D>& f, const ItemRef& r) {
+#pragma unroll
+  for (int ds = 0; ds < D / 32; ++ds) {
+    f.k0[ds] = *reinterpret_cast<const bf16x8*>(r.k + ds * 32);
+    f.k1[ds] = *reinterpret_cast<const bf16x8*>(r.k + 16 * D + ds * 32);
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    f.vlo[dt] = *reinterpret_cast<const bf16x4*>(r.v + dt * 16 * kKeyBlock);
+    f.vhi[dt] = *reinterpret_cast<const bf16x4*>(r.v + dt * 16 * kKeyBlock + 16);
+  }
+}
+
+// S^T = K . Q^T for the block's 32 keys, online softmax update, O^T += V^T . P^T
+template <int D>
+__device__ __forceinline__ void attend_block(const AttnParams& a, const KeyBlock<D>& f,
+                                             const ItemRef& r, const bf16x8 (&qf)[D / 32],
+                                             int kmin_pos, int h4, f32x4 (&o)[D / 16], float& m,
+                                             float& l) {
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ds = 0; ds < D / 32; ++ds) {
+    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k0[ds], qf[ds], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k1[ds], qf[ds], s1, 0, 0, 0);
+  }
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    y[i] = s0[i];
+    y[4 + i] = s1[i];
+  }
+  float bm = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int key = r.kb + (i >> 2) * 16 + 4 * h4 + (i & 3);
+    float x = y[i] * a.scale;
+    if (a.softcap > 0.0f) x = softcap_fn(x, a.softcap, a.inv_softcap);
+    x *= kLog2e;
+    y[i] = (key < r.lim && r.pos0 + key >= kmin_pos) ? x : -INFINITY;
+    bm = fmaxf(bm, y[i]);
+  }
+  bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+  bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+  const float mn = fmaxf(m, bm);
+  const bool none = mn == -INFINITY;
+  const float alpha = none ? 1.0f : __builtin_amdgcn_exp2f(m - mn);
+  float ps = 0.0f;
+  bf16x8 pb;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float pv = none ? 0.0f : __builtin_amdgcn_exp2f(y[i] - mn);
+    ps += pv;
+    pb[i] = static_cast<__bf16>(pv);
+  }
+  l = fmaf(l, alpha, ps);
+  m = mn;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    const bf16x8 va = {f.vlo[dt][0], f.vlo[dt][1], f.vlo[dt][2], f.vlo[dt][3],
+                       f.vhi[dt][0], f.vhi[dt][1], f.vhi[dt][2], f.vhi[dt][3]};
+    o[dt] *= alpha;
+    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
+  }
+}
+
+// PF: register double buffering (the next block's loads in flight while the current one
+// is attended) for the latency-bound decode launches (few workgroups, a plan); without it
+// the kernel holds fewer registers and more waves per SIMD, which serves the many-workgroup
+// scoring launches (T > 1) better.
+template <int D, bool PF>
+__global__ __launch_bounds__(kAttnThreads, PF ? (D <= 128 ? 2 : 1) : (D <= 128 ? 3 : 2))
+void prefix_attn_kernel(AttnParams a) {
   constexpr int NDS = D / 32;   // 32-wide d steps of S^T = K . Q^T
   constexpr int NDT = D / 16;   // 16-row d tiles of O^T
   constexpr int LDSW = D + 2;   // per query row: O[D], m, l
   __shared__ float sm[3][16][LDSW];
 
-  const int bid = logical_block(a.swizzle);
-  const int split = bid % a.n_split;
-  const int rest = bid / a.n_split;
-  const int qg = rest % a.n_qg;
-  const int pg = rest / a.n_qg;
+  int pg, qg, split, n_used, slot;
+  if (a.plan) {
+    const int4 e = a.plan[blockIdx.x];
+    pg = e.x;
+    qg = e.y;
+    split = e.z & 255;
+    n_used = e.z >> 8;
+    slot = e.w;
+  } else {
+    const int bid = logical_block(a.swizzle);
+    qg = bid % a.n_qg;
+    pg = bid / a.n_qg;
+    split = 0;
+    n_used = 1;
+    slot = 0;
+  }
   const int gi = pg / a.Hkv, g = pg % a.Hkv;
   const int p = a.gpfx ? a.gpfx[gi] : gi;
   const int M = a.n_str * a.T * a.rep;
@@ -138,6 +249,7 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   const int head = g * a.rep + jh;
   const int hb = *a.hist_base;
   const int pl = a.plen[p];
+  const int64_t po = a.poff[p];
   const int hv = min(hb + t + 1, static_cast<int>(a.ldh));
   // sliding window (Gemma-2 even layers): key position > qpos - window; prefix key j sits at
   // position j, history slot j at pl + j, the query at pl + hb + t
@@ -150,8 +262,6 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
   const int nbp = (pl + kKeyBlock - 1) / kKeyBlock;
   const int n_items = nbp + (b_hi - b_lo + 1) * nbh;
-  const int n_used = a.n_split == 1 ? 1 : splits_used(a, M, r0, nbp, hb);
-  if (split >= n_used) return;                       // whole workgroup: uniform
 
   bf16x8 qf[NDS];
   {
@@ -172,84 +282,38 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.0f;
 
-  if (active) {
-    const int nslot = n_used * kw;
-    for (int it = split * kw + ks; it < n_items; it += nslot) {
-      const __bf16* kbase;
-      const __bf16* vbase;
-      int64_t ldv;
-      int kb, lim, pos0;
-      if (it < nbp) {
-        kb = it * kKeyBlock;
-        const int64_t po = a.poff[p];
-        kbase = a.kp + (static_cast<int64_t>(g) * a.ldp + po) * D;
-        vbase = a.vtp + (static_cast<int64_t>(g) * a.ldp + po + kb) * D;   // the key block's tile
-        ldv = kKeyBlock;
-        lim = vrow ? pl : 0;
-        pos0 = 0;
-      } else {
-        const int ih = it - nbp;
-        const int bb = b_lo + ih / nbh;
-        kb = (ih % nbh) * kKeyBlock;
-        const int64_t sh = (static_cast<int64_t>(gi) * a.n_str + bb) * a.Hkv + g;
-        kbase = a.kh + sh * a.ldh * D;
-        vbase = a.vth + (sh * a.ldh + kb) * D;                              // the key block's tile
-        ldv = kKeyBlock;
-        lim = (vrow && bb == b) ? hv : 0;
-        pos0 = pl;
-      }
-      // S^T tiles: keys kb + [0, 16) and kb + [16, 32)
-      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-      const __bf16* k0 = kbase + static_cast<int64_t>(kb + col) * D + 8 * h4;
-      const __bf16* k1 = k0 + 16 * D;
-#pragma unroll
-      for (int ds = 0; ds < NDS; ++ds) {
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(k0 + ds * 32);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(k1 + ds * 32);
-        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[ds], s0, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[ds], s1, 0, 0, 0);
-      }
-      float y[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        y[i] = s0[i];
-        y[4 + i] = s1[i];
-      }
-      float bm = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int key = kb + (i >> 2) * 16 + 4 * h4 + (i & 3);
-        float x = y[i] * a.scale;
-        if (a.softcap > 0.0f) x = softcap_fn(x, a.softcap, a.inv_softcap);
-        x *= kLog2e;
-        y[i] = (key < lim && pos0 + key >= kmin_pos) ? x : -INFINITY;
-        bm = fmaxf(bm, y[i]);
-      }
-      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-      const float mn = fmaxf(m, bm);
-      const bool none = mn == -INFINITY;
-      const float alpha = none ? 1.0f : __builtin_amdgcn_exp2f(m - mn);
-      float ps = 0.0f;
-      bf16x8 pb;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float pv = none ? 0.0f : __builtin_amdgcn_exp2f(y[i] - mn);
-        ps += pv;
-        pb[i] = static_cast<__bf16>(pv);
-      }
-      l = fmaf(l, alpha, ps);
-      m = mn;
-      const __bf16* vrow0 = vbase + static_cast<int64_t>(col) * ldv + 4 * h4;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const __bf16* vp = vrow0 + static_cast<int64_t>(dt * 16) * ldv;
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vp);
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vp + 16);
-        const bf16x8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dt] *= alpha;
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
-      }
+  // the wave's blocks it0, it0 + nslot, ...: two register buffers, the next block's loads
+  // in flight while the current one is attended (a wave issues ONE round trip per block,
+  // overlapped with the previous block's MFMA / softmax work).  The last block's
+  // "next" is itself again (an L2 hit) so the loop body has no branch around the loads.
+  const int nslot = n_used * kw;
+  int it = split * kw + ks;
+  if (!PF && active) {
+    for (; it < n_items; it += nslot) {
+      KeyBlock<D> f;
+      const ItemRef r = item_ref(a, it, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D);
+      load_block<D>(f, r);
+      attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+    }
+  } else if (active && it < n_items) {
+    KeyBlock<D> fa, fb;
+    ItemRef ra = item_ref(a, it, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D), rb;
+    load_block<D>(fa, ra);
+    while (true) {
+      int itn = it + nslot < n_items ? it + nslot : it;
+      rb = item_ref(a, itn, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D);
+      load_block<D>(fb, rb);
+      __builtin_amdgcn_sched_barrier(0);
+      attend_block<D>(a, fa, ra, qf, kmin_pos, h4, o, m, l);
+      it += nslot;
+      if (it >= n_items) break;
+      itn = it + nslot < n_items ? it + nslot : it;
+      ra = item_ref(a, itn, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D);
+      load_block<D>(fa, ra);
+      __builtin_amdgcn_sched_barrier(0);
+      attend_block<D>(a, fb, rb, qf, kmin_pos, h4, o, m, l);
+      it += nslot;
+      if (it >= n_items) break;
     }
   }
   l += __shfl_xor(l, 16, 64);
@@ -258,14 +322,14 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   // waves that share a query tile combine through LDS (fixed order: ks = 0, 1, ...)
   if (kw > 1) {
     if (active && ks > 0) {
-      const int slot = w - n_qt;
+      const int sl = w - n_qt;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sm[slot][col][dt * 16 + 4 * h4 + i] = o[dt][i];
+        for (int i = 0; i < 4; ++i) sm[sl][col][dt * 16 + 4 * h4 + i] = o[dt][i];
       if (h4 == 0) {
-        sm[slot][col][D] = m;
-        sm[slot][col][D + 1] = l;
+        sm[sl][col][D] = m;
+        sm[sl][col][D + 1] = l;
       }
     }
     __syncthreads();
@@ -277,20 +341,20 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) o[dt] *= c0;
       for (int k = 1; k < kw; ++k) {
-        const int slot = qt + n_qt * k - n_qt;
-        const float mk = sm[slot][col][D];
+        const int sl = qt + n_qt * k - n_qt;
+        const float mk = sm[sl][col][D];
         const float ck = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mk - mt);
-        l = fmaf(sm[slot][col][D + 1], ck, l);
+        l = fmaf(sm[sl][col][D + 1], ck, l);
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[dt][i] = fmaf(sm[slot][col][dt * 16 + 4 * h4 + i], ck, o[dt][i]);
+          for (int i = 0; i < 4; ++i) o[dt][i] = fmaf(sm[sl][col][dt * 16 + 4 * h4 + i], ck, o[dt][i]);
       }
       m = mt;
     }
   }
   if (!vrow || ks != 0) return;
-  if (a.n_split == 1) {
+  if (n_used == 1) {
     const float inv = l > 0.0f ? 1.0f / l : 0.0f;
     __bf16* orow = a.out + (tok * a.H + head) * D + 4 * h4;
 #pragma unroll
@@ -301,9 +365,7 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
       *reinterpret_cast<bf16x4*>(orow + dt * 16) = v;
     }
   } else {
-    float* pr = a.part + ((static_cast<int64_t>(pg) * a.n_qg + qg) * a.n_split + split) *
-                             kGroupRows * LDSW +
-                static_cast<int64_t>(qt * 16 + col) * LDSW;
+    float* pr = a.part + (static_cast<int64_t>(slot) * kGroupRows + qt * 16 + col) * LDSW;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
       *reinterpret_cast<f32x4*>(pr + dt * 16 + 4 * h4) = o[dt];
@@ -314,50 +376,56 @@ __global__ __launch_bounds__(kAttnThreads) void prefix_attn_kernel(AttnParams a)
   }
 }
 
-// one workgroup per (group, head, query group): first one thread per row folds the splits'
-// (m, l) into per-split weights (LDS), then every (row, 4-column chunk) sums the weighted
-// partial outputs — all loads of a phase independent, fixed split order (deterministic)
+// One workgroup per merge entry (kMergeRows rows of a split (group, head, query group)),
+// each wave two rows, one per 32-lane half: the half's lanes fold the splits' (m, l) into
+// per-split weights, then the wave sums the weighted partial outputs (f32x4 columns).
+// Fixed split order: deterministic.
 template <int D>
 __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) {
   constexpr int LDSW = D + 2;
   constexpr int NC = D / 4;
-  __shared__ float wgt[kMaxSplit][kGroupRows];
-  __shared__ float inv_l[kGroupRows];
-  const int qg = blockIdx.x % a.n_qg;
-  const int pg = blockIdx.x / a.n_qg;
+  __shared__ float wsm[kAttnThreads / 64][2][kMaxSplit];
+  __shared__ float linv[kAttnThreads / 64][2];
+  const int4 e = a.plan[a.n_attn + blockIdx.x];
+  const int pg = e.x, qg = e.y, slot0 = e.z, chunk = e.w & 255, nu = e.w >> 8;
   const int gi = pg / a.Hkv, g = pg % a.Hkv;
   const int M = a.n_str * a.T * a.rep;
-  const int r0 = qg * kGroupRows;
-  const int nrows = min(kGroupRows, M - r0);
-  const int p = a.gpfx ? a.gpfx[gi] : gi;
-  const int nbp = (a.plen[p] + kKeyBlock - 1) / kKeyBlock;
-  const int n_used = splits_used(a, M, r0, nbp, *a.hist_base);
-  const float* base = a.part + (static_cast<int64_t>(pg) * a.n_qg + qg) * a.n_split * kGroupRows * LDSW;
-  for (int rl = threadIdx.x; rl < nrows; rl += kAttnThreads) {
-    float mt = -INFINITY;
-#pragma unroll 8
-    for (int sp = 0; sp < n_used; ++sp) mt = fmaxf(mt, base[(sp * kGroupRows + rl) * LDSW + D]);
-    float l = 0.0f;
-#pragma unroll 8
-    for (int sp = 0; sp < n_used; ++sp) {
-      const float m = base[(sp * kGroupRows + rl) * LDSW + D];
-      const float c = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m - mt);
-      wgt[sp][rl] = c;
-      l = fmaf(base[(sp * kGroupRows + rl) * LDSW + D + 1], c, l);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  const float* base = a.part + static_cast<int64_t>(slot0) * kGroupRows * LDSW;
+  {
+    const int rl = chunk * kMergeRows + 2 * w + half;
+    const bool vr = qg * kGroupRows + rl < M && l32 < nu;
+    float ms = -INFINITY, ls = 0.0f;
+    if (vr) {
+      const float* pm = base + (static_cast<int64_t>(l32) * kGroupRows + rl) * LDSW + D;
+      ms = pm[0];
+      ls = pm[1];
     }
-    inv_l[rl] = l > 0.0f ? 1.0f / l : 0.0f;
+    float mt = ms;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) mt = fmaxf(mt, __shfl_xor(mt, o, 64));
+    const float wt = (vr && mt != -INFINITY) ? __builtin_amdgcn_exp2f(ms - mt) : 0.0f;
+    float lt = wt * ls;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) lt += __shfl_xor(lt, o, 64);
+    if (l32 < kMaxSplit) wsm[w][half][l32] = wt;
+    if (l32 == 0) linv[w][half] = lt > 0.0f ? 1.0f / lt : 0.0f;
   }
   __syncthreads();
-  for (int item = threadIdx.x; item < nrows * NC; item += kAttnThreads) {
-    const int rl = item / NC, c4 = item % NC;
+  for (int item = lane; item < 2 * NC; item += 64) {
+    const int hr = item / NC, c4 = item % NC;
+    const int rl = chunk * kMergeRows + 2 * w + hr;
+    const int row = qg * kGroupRows + rl;
+    if (row >= M) continue;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-    for (int sp = 0; sp < n_used; ++sp) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(base + (sp * kGroupRows + rl) * LDSW + 4 * c4);
-      acc += v * wgt[sp][rl];
+    for (int sp = 0; sp < nu; ++sp) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(
+          base + (static_cast<int64_t>(sp) * kGroupRows + rl) * LDSW + 4 * c4);
+      acc += v * wsm[w][hr][sp];
     }
-    const float inv = inv_l[rl];
-    const int row = r0 + rl;
+    const float inv = linv[w][hr];
     const int jh = row % a.rep, bt = row / a.rep;
     const int t = bt % a.T, b = bt / a.T;
     const int64_t tok = (static_cast<int64_t>(gi) * a.n_str + b) * a.T + t;
@@ -462,37 +530,137 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
     reinterpret_cast<u32x4_t*>(dst_v + dn)[i] = reinterpret_cast<const u32x4_t*>(src_v + so)[i];
 }
 
-int attn_plan(int32_t n_grp, int32_t n_str, int32_t T, int32_t Hkv, int32_t rep, int64_t max_plen,
-              int64_t ldh, int32_t* n_qg, int32_t* n_split) {
-  const int64_t M = static_cast<int64_t>(n_str) * T * rep;
-  const int64_t qg = (M + kGroupRows - 1) / kGroupRows;
-  const int64_t base = static_cast<int64_t>(n_grp) * Hkv * qg;
-  if (qg > 0x7fffffff || base > 0x7fffffff) return -1;
-  *n_qg = static_cast<int32_t>(qg);
-  int64_t ns = 1;
-  if (base < 1024) {
-    // an upper bound of the splits any (group, head, query group) uses: every prefix
-    // block plus the history blocks of the <= 16 streams of a tile, kItemsPerWave per wave
-    const int64_t streams = std::min<int64_t>(16, std::max<int64_t>(1, 16 / std::max<int64_t>(1, static_cast<int64_t>(T) * rep)));
-    const int64_t items = (max_plen + kKeyBlock - 1) / kKeyBlock + streams * (ldh / kKeyBlock);
-    ns = std::min<int64_t>((items + kItemsPerWave - 1) / kItemsPerWave, kMaxSplit);
+// plan tunables (CS_ATTN_TARGET_WGS, CS_ATTN_MIN_ITEMS override; read once)
+int env_int(const char* name, int dflt, int lo, int hi) {
+  if (const char* e = getenv(name)) {
+    const int y = atoi(e);
+    if (y >= lo && y <= hi) return y;
   }
-  *n_split = static_cast<int32_t>(std::max<int64_t>(ns, 1));
-  return 0;
+  return dflt;
 }
+int attn_target_wgs() {
+  static const int v = env_int("CS_ATTN_TARGET_WGS", kTargetWgsDefault, 1, 1 << 20);
+  return v;
+}
+int attn_min_items() {
+  static const int v = env_int("CS_ATTN_MIN_ITEMS", kMinItemsDefault, 1, 4096);
+  return v;
+}
+
+struct PlanCell {
+  int32_t gi, qg, splits, per_wg;
+};
 
 }  // namespace
 
 extern "C" {
 
-size_t cs_prefix_attention_workspace_size(int32_t n_groups, int32_t n_str, int32_t T, int32_t H,
-                                          int32_t Hkv, int32_t D, int32_t max_prefix_len,
-                                          int64_t ld_hist) {
-  if (n_groups <= 0 || n_str <= 0 || T <= 0 || Hkv <= 0 || H % Hkv != 0) return 0;
-  int32_t nqg = 0, ns = 0;
-  if (attn_plan(n_groups, n_str, T, Hkv, H / Hkv, max_prefix_len, ld_hist, &nqg, &ns) != 0 || ns == 1)
-    return 0;
-  return static_cast<size_t>(n_groups) * Hkv * nqg * ns * kGroupRows * (D + 2) * sizeof(float);
+int64_t cs_prefix_attention_plan(const int32_t* prefix_len, int32_t n_prefix,
+                                 const int32_t* group_prefix, int32_t n_groups, int32_t n_str,
+                                 int32_t T, int32_t H, int32_t Hkv, int32_t D, int64_t ld_hist,
+                                 int32_t* plan, int64_t plan_cap, int32_t* n_attn, int32_t* n_merge,
+                                 size_t* workspace_bytes) {
+  if (n_attn) *n_attn = 0;
+  if (n_merge) *n_merge = 0;
+  if (workspace_bytes) *workspace_bytes = 0;
+  if (n_groups < 0 || n_str < 0 || T < 0 || n_prefix < 0)
+    return fail(CS_ERR_INVALID, "cs_prefix_attention_plan: negative size");
+  if (n_groups == 0 || n_str == 0 || T == 0) return 0;
+  if (!prefix_len || Hkv <= 0 || H <= 0 || H % Hkv != 0 || ld_hist <= 0 || ld_hist % kKeyBlock != 0 ||
+      (D != 64 && D != 128 && D != 256))
+    return fail(CS_ERR_INVALID, "cs_prefix_attention_plan: bad shape");
+  const int64_t rep = H / Hkv;
+  const int64_t M = static_cast<int64_t>(n_str) * T * rep;
+  const int64_t n_qg = (M + kGroupRows - 1) / kGroupRows;
+  const int64_t base = static_cast<int64_t>(n_groups) * Hkv * n_qg;
+  if (base >= kPlanMinBase) return 0;   // enough workgroups without key splits
+  const int64_t nbh_max = ld_hist / kKeyBlock;
+  // every cell's key blocks per query tile (an upper bound: history at capacity)
+  struct Cell { int32_t gi, qg; int64_t items, kw, nrows; };
+  std::vector<Cell> cl;
+  cl.reserve(static_cast<size_t>(n_groups * n_qg));
+  for (int32_t gi = 0; gi < n_groups; ++gi) {
+    const int32_t p = group_prefix ? group_prefix[gi] : gi;
+    if (p < 0 || p >= n_prefix || prefix_len[p] < 0)
+      return fail(CS_ERR_INVALID, "cs_prefix_attention_plan: group_prefix / prefix_len out of range");
+    const int64_t nbp = (prefix_len[p] + kKeyBlock - 1) / kKeyBlock;
+    for (int64_t qg = 0; qg < n_qg; ++qg) {
+      const int64_t r0 = qg * kGroupRows;
+      const int64_t nrows = std::min<int64_t>(kGroupRows, M - r0);
+      const int64_t n_qt = (nrows + 15) / 16;
+      const int64_t kw = n_qt == 1 ? 4 : (n_qt == 2 ? 2 : 1);
+      int64_t items = 0;
+      for (int64_t q = 0; q < n_qt; ++q) {
+        const int64_t rt0 = r0 + 16 * q, rt1 = std::min(rt0 + 15, M - 1);
+        const int64_t streams = (rt1 / rep) / T - (rt0 / rep) / T + 1;
+        items = std::max(items, nbp + streams * nbh_max);
+      }
+      cl.push_back({gi, static_cast<int32_t>(qg), items, kw, nrows});
+    }
+  }
+  // one per-wave budget q for all cells (a cell of `items` blocks on kw waves takes
+  // ceil(items / (q kw)) splits, at most kMaxSplit): the whole launch's wave-serial work
+  // spread over about attn_target_wgs() workgroups, never below attn_min_items() blocks per
+  // wave — so the split workgroups are about equally long and no cell is the long pole
+  auto splits_of = [](const Cell& c, int64_t q) {
+    return std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, (c.items + q * c.kw - 1) / (q * c.kw)));
+  };
+  int64_t work = 0;
+  for (const Cell& c : cl) work += (c.items + c.kw - 1) / c.kw;
+  work *= Hkv;
+  const int64_t q = std::max<int64_t>(attn_min_items(), (work + attn_target_wgs() - 1) / attn_target_wgs());
+  std::vector<PlanCell> cells;
+  cells.reserve(cl.size());
+  int64_t na = 0, nm = 0, slots = 0;
+  for (const Cell& c : cl) {
+    const int64_t s = splits_of(c, q);
+    const int64_t per = (c.items + s * c.kw - 1) / (s * c.kw);
+    cells.push_back({c.gi, c.qg, static_cast<int32_t>(s), static_cast<int32_t>(per)});
+    na += s * Hkv;
+    if (s > 1) {
+      slots += s * Hkv;
+      nm += (c.nrows + kMergeRows - 1) / kMergeRows * Hkv;
+    }
+  }
+  if (nm == 0) return 0;   // no cell splits: the plain grid
+  if (na + nm > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_prefix_attention_plan: plan too large");
+  if (n_attn) *n_attn = static_cast<int32_t>(na);
+  if (n_merge) *n_merge = static_cast<int32_t>(nm);
+  if (workspace_bytes) *workspace_bytes = static_cast<size_t>(slots) * kGroupRows * (D + 2) * sizeof(float);
+  const int64_t total = na + nm;
+  if (!plan) return total;
+  if (plan_cap < total) return fail(CS_ERR_INVALID, "cs_prefix_attention_plan: plan_cap too small");
+  // the longest workgroups first (dispatched first: the tail of the launch is short ones)
+  std::stable_sort(cells.begin(), cells.end(),
+                   [](const PlanCell& x, const PlanCell& y) { return x.per_wg > y.per_wg; });
+  int32_t* pa = plan;
+  int32_t* pm = plan + 4 * na;
+  int32_t slot = 0;
+  for (const PlanCell& c : cells) {
+    const int64_t r0 = static_cast<int64_t>(c.qg) * kGroupRows;
+    const int64_t nrows = std::min<int64_t>(kGroupRows, M - r0);
+    for (int32_t g = 0; g < Hkv; ++g) {
+      const int32_t pg = c.gi * Hkv + g;
+      for (int32_t sp = 0; sp < c.splits; ++sp) {
+        pa[0] = pg;
+        pa[1] = c.qg;
+        pa[2] = sp | (c.splits << 8);
+        pa[3] = c.splits > 1 ? slot + sp : 0;
+        pa += 4;
+      }
+      if (c.splits > 1) {
+        for (int32_t ch = 0; ch < (nrows + kMergeRows - 1) / kMergeRows; ++ch) {
+          pm[0] = pg;
+          pm[1] = c.qg;
+          pm[2] = slot;
+          pm[3] = ch | (c.splits << 8);
+          pm += 4;
+        }
+        slot += c.splits;
+      }
+    }
+  }
+  return total;
 }
 
 int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
@@ -500,8 +668,9 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
                         int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
                         const void* k_hist, const void* vt_hist, int64_t ld_hist,
                         const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
-                        int32_t D, float scale, float softcap, int32_t window, void* out,
-                        void* workspace, size_t workspace_bytes, cs_stream_t stream) {
+                        int32_t D, float scale, float softcap, int32_t window, const void* plan,
+                        int32_t n_attn, int32_t n_merge, void* out, void* workspace,
+                        size_t workspace_bytes, cs_stream_t stream) {
   if (n_groups < 0 || n_str < 0 || T < 0) return fail(CS_ERR_INVALID, "cs_prefix_attention: negative size");
   if (n_groups == 0 || n_str == 0 || T == 0) return CS_OK;
   if (Hkv <= 0 || H <= 0 || H % Hkv != 0 || H / Hkv > 64)
@@ -516,6 +685,15 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
       !hist_base || !out)
     return fail(CS_ERR_INVALID, "cs_prefix_attention: NULL pointer");
   if (!(scale > 0.0f) || softcap < 0.0f) return fail(CS_ERR_INVALID, "cs_prefix_attention: bad scale / softcap");
+  if (plan && (n_attn <= 0 || n_merge <= 0))
+    return fail(CS_ERR_INVALID, "cs_prefix_attention: a plan needs n_attn > 0 and n_merge > 0");
+  if (plan && !workspace)
+    return fail(CS_ERR_WORKSPACE, "cs_prefix_attention: a plan needs the workspace "
+                                  "cs_prefix_attention_plan() sized");
+  const int64_t M = static_cast<int64_t>(n_str) * T * (H / Hkv);
+  const int64_t n_qg = (M + kGroupRows - 1) / kGroupRows;
+  const int64_t base = static_cast<int64_t>(n_groups) * Hkv * n_qg;
+  if (n_qg > 0x7fffffff || base > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_prefix_attention: too many query rows");
   AttnParams a;
   a.q = static_cast<const __bf16*>(q);
   a.kp = static_cast<const __bf16*>(k_prefix);
@@ -527,6 +705,8 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   a.vth = static_cast<const __bf16*>(vt_hist);
   a.hist_base = hist_base;
   a.out = static_cast<__bf16*>(out);
+  a.part = static_cast<float*>(workspace);
+  a.plan = static_cast<const int4*>(plan);
   a.ldp = ld_prefix;
   a.ldh = ld_hist;
   a.n_grp = n_groups;
@@ -535,31 +715,25 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   a.H = H;
   a.Hkv = Hkv;
   a.rep = H / Hkv;
+  a.n_qg = static_cast<int32_t>(n_qg);
+  a.n_attn = plan ? n_attn : 0;
   a.scale = scale;
   a.softcap = softcap;
   a.inv_softcap = softcap > 0.0f ? 1.0f / softcap : 0.0f;
   a.window = window > 0 ? window : 0;
-  if (attn_plan(n_groups, n_str, T, Hkv, a.rep, max_prefix_len, ld_hist, &a.n_qg, &a.n_split) != 0)
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: too many query rows");
-  const int64_t nwg = static_cast<int64_t>(n_groups) * Hkv * a.n_qg * a.n_split;
-  if (nwg > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_prefix_attention: grid too large");
-  a.part = nullptr;
-  if (a.n_split > 1) {
-    const size_t need =
-        cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, max_prefix_len, ld_hist);
-    if (!workspace || workspace_bytes < need)
-      return fail(CS_ERR_WORKSPACE, "cs_prefix_attention: workspace smaller than "
-                                    "cs_prefix_attention_workspace_size()");
-    a.part = static_cast<float*>(workspace);
-  }
-  a.swizzle = (nwg % 8 == 0 && nwg >= 64) ? 1 : 0;
+  (void)workspace_bytes;   // sized by cs_prefix_attention_plan for this plan
+  const int64_t nwg = plan ? n_attn : base;
+  a.swizzle = (!plan && nwg % 8 == 0 && nwg >= 64) ? 1 : 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<uint32_t>(nwg));
-  const dim3 merge_grid(static_cast<uint32_t>(static_cast<int64_t>(n_groups) * Hkv * a.n_qg));
+  const dim3 merge_grid(static_cast<uint32_t>(plan ? n_merge : 0));
 #define CS_ATTN_LAUNCH(DV)                                                              \
   do {                                                                                  \
-    hipLaunchKernelGGL(prefix_attn_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a);      \
-    if (a.n_split > 1)                                                                  \
+    if (plan)                                                                           \
+      hipLaunchKernelGGL((prefix_attn_kernel<DV, true>), grid, dim3(kAttnThreads), 0, st, a); \
+    else                                                                                \
+      hipLaunchKernelGGL((prefix_attn_kernel<DV, false>), grid, dim3(kAttnThreads), 0, st, a); \
+    if (plan)                                                                           \
       hipLaunchKernelGGL(attn_merge_kernel<DV>, merge_grid, dim3(kAttnThreads), 0, st, a); \
   } while (0)
   if (D == 64) {

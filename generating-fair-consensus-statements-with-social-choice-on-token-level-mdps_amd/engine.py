@@ -217,7 +217,8 @@ class ScoringEngine:
                                   device=dev) for _ in range(c.n_layers)]
                 h = m.forward_streams(ids.reshape(-1), _empty_prefix(m), hk, hv,
                                       torch.zeros(1, dtype=torch.int32, device=dev), 1, Pb,
-                                      group_prefix=torch.zeros(nb, dtype=torch.int32, device=dev))
+                                      group_prefix=torch.zeros(nb, dtype=torch.int32, device=dev),
+                                      group_prefix_host=[0] * nb)
                 h = h.view(nb, Pb, -1)
                 kv = [(k, ops.rows_from_blocked(v)) for k, v in zip(hk, hv)]
             else:
@@ -232,7 +233,7 @@ class ScoringEngine:
         del vrs
         fp = FusedPrefix(k=ks, vt=vts, off=torch.as_tensor(off[:-1], dtype=torch.int64, device=dev),
                          lengths=torch.as_tensor(lens, dtype=torch.int32, device=dev),
-                         max_len=max(lens))
+                         max_len=max(lens), lens_host=list(lens))
         return StreamPrefix(fused=fp, last_hidden=last,
                             lengths=torch.as_tensor(lens, dtype=torch.long, device=dev), lens=lens)
 
@@ -409,7 +410,8 @@ class ScoringEngine:
                 gp = torch.as_tensor(gs, dtype=torch.int32, device=dev)
                 # one history buffer serves every layer: a chunk's K/V are not kept
                 h = m.forward_streams(toks[:, :Tc - 1].reshape(-1), pfx, [hk] * c.n_layers,
-                                      [hv] * c.n_layers, hb, n_str, Tc - 1, group_prefix=gp)
+                                      [hv] * c.n_layers, hb, n_str, Tc - 1, group_prefix=gp,
+                                      group_prefix_host=list(gs))
                 hpad = torch.cat([last[:, None, :], h.view(S, Tc - 1, -1)], dim=1)   # [S, Tc, d]
                 del h, hk, hv
             else:
@@ -612,6 +614,7 @@ class FusedPrefix:
     off: torch.Tensor           # [n_prefix] int64 (device)
     lengths: torch.Tensor       # [n_prefix] int32 (device)
     max_len: int                # host copy of max(lengths)
+    lens_host: Optional[List[int]] = None   # host copies of the lengths (or bounds), if known
 
 
 @dataclass
@@ -632,7 +635,7 @@ def _empty_prefix(m: Model) -> FusedPrefix:
         k=[torch.zeros(c.n_kv_heads, 32, c.head_dim, dtype=m.dtype, device=dev)] * c.n_layers,
         vt=[torch.zeros(c.n_kv_heads, 1, c.head_dim, 32, dtype=m.dtype, device=dev)] * c.n_layers,
         off=torch.zeros(1, dtype=torch.int64, device=dev),
-        lengths=torch.zeros(1, dtype=torch.int32, device=dev), max_len=0)
+        lengths=torch.zeros(1, dtype=torch.int32, device=dev), max_len=0, lens_host=[0])
 
 
 def _offsets32(lens: Sequence[int]) -> List[int]:

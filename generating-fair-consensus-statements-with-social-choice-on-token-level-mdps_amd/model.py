@@ -24,7 +24,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field, replace
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.nn.functional as F
@@ -377,7 +377,8 @@ class Model:
     @torch.no_grad()
     def forward_streams(self, tokens: torch.Tensor, pfx, hist_k: List[torch.Tensor],
                         hist_vt: List[torch.Tensor], hist_base: torch.Tensor, n_str: int, T: int,
-                        group_prefix: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        group_prefix: Optional[torch.Tensor] = None,
+                        group_prefix_host: Optional[Sequence[int]] = None) -> torch.Tensor:
         """T new tokens for each of S = n_groups * n_str streams (tokens [S*T], stream-major):
         stream s = i * n_str + b attends to its group's prefix (pfx: engine.FusedPrefix, the
         ragged layouts of include/consensus_scoring.h cs_prefix_attention; group i uses
@@ -386,7 +387,8 @@ class Model:
         K / V are written to slots hist_base + t.  Per layer: one fused q|k|v GEMM,
         cs_rope_place, cs_prefix_attention, output GEMM, MLP.  No host synchronisation and
         no shape depends on hist_base: a decode step is graph-capturable.  Returns the
-        final-norm hidden [S*T, d]."""
+        final-norm hidden [S*T, d].  pfx.lens_host (+ group_prefix_host) size the key splits
+        of the attention work plan."""
         from . import ops   # local: model.py stays importable without the library
         c = self.cfg
         H, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
@@ -408,7 +410,9 @@ class Model:
                                      hist_k[i], hist_vt[i], hist_base, n_str, T, scale=scale,
                                      softcap=c.attn_softcap,
                                      window=c.sliding_window if i % 2 == 0 else 0,
-                                     group_prefix=group_prefix)
+                                     group_prefix=group_prefix,
+                                     prefix_len_host=getattr(pfx, "lens_host", None),
+                                     group_prefix_host=group_prefix_host)
             o = o.view(n_tok, H * D) @ self.w[p + "wo"].t()
             if g2:
                 o = ops.add_rms_norm(o, self.w[p + "post_attn_norm"], eps, plus_one=True)

@@ -9,8 +9,11 @@ Reference semantics each op restates are cited on the op.
 """
 from __future__ import annotations
 
-from typing import Optional
+import collections
+import ctypes
+from typing import Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -440,7 +443,60 @@ def vocab_sample(logits: torch.Tensor, seeds: torch.Tensor, *, temperature: floa
     return ids, lp
 
 
-_attn_ws: dict = {}
+class AttnPlan:
+    """A cs_prefix_attention work plan on the device (entries, counts) and the split
+    partials' workspace it needs; built once per (prefix-length bounds, shape) and reused by
+    every launch (and graph replay) of that shape."""
+
+    def __init__(self, entries: Optional[torch.Tensor], n_attn: int, n_merge: int,
+                 workspace: Optional[torch.Tensor]) -> None:
+        self.entries, self.n_attn, self.n_merge, self.workspace = entries, n_attn, n_merge, workspace
+
+
+_attn_plans: "collections.OrderedDict" = collections.OrderedDict()
+_ATTN_PLAN_CACHE = 64
+
+
+def attention_plan(prefix_len_host: Sequence[int], group_prefix_host: Optional[Sequence[int]],
+                   n_groups: int, n_str: int, T: int, H: int, Hkv: int, D: int, ld_hist: int,
+                   device) -> AttnPlan:
+    """The work plan of cs_prefix_attention_plan for host bounds of the prefix lengths
+    (cached; the device copy is made outside any graph capture)."""
+    key = (tuple(int(x) for x in prefix_len_host),
+           None if group_prefix_host is None else tuple(int(x) for x in group_prefix_host),
+           n_groups, n_str, T, H, Hkv, D, ld_hist, str(device))
+    plan = _attn_plans.get(key)
+    if plan is not None:
+        _attn_plans.move_to_end(key)
+        return plan
+    if torch.cuda.is_current_stream_capturing():
+        raise CSError("cs_prefix_attention: the work plan of this shape must be built before "
+                      "graph capture (run the step once eagerly)")
+    L = _lib.load()
+    lens = np.ascontiguousarray(np.asarray(key[0], dtype=np.int32))
+    gp = None if key[1] is None else np.ascontiguousarray(np.asarray(key[1], dtype=np.int32))
+    n_a, n_m = ctypes.c_int32(0), ctypes.c_int32(0)
+    wsb = ctypes.c_size_t(0)
+    args = (lens.ctypes.data, lens.size, None if gp is None else gp.ctypes.data, n_groups, n_str,
+            T, H, Hkv, D, ld_hist)
+    total = int(L.cs_prefix_attention_plan(*args, None, 0, ctypes.byref(n_a), ctypes.byref(n_m),
+                                           ctypes.byref(wsb)))
+    if total < 0:
+        _lib.check(total, "cs_prefix_attention_plan")
+    if total == 0:
+        plan = AttnPlan(None, 0, 0, None)
+    else:
+        host = np.zeros((total, 4), dtype=np.int32)
+        rc = int(L.cs_prefix_attention_plan(*args, host.ctypes.data, total, ctypes.byref(n_a),
+                                            ctypes.byref(n_m), ctypes.byref(wsb)))
+        if rc != total:
+            _lib.check(rc if rc < 0 else -1, "cs_prefix_attention_plan")
+        plan = AttnPlan(torch.from_numpy(host).to(device), n_a.value, n_m.value,
+                        torch.empty(max(int(wsb.value), 16), dtype=torch.uint8, device=device))
+    _attn_plans[key] = plan
+    while len(_attn_plans) > _ATTN_PLAN_CACHE:
+        _attn_plans.popitem(last=False)
+    return plan
 
 
 def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.Tensor,
@@ -448,7 +504,9 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
                      k_hist: torch.Tensor, vt_hist: torch.Tensor, hist_base: torch.Tensor,
                      n_str: int, T: int, *, scale: float, softcap: float = 0.0, window: int = 0,
                      group_prefix: Optional[torch.Tensor] = None,
-                     out: Optional[torch.Tensor] = None, workspace: Optional[Workspace] = None):
+                     prefix_len_host: Optional[Sequence[int]] = None,
+                     group_prefix_host: Optional[Sequence[int]] = None,
+                     out: Optional[torch.Tensor] = None, plan: Optional[AttnPlan] = None):
     """Cascade attention of candidate streams over shared per-agent prefix K/V
     (cs_prefix_attention; layouts in include/consensus_scoring.h).
 
@@ -456,9 +514,11 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     (ragged prefixes: prefix p's keys are rows prefix_off[p] ..; V transposed in 32-key
     tiles, see blocked_vt); prefix_off [n_prefix] int64, prefix_len [n_prefix] int32
     (device), max_prefix_len >= every prefix_len (host); k_hist [S, Hkv, ldh, D], vt_hist
-    [S, Hkv, ldh/32, D, 32] (S = n_groups*n_str); hist_base [1]
-    int32 (device).  Returns out [n_tok, H, D] bf16.  Replaces the per-call prompt
-    re-encoding of src/utils.py:249-259."""
+    [S, Hkv, ldh/32, D, 32] (S = n_groups*n_str); hist_base [1] int32 (device).
+    prefix_len_host (per prefix) / group_prefix_host: host bounds that size the key splits
+    of the work plan (default: max_prefix_len everywhere); ``plan`` overrides them.
+    Returns out [n_tok, H, D] bf16.  Replaces the per-call prompt re-encoding of
+    src/utils.py:249-259."""
     L = _lib.load()
     if q.dim() != 3 or q.dtype != torch.bfloat16 or not q.is_contiguous():
         raise CSError("q must be a contiguous [n_tok, H, D] bfloat16 tensor")
@@ -492,16 +552,25 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     if out is None:
         out = torch.empty_like(q)
     mpl = int(max_prefix_len)
-    nbytes = int(L.cs_prefix_attention_workspace_size(n_groups, n_str, T, H, Hkv, D, mpl, ldh))
-    if workspace is None:
-        workspace = _attn_ws.setdefault(q.device, Workspace())
-    ws = workspace.get(nbytes, q.device)
+    if plan is None:
+        if prefix_len_host is None or (group_prefix is not None and group_prefix_host is None):
+            # no host lengths: every group bounded by max_prefix_len
+            lens_h, gp_h = [mpl], [0] * n_groups
+        else:
+            lens_h = [min(int(x), mpl) for x in prefix_len_host]
+            gp_h = None if group_prefix is None else list(group_prefix_host)
+            if len(lens_h) != n_prefix or (gp_h is not None and len(gp_h) != n_groups):
+                raise CSError("prefix_len_host / group_prefix_host sizes do not match")
+        plan = attention_plan(lens_h, gp_h, n_groups, n_str, T, H, Hkv, D, ldh, q.device)
+    ws = plan.workspace
     rc = L.cs_prefix_attention(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), Lp,
                                prefix_off.data_ptr(), prefix_len.data_ptr(), mpl,
                                group_prefix.data_ptr() if group_prefix is not None else None,
                                n_groups, k_hist.data_ptr(), vt_hist.data_ptr(), ldh,
                                hist_base.data_ptr(), n_str, T, H, Hkv, D, float(scale),
-                               float(softcap), int(window), out.data_ptr(),
+                               float(softcap), int(window),
+                               plan.entries.data_ptr() if plan.entries is not None else None,
+                               plan.n_attn, plan.n_merge, out.data_ptr(),
                                ws.data_ptr() if ws is not None else None,
                                ws.numel() if ws is not None else 0, _stream())
     _lib.check(rc, "cs_prefix_attention")

@@ -269,41 +269,55 @@ int cs_vocab_sample(const void* logits, int dtype, int64_t rows, int64_t vocab, 
  * n_groups groups of n_str streams each; group i uses prefix group_prefix[i] (NULL =
  * identity).  Stream s = i*n_str + b carries T query tokens; token t of stream s is
  * q[(s*T + t)][H][D] and sees
- *     prefix keys  [0, prefix_len[pfx])       k_prefix [Hkv][ld_prefix][D],
- *                                             vt_prefix [Hkv][D][ld_prefix]: prefix p's key
- *                                             j is row prefix_off[p] + j (ragged prefixes
- *                                             in one buffer; prefix_off[p] % 32 == 0 and
- *                                             rows up to the next multiple of 32 readable)
- *     its history  [0, *hist_base + t]        k_hist  [S][Hkv][ld_hist][D],
- *                                             vt_hist [S][Hkv][D][ld_hist]
- * (V transposed: key-contiguous rows; ld_prefix, ld_hist multiples of 32; key slots past
- * the visible range must hold finite values).  out [(s*T + t)][H][D].  Query head h uses
- * K/V head h / (H / Hkv).  scores = q.k * scale, then softcap * tanh(./softcap) when
- * softcap > 0 (Gemma-2 attention soft-cap), softmax over the visible keys; window > 0
- * also hides keys more than window - 1 positions behind the query (Gemma-2's sliding
- * window; prefix key j sits at position j, history slot j at prefix_len + j).  D in
- * {64, 128, 256}.  hist_base lives in device memory so that a captured decode step
- * replays with a growing history.  max_prefix_len (host) bounds prefix_len and sizes the
- * key split.  One workgroup holds all query rows of (group, K/V head) (64 per
- * workgroup), so a prefix key block is read once for every candidate of that agent.
- * Workspace: cs_prefix_attention_workspace_size() bytes (0 = none needed); results are
- * deterministic (fixed-order split merge).
+ *     prefix keys  [0, prefix_len[pfx])   k_prefix  [Hkv][ld_prefix][D]
+ *                                         vt_prefix [Hkv][ld_prefix/32][D][32]
+ *                                         prefix p's key j is row prefix_off[p] + j (ragged
+ *                                         prefixes in one buffer; prefix_off[p] % 32 == 0,
+ *                                         rows up to the next multiple of 32 readable)
+ *     its history  [0, *hist_base + t]    k_hist  [S][Hkv][ld_hist][D]
+ *                                         vt_hist [S][Hkv][ld_hist/32][D][32]
+ * V is stored transposed in 32-key tiles: keys 32c .. 32c+31 are the tile
+ * vt[..][c][0..D)[0..32), key-contiguous rows of 64 B.  ld_prefix, ld_hist multiples of 32;
+ * key slots past the visible range must hold finite values.  out [(s*T + t)][H][D].
+ * Query head h uses K/V head h / (H / Hkv).  scores = q.k * scale, then
+ * softcap * tanh(./softcap) when softcap > 0 (Gemma-2 attention soft-cap), softmax over the
+ * visible keys; window > 0 also hides keys more than window - 1 positions behind the query
+ * (Gemma-2's sliding window; prefix key j sits at position j, history slot j at
+ * prefix_len + j).  D in {64, 128, 256}.  hist_base lives in device memory so that a
+ * captured decode step replays with a growing history.  max_prefix_len (host) bounds
+ * prefix_len.  One workgroup holds all query rows of (group, K/V head) (64 per workgroup),
+ * so a prefix key block is read once for every candidate of that agent.
+ *
+ * Work plan: when few (group, head, query group) cells would leave the chip idle (decode
+ * steps), each cell's keys are split over several workgroups and the splits merged in a
+ * second launch.  cs_prefix_attention_plan (host) sizes the splits per cell from host
+ * bounds of the prefix lengths (prefix_len[p] >= the device length; the split count is a
+ * performance choice only) and the history capacity, and writes int32 x 4 entries:
+ *     plan == NULL:  returns the entry count (0 = no plan needed: pass plan = NULL, no
+ *                    workspace), n_attn / n_merge / workspace_bytes through the pointers;
+ *     plan != NULL:  fills up to plan_cap entries.
+ * The caller copies the entries to device memory once per prefix set and passes them with
+ * n_attn, n_merge and a workspace of workspace_bytes.  Results are deterministic (fixed-order
+ * split merge), and equal for every plan up to fp32 reassociation.
  *
  * Replaces: the per-(agent, candidate) re-encoding of the agent's whole prompt behind
  *   every get_prompt_logprobs call (src/utils.py:249-259; driven per candidate at
  *   src/methods/beam_search.py:495-538, best_of_n.py:266-321,
  *   finite_lookahead.py:464-524, src/evaluation.py:177-230).
  */
-size_t cs_prefix_attention_workspace_size(int32_t n_groups, int32_t n_str, int32_t T, int32_t H,
-                                          int32_t Hkv, int32_t D, int32_t max_prefix_len,
-                                          int64_t ld_hist);
+int64_t cs_prefix_attention_plan(const int32_t* prefix_len, int32_t n_prefix,
+                                 const int32_t* group_prefix, int32_t n_groups, int32_t n_str,
+                                 int32_t T, int32_t H, int32_t Hkv, int32_t D, int64_t ld_hist,
+                                 int32_t* plan, int64_t plan_cap, int32_t* n_attn, int32_t* n_merge,
+                                 size_t* workspace_bytes);
 int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
                         int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
                         int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
                         const void* k_hist, const void* vt_hist, int64_t ld_hist,
                         const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
-                        int32_t D, float scale, float softcap, int32_t window, void* out,
-                        void* workspace, size_t workspace_bytes, cs_stream_t stream);
+                        int32_t D, float scale, float softcap, int32_t window, const void* plan,
+                        int32_t n_attn, int32_t n_merge, void* out, void* workspace,
+                        size_t workspace_bytes, cs_stream_t stream);
 
 /*
  * cs_rope_place — rotary embedding (half-rotation convention, angle = position *

@@ -106,3 +106,86 @@ def test_ops_refuse_cpu_tensors(ops):
     t = torch.zeros(4, 1, dtype=torch.int32)
     with pytest.raises(ops.CSError):
         ops.logsoftmax_gather(x, t)
+
+
+def _plan(L, lens, gmap, n_str, T, H, Hkv, D, ldh):
+    import numpy as np
+    lens = np.asarray(lens, dtype=np.int32)
+    gp = None if gmap is None else np.asarray(gmap, dtype=np.int32)
+    n_groups = len(lens) if gmap is None else len(gmap)
+    na, nm, ws = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_size_t()
+    args = (lens.ctypes.data, lens.size, None if gp is None else gp.ctypes.data, n_groups, n_str,
+            T, H, Hkv, D, ldh)
+    total = L.cs_prefix_attention_plan(*args, None, 0, ctypes.byref(na), ctypes.byref(nm),
+                                       ctypes.byref(ws))
+    if total <= 0:
+        return total, None, 0, 0, 0
+    out = np.zeros((total, 4), dtype=np.int32)
+    assert L.cs_prefix_attention_plan(*args, out.ctypes.data, total, ctypes.byref(na),
+                                      ctypes.byref(nm), ctypes.byref(ws)) == total
+    return total, out, na.value, nm.value, ws.value
+
+
+@pytest.mark.parametrize("shape", [
+    # lens, group map, n_str, T, H, Hkv, D, ldh
+    ([5500] + [210] * 64, None, 8, 1, 64, 8, 128, 32),      # C5 decode: one long reference prompt
+    ([1700] + [210] * 16, None, 16, 1, 16, 8, 256, 32),     # C3 decode
+    ([600] + [210] * 4, None, 4, 1, 32, 8, 64, 64),         # C1 decode
+    ([3000, 700], [1, 0, 1], 4, 1, 32, 8, 64, 96),          # group -> prefix map
+    ([0], [0, 0], 1, 300, 32, 8, 128, 320),                 # prompts as streams: no prefix
+])
+def test_prefix_attention_plan_covers_every_cell(pkg, shape):
+    """cs_prefix_attention_plan (host): every (group, head, query group) cell is covered by
+    exactly n_used attention entries with splits 0 .. n_used-1; split cells own distinct
+    partial slots inside the workspace and are merged row chunk by row chunk."""
+    from importlib import import_module
+    L = import_module(pkg.__name__ + "._lib").load()
+    lens, gmap, n_str, T, H, Hkv, D, ldh = shape
+    total, plan, na, nm, ws = _plan(L, lens, gmap, n_str, T, H, Hkv, D, ldh)
+    n_groups = len(lens) if gmap is None else len(gmap)
+    M = n_str * T * (H // Hkv)
+    n_qg = -(-M // 64)
+    if plan is None:                      # enough cells without splits
+        assert total == 0 and n_groups * Hkv * n_qg >= 1024 or total == 0
+        return
+    assert total == na + nm and nm > 0
+    att, mer = plan[:na], plan[na:]
+    cells = {}
+    slots = set()
+    for pg, qg, z, slot in att.tolist():
+        sp, nu = z & 255, z >> 8
+        assert 0 <= pg < n_groups * Hkv and 0 <= qg < n_qg and 1 <= nu <= 32 and sp < nu
+        cells.setdefault((pg, qg), set()).add((sp, nu))
+        if nu > 1:
+            assert slot not in slots
+            slots.add(slot)
+    assert len(cells) == n_groups * Hkv * n_qg
+    for key, ss in cells.items():
+        nu = next(iter(ss))[1]
+        assert ss == {(s, nu) for s in range(nu)}, key
+    assert ws == len(slots) * 64 * (D + 2) * 4
+    merged = {}
+    for pg, qg, slot0, z in mer.tolist():
+        ch, nu = z & 255, z >> 8
+        assert nu > 1 and 0 <= slot0 and slot0 + nu <= len(slots)
+        merged.setdefault((pg, qg), []).append(ch)
+    for key, ss in cells.items():
+        nu = next(iter(ss))[1]
+        if nu > 1:
+            rows = min(64, M - key[1] * 64)
+            assert sorted(merged[key]) == list(range(-(-rows // 8))), key
+        else:
+            assert key not in merged
+    # the long reference prompt's cells split further than the agents' short ones
+    if gmap is None and lens[0] > 4 * lens[-1]:
+        nu_of = {pg // Hkv: z >> 8 for pg, qg, z, _ in att.tolist()}
+        assert nu_of[0] > nu_of[len(lens) - 1]
+
+
+def test_prefix_attention_plan_rejects_bad_arguments(pkg):
+    from importlib import import_module
+    L = import_module(pkg.__name__ + "._lib").load()
+    assert _plan(L, [100, 100], [0, 5], 4, 1, 32, 8, 128, 32)[0] == -1     # prefix index range
+    assert _plan(L, [100], None, 4, 1, 30, 8, 128, 32)[0] == -1            # H % Hkv
+    assert _plan(L, [100], None, 4, 1, 32, 8, 96, 32)[0] == -1             # head_dim
+    assert _plan(L, [100], None, 4, 1, 32, 8, 128, 40)[0] == -1            # ld_hist % 32

@@ -64,6 +64,8 @@ CASES = [
     (2, 3, 1, 4, 4, 64, [31, 33], 0, 0.0, None),                       # rep 1, first step
     (2, 4, 3, 16, 8, 256, [300, 120], 40, 50.0, None, 64),             # Gemma sliding window
     (3, 8, 1, 16, 8, 256, [500, 64, 250], 30, 50.0, None, 100),        # window, decode shape
+    (5, 8, 1, 64, 8, 128, [2000, 100, 90, 210, 150], 25, 0.0, None),   # C5 mix: long ref prompt
+    (2, 4, 1, 32, 8, 64, [3000, 700], 60, 0.0, [1, 0]),                # long prefixes, mapped
 ]
 
 
@@ -106,12 +108,18 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
     gp = torch.tensor(gmap, dtype=torch.int32, device=dev) if gmap is not None else None
     scale = D ** -0.5 * (4.0 if cap else 1.0)      # the cap case drives scores into the cap
 
-    def run():
+    vth = ops.blocked_vt(vh)
+
+    def run(**kw):
         return ops.prefix_attention(q, kflat, vtflat, offt, plen, max(plens), kh,
-                                    ops.blocked_vt(vh), hbt, n_str, T, scale=scale,
-                                    softcap=cap, window=window, group_prefix=gp)
+                                    vth, hbt, n_str, T, scale=scale,
+                                    softcap=cap, window=window, group_prefix=gp, **kw)
 
     out = run()
+    # every work plan gives the same attention: exact host lengths (per-group key splits),
+    # and no plan at all (one workgroup per (group, head, query group))
+    outs = {"exact": run(prefix_len_host=plens, group_prefix_host=gmap),
+            "plain": run(plan=ops.AttnPlan(None, 0, 0, None))}
     torch.cuda.synchronize()
     # reference on padded per-prefix tensors [n_prefix, Hkv, Pmax, D]
     Pm = max(plens)
@@ -121,9 +129,10 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
         kp[i, :, :k.shape[1]] = k
         vp[i, :, :v.shape[1]] = v
     ref = ref_attention(q, kp, vp, plens, kh, vh, hb, n_str, T, scale, cap, gmap, window)
-    err = (out.float() - ref).abs()
     bound = 2e-2 + 2e-2 * ref.abs()
-    assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}"
+    for name, o in [("default", out)] + list(outs.items()):
+        err = (o.float() - ref).abs()
+        assert bool((err <= bound).all()), f"{name}: max err {float(err.max()):.3e}"
     assert torch.equal(out, run())          # deterministic: bit-identical relaunch
 
 

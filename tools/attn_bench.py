@@ -32,6 +32,12 @@ def ceil32(n):
 
 def run(name, reps=50):
     ops = importlib.import_module(PKG + ".ops")
+    if "=" in name:     # ad-hoc shape: name=nA,La,Lr,n_str,T,H,Hkv,D,G,cap (Lr 0: none)
+        name, spec = name.split("=", 1)
+        v = [float(x) for x in spec.split(",")]
+        SHAPES[name] = tuple(int(x) for x in v[:9]) + (v[9],)
+        if not SHAPES[name][2]:
+            SHAPES[name] = SHAPES[name][:2] + (None,) + SHAPES[name][3:]
     nA, La, Lr, n_str, T, H, Hkv, D, G, cap = SHAPES[name]
     dev = torch.device("cuda:0")
     lens = [La] * nA + ([Lr] if Lr else [])
@@ -55,7 +61,7 @@ def run(name, reps=50):
 
     def go():
         ops.prefix_attention(q, kp, vt, offt, plen, max(lens), kh, vh, hb, n_str, T,
-                             scale=D ** -0.5, softcap=cap, out=out)
+                             scale=D ** -0.5, softcap=cap, out=out, prefix_len_host=lens)
 
     for _ in range(5):
         go()
