@@ -830,6 +830,7 @@ def main():
         return
     dev = torch.device("cuda", torch.cuda.current_device())
     par = importlib.import_module(PKG_DIR + ".parallel")
+    gemm_tuning = importlib.import_module(PKG_DIR + ".runtime").use_gemm_tuning()
 
     errors = {}
 
@@ -901,6 +902,8 @@ def main():
                        "agents_per_gpu": A, "candidates": N, "tokens_per_candidate": T,
                        "vocab": V, "welfare": wkind,
                        "parallelism": f"agents sharded over {world} GPU(s)"},
+            "gemm_tuning": (os.path.relpath(gemm_tuning, os.path.dirname(os.path.abspath(__file__)))
+                            if gemm_tuning else None),
             "roofline": kern["roofline"],
             "cpu_baseline": cpu,
             "kernel_only": {k: v for k, v in kern.items() if k != "roofline"},

@@ -56,8 +56,8 @@ constexpr int kMaxSplit = 32;       // key splits of one (group, head, query gro
 constexpr int kPlanMinBase = 1024;  // from this many (group, head, query group) workgroups on,
                                     // the chip is full without key splits: no plan
 constexpr int kMergeRows = 8;       // query rows per merge workgroup (2 per wave)
-constexpr int kTargetWgsDefault = 1024;   // plan: split cells until about this many workgroups
-constexpr int kMinItemsDefault = 2;       // ... but never below this many key blocks per wave
+constexpr int kTargetWgsDefault = 512;    // plan: split cells until about this many workgroups
+constexpr int kMinItemsDefault = 3;       // ... but never below this many key blocks per wave
 
 // Work plan entries (int32 x 4, device memory), attention entries first:
 //   attention  {pg = group * Hkv + head, query group, split | n_used << 8, partial slot}

@@ -64,6 +64,12 @@ class Workspace:
             self.buf = alloc(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         return self.buf
 
+    def reset(self) -> None:
+        """Zero a zeroed workspace again (its arrival counters), e.g. after a failed launch
+        that may have stopped with counters half-counted."""
+        if self.zeroed and self.buf is not None and not torch.cuda.is_current_stream_capturing():
+            self.buf.zero_()
+
 
 _default_ws: dict = {}
 _beam_ws: dict = {}
@@ -305,6 +311,8 @@ def beam_step(logits: torch.Tensor, targets: torch.Tensor, rewards: torch.Tensor
                         kept_out.data_ptr() if kept_out is not None else None,
                         ws.data_ptr() if ws is not None else None,
                         ws.numel() if ws is not None else 0, _stream())
+    if rc != 0:
+        workspace.reset()
     _lib.check(rc, "cs_beam_step")
     if n_order == 0:
         return U, W, None, None
@@ -376,6 +384,8 @@ def beam_decode_step(ref_logits: torch.Tensor, logits: torch.Tensor, rewards: to
                                oval.data_ptr() if n_order else None,
                                kept_out.data_ptr() if kept_out is not None else None,
                                ws.data_ptr(), ws.numel(), _stream())
+    if rc != 0:
+        workspace.reset()
     _lib.check(rc, "cs_beam_decode_step")
     if n_order == 0:
         return ids, U, W, None, None

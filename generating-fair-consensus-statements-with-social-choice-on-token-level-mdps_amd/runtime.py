@@ -153,12 +153,53 @@ def _model_dir(model_identifier: str) -> Optional[str]:
     return None
 
 
+# --- GEMM solution selection -------------------------------------------------------
+GEMM_TUNING = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "gemm_mi355x.csv")
+_gemm_tuning: Optional[str] = None
+_gemm_tuning_tried = False
+
+
+def use_gemm_tuning(path: Optional[str] = None) -> Optional[str]:
+    """Pick each forward GEMM's hipBLASLt solution from a committed PyTorch TunableOp
+    results file (measured on MI355X by tools/tune_gemms.py) instead of the library
+    heuristic — read only, no tuning at run time; shapes not in the file keep the heuristic.
+    Returns the file in use (None: not used).  An explicit TunableOp session
+    (PYTORCH_TUNABLEOP_ENABLED in the environment, e.g. while tuning) is left alone;
+    CS_GEMM_TUNING=0 disables, CS_GEMM_TUNING=<file> selects another file."""
+    global _gemm_tuning, _gemm_tuning_tried
+    with _lock:
+        if _gemm_tuning_tried and path is None:
+            return _gemm_tuning
+        _gemm_tuning_tried = True
+        env = os.environ.get("CS_GEMM_TUNING")
+        if env == "0" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ or not torch.cuda.is_available():
+            return None
+        path = path or env or GEMM_TUNING
+        if not os.path.exists(path):
+            return None
+        import tempfile
+
+        import torch.cuda.tunable as tunable
+        tunable.enable(True)
+        tunable.tuning_enable(False)
+        tunable.record_untuned_enable(False)
+        # results are written back at exit to this file, never to the committed one
+        tunable.set_filename(os.path.join(tempfile.gettempdir(), f"cs_tunableop_{os.getpid()}.csv"))
+        if not tunable.read_file(path):
+            logger.warning("GEMM tuning file %s not usable here (versions differ?)", path)
+            tunable.enable(False)
+            return None
+        _gemm_tuning = path
+        return path
+
+
 def get_engine(model_identifier: str) -> Tuple[ScoringEngine, CharTokenizer]:
     with _lock:
         if model_identifier in _ENGINES:
             return _ENGINES[model_identifier]
         if not torch.cuda.is_available():
             raise ops.CSError("no HIP device: the scoring engine has no CPU path")
+        use_gemm_tuning()
         path = _model_dir(model_identifier)
         if path is not None:
             from .checkpoint import load_engine

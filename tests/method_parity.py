@@ -26,6 +26,10 @@ TOL = 1e-3
 
 
 TRACE_FILES = ["method_traces.json", "method_traces_gemma.json"]
+# BASELINE C1 shape (Llama-3.2-1B widths and vocabulary, 2 layers; beam 4, BoN N = 8, FL
+# bf 3 / depth 2): replayed on the GPU (the CPU emulation of its 128,256-wide LM head
+# over ~700 reference scoring calls is too slow for the CPU suite)
+GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json"]
 
 
 def load_traces(name: str = "method_traces.json"):

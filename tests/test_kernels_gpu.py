@@ -592,6 +592,43 @@ def test_fused_beam_launches_stress_shared_workspace(ops, dev):
         assert torch.equal(o[:o2.numel()], o2), it
 
 
+def test_fused_beam_decode_graph_replays_stress(ops, dev):
+    """The arrival-counter hand-offs under back-to-back hipGraph replays (no host gap between
+    launches, the counters of one replay reset by its last arrivers just before the next
+    replay's first arrivals): 300 replays of the C3-shaped decode step, every 50th compared
+    word for word with the eager unfused kernels."""
+    A, B, K, V, cap = 16, 16, 50, 64000, 30.0
+    g = torch.Generator(device=dev).manual_seed(5)
+    ref = (torch.randn(B, V, generator=g, device=dev) * 3.0).to(torch.bfloat16)
+    x = (torch.randn(A * B, V, generator=g, device=dev) * 3.0).to(torch.bfloat16)
+    R = -torch.rand(A, B, generator=g, device=dev) * 10.0
+    ids, _ = ops.vocab_topk(ref, K, softcap=cap)
+    U, W, o, _ = ops.beam_step(x, ids, R, "min", softcap=cap)
+    ws = ops.Workspace(zeroed=True)
+    out_ids = torch.empty(B, K, dtype=torch.int32, device=dev)
+    out_o = torch.empty(B * K, dtype=torch.int32, device=dev)
+    U2 = torch.empty(A, B * K, device=dev)
+    W2 = torch.empty(B * K, device=dev)
+    kw = dict(softcap=cap, workspace=ws, out_ids=out_ids, out_order=out_o, out_U=U2, out_W=W2)
+    ops.beam_decode_step(ref, x, R, K, "min", **kw)           # sizes the workspace
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            ops.beam_decode_step(ref, x, R, K, "min", **kw)
+    torch.cuda.current_stream().wait_stream(s)
+    for it in range(300):
+        graph.replay()
+        if it % 50 == 49:
+            torch.cuda.synchronize()
+            assert torch.equal(ids, out_ids), it
+            assert torch.equal(U, U2) and torch.equal(W, W2), it
+            assert torch.equal(o, out_o), it
+    assert int(ws.buf[:4096].count_nonzero()) == 0     # counters left at zero
+
+
 def _fuzz_cases(n=24, seed=2024):
     rng = np.random.default_rng(seed)
     cases = []

@@ -12,7 +12,7 @@ import method_parity as mp
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=mp.TRACE_FILES)
+@pytest.fixture(scope="module", params=mp.GPU_TRACE_FILES)
 def traces(request, dev):
     t = mp.load_traces(request.param)
     mp.register_fixture_engine(t, dev)
