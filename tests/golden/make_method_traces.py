@@ -36,7 +36,13 @@ FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
             # BASELINE C1 shape: Llama-3.2-1B widths (d 2048, 32/8 heads of 64, vocab
             # 128,256 -- the kernels' shapes) with 2 of its 16 layers, so that the
             # reference's ~1,300 serial CPU calls finish in minutes
-            "c1": ("llama-3.2-1b-shaped-fixture", "method_traces_c1.json")}
+            "c1": ("llama-3.2-1b-shaped-fixture", "method_traces_c1.json"),
+            # the byte-level BPE fixture tokenizer (tests/golden/bpe_fixture): the hosted
+            # API re-tokenizes every appended string, so beam candidates whose text merges
+            # with the statement differently than the id-level append are scored on the
+            # re-tokenized text by the reference
+            "bpe": ("tiny-llama-bpe-fixture", "method_traces_bpe.json")}
+BPE_DIR = os.path.join(HERE, "bpe_fixture")
 # untied LM head: with the random tied embedding a shallow model's residual stream makes
 # the last token's own logit ~45 sigma above the rest (every draw repeats it); an
 # independent head (std 0.02) gives logits of std ~1 and diverse samples
@@ -50,6 +56,9 @@ def fixture_model(family: str = "llama3"):
     if family == "c1":
         cfg = Mm.preset("llama-3.2-1b", **C1_OVERRIDES)
         tok = T.CharTokenizer("llama3", vocab_size=cfg.vocab)
+    elif family == "bpe":
+        tok = T.BPETokenizer(BPE_DIR, family="llama3")
+        cfg = Mm.preset("tiny-llama", vocab=tok.vocab_size)
     else:
         tok = T.CharTokenizer(family)
         name = "tiny-llama" if family == "llama3" else "tiny-gemma"
@@ -66,6 +75,18 @@ C1_RUNS = [
     ("best_of_n", {"n": 8, "max_tokens": 16, "seed": 7, "temperature": 1.0, "api_delay": 0,
                    "log_level": "WARNING"}),
     ("finite_lookahead", {"branching_factor": 3, "max_depth": 2, "max_tokens": 3, "seed": 11,
+                          "api_delay": 0, "log_level": "WARNING"}),
+]
+
+
+BPE_RUNS = [
+    ("beam_search", {"beam_width": 3, "max_tokens": 8, "max_sampling_attempts": 6, "seed": 3,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+    ("beam_search", {"beam_width": 2, "max_tokens": 10, "max_sampling_attempts": 4, "seed": 8,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+    ("best_of_n", {"n": 4, "max_tokens": 12, "seed": 7, "temperature": 1.0, "api_delay": 0,
+                   "log_level": "WARNING"}),
+    ("finite_lookahead", {"branching_factor": 2, "max_depth": 2, "max_tokens": 4, "seed": 11,
                           "api_delay": 0, "log_level": "WARNING"}),
 ]
 
@@ -124,12 +145,14 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
-           "family": "llama3" if args.family == "c1" else args.family,
+           "family": "llama3" if args.family in ("c1", "bpe") else args.family,
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
     if args.family == "c1":
         out["preset_overrides"] = dict(C1_OVERRIDES)
         out["tokenizer_vocab"] = cfg.vocab
-    runs = C1_RUNS if args.family == "c1" else [
+    if args.family == "bpe":
+        out["tokenizer"] = "bpe_fixture"
+    runs = C1_RUNS if args.family == "c1" else BPE_RUNS if args.family == "bpe" else [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,
                        "log_level": "WARNING"}),
         ("finite_lookahead", {"branching_factor": 2, "max_depth": 2, "max_tokens": 6, "seed": 11,

@@ -42,7 +42,12 @@ def register_fixture_engine(traces, device):
     T = importlib.import_module(PKG + ".tokenizer")
     E = importlib.import_module(PKG + ".engine")
     R = importlib.import_module(PKG + ".runtime")
-    tok = T.CharTokenizer(traces.get("family", "llama3"), vocab_size=traces.get("tokenizer_vocab", 0))
+    if traces.get("tokenizer") == "bpe_fixture":
+        tok = T.BPETokenizer(os.path.join(HERE, "golden", "bpe_fixture"),
+                             family=traces.get("family", "llama3"))
+    else:
+        tok = T.CharTokenizer(traces.get("family", "llama3"),
+                              vocab_size=traces.get("tokenizer_vocab", 0))
     cfg = Mm.preset(traces["preset"], vocab=traces["vocab"], **traces.get("preset_overrides", {}))
     cpu = Mm.Model(cfg, "cpu", torch.float32, seed=traces["weight_seed"])
     if "embed_scale" in traces:          # the C1-shaped fixture (make_method_traces.py)

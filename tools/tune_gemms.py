@@ -17,6 +17,7 @@ import os
 import shutil
 import subprocess
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
@@ -26,18 +27,37 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "gemm_tuned.csv"))
     ap.add_argument("--install", action="store_true")
-    ap.add_argument("--method", default="c1,c3,c5")
-    ap.add_argument("--iters", default="30")
-    ap.add_argument("--ms", default="30")
+    ap.add_argument("--resume", type=int, default=1)
+    ap.add_argument("--legs", default="e2e,c1,c3,c5")
+    ap.add_argument("--iters", default="10")
+    ap.add_argument("--ms", default="20")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    # continue from the installed results (TunableOp reads its file at start and only tunes
+    # the shapes it does not hold; device 0 writes <out stem>0.csv)
+    installed = os.path.join(REPO, PKG, "tuned", "gemm_mi355x.csv")
+    first = os.path.splitext(args.out)[0] + "0.csv"
+    if args.resume and os.path.exists(installed) and not os.path.exists(first):
+        shutil.copy(installed, first)
     env = dict(os.environ, PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="1",
                PYTORCH_TUNABLEOP_FILENAME=args.out, PYTORCH_TUNABLEOP_VERBOSE="1",
                PYTORCH_TUNABLEOP_MAX_TUNING_ITERATIONS=args.iters,
                PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=args.ms)
-    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
-           "--beam", "", "--cpu-seconds", "0", "--method", args.method]
-    rc = subprocess.call(cmd, env=env, cwd=REPO)
+    # one child per leg (each appends its new shapes to the same results file), a heartbeat
+    # line every 30 s while a child tunes
+    legs = [(m, ["--method", ""] if m == "e2e" else ["--e2e", "0", "--method", m])
+            for m in args.legs.split(",") if m]
+    rc = 0
+    for name, extra in legs:
+        cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup",
+               "1", "--beam", "", "--cpu-seconds", "0"] + extra
+        t0 = time.time()
+        p = subprocess.Popen(cmd, env=env, cwd=REPO)
+        while p.poll() is None:
+            time.sleep(30)
+            print(f"tuning {name}: {time.time() - t0:.0f} s", flush=True)
+        rc = rc or p.returncode
+        print(f"leg {name}: rc {p.returncode}, {time.time() - t0:.0f} s", flush=True)
     outs = sorted(glob.glob(os.path.splitext(args.out)[0] + "*.csv"))
     print("tuning results:", outs, "rc", rc, flush=True)
     if rc == 0 and args.install and outs:
