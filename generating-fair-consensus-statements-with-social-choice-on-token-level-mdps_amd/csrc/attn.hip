@@ -452,33 +452,38 @@ struct RopeParams {
   int32_t n_str, T, H, Hkv, D;
 };
 
-// one thread per (token, 4 consecutive rotation pairs): the 4 angles' sincos once, then
-// every head of the token (q, k rotated; v placed) with 8-byte loads / stores
+// one workgroup per token: the token's D/2 angles' sincos once into LDS, then every
+// (head, 4-pair quad) of the token (q, k rotated; v placed) by its own thread with 8-byte
+// loads / stores — all of a token's heads in flight at once (a per-thread loop over the
+// heads serialised one memory round trip per head: ~30 us per decode step and layer)
 __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
+  __shared__ float cs[128], sn[128];                // D / 2 <= 128
   const int half = r.D >> 1;
   const int nq = half >> 2;                         // 4-pair quads per head
   const int nh = r.H + 2 * r.Hkv;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (idx >= r.n_tok * nq) return;
-  const int i0 = 4 * static_cast<int>(idx % nq);
-  const int64_t tok = idx / nq;
+  const int64_t tok = blockIdx.x;
   const int64_t s = tok / r.T;
   const int t = static_cast<int>(tok % r.T);
   const int gi = static_cast<int>(s / r.n_str);
   const int p = r.gpfx ? r.gpfx[gi] : gi;
   const int slot = *r.hist_base + t;
   const float pos = static_cast<float>(r.plen[p] + slot);
-  float cs[4], sn[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sincosf(pos * r.inv_freq[i0 + e], &sn[e], &cs[e]);
-  const __bf16* row = r.qkv + tok * r.ldqkv;
-  for (int hh = 0; hh < nh; ++hh) {
+  for (int i = threadIdx.x; i < half; i += 256) sincosf(pos * r.inv_freq[i], &sn[i], &cs[i]);
+  __syncthreads();
+  const __bf16* __restrict__ row = r.qkv + tok * r.ldqkv;
+  __bf16* __restrict__ qo = r.q_out;
+  __bf16* __restrict__ kh = r.kh;
+  __bf16* __restrict__ vth = r.vth;
+#pragma unroll 4
+  for (int item = threadIdx.x; item < nh * nq; item += 256) {
+    const int hh = item / nq;
+    const int i0 = 4 * (item - hh * nq);
     const __bf16* src = row + static_cast<int64_t>(hh) * r.D + i0;
     const bf16x4 a = *reinterpret_cast<const bf16x4*>(src);
     const bf16x4 b = *reinterpret_cast<const bf16x4*>(src + half);
     if (hh >= r.H + r.Hkv) {                         // v: transposed placement, no rotation
       const int g = hh - r.H - r.Hkv;
-      __bf16* dst = r.vth + ((s * r.Hkv + g) * r.ldh + (slot & ~31)) * r.D +
+      __bf16* dst = vth + ((s * r.Hkv + g) * r.ldh + (slot & ~31)) * r.D +
                     static_cast<int64_t>(i0) * 32 + (slot & 31);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -491,11 +496,11 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float x1 = static_cast<float>(a[e]), x2 = static_cast<float>(b[e]);
-      y1[e] = static_cast<__bf16>(fmaf(x1, cs[e], -x2 * sn[e]));
-      y2[e] = static_cast<__bf16>(fmaf(x2, cs[e], x1 * sn[e]));
+      y1[e] = static_cast<__bf16>(fmaf(x1, cs[i0 + e], -x2 * sn[i0 + e]));
+      y2[e] = static_cast<__bf16>(fmaf(x2, cs[i0 + e], x1 * sn[i0 + e]));
     }
-    __bf16* dst = hh < r.H ? r.q_out + (tok * r.H + hh) * r.D
-                           : r.kh + ((s * r.Hkv + (hh - r.H)) * r.ldh + slot) * r.D;
+    __bf16* dst = hh < r.H ? qo + (tok * r.H + hh) * r.D
+                           : kh + ((s * r.Hkv + (hh - r.H)) * r.ldh + slot) * r.D;
     *reinterpret_cast<bf16x4*>(dst + i0) = y1;
     *reinterpret_cast<bf16x4*>(dst + half + i0) = y2;
   }
@@ -510,24 +515,49 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
     const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
     __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
     int64_t S, int32_t Hkv, int32_t ldh, int32_t D) {
-  // one workgroup per (layer, stream, head)
-  const int64_t lsg = blockIdx.x;
-  const int g = static_cast<int>(lsg % Hkv);
-  const int64_t ls = lsg / Hkv;
+  // one workgroup per (layer, stream): all Hkv heads' K rows and V^T tiles, 16-byte
+  // vectors, 8 per thread in flight
+  const int64_t ls = blockIdx.x;
   const int64_t l = ls / S, s = ls % S;
   const int hb = min(*hist_base, ldh);
   if (hb <= 0) return;
   const int64_t p = parent[s];
   const int64_t per = static_cast<int64_t>(ldh) * D;                 // elements per (l, s, g)
-  const int64_t so = ((l * S + p) * Hkv + g) * per, dn = ((l * S + s) * Hkv + g) * per;
-  // K: hb * D contiguous elements
-  const int kv = hb * D / 8;
-  for (int i = threadIdx.x; i < kv; i += 256)
-    reinterpret_cast<u32x4_t*>(dst_k + dn)[i] = reinterpret_cast<const u32x4_t*>(src_k + so)[i];
-  // V^T tiles: the first ceil32(hb) slots are ceil32(hb) * D contiguous elements
-  const int vv = ((hb + 31) & ~31) * D / 8;
-  for (int i = threadIdx.x; i < vv; i += 256)
-    reinterpret_cast<u32x4_t*>(dst_v + dn)[i] = reinterpret_cast<const u32x4_t*>(src_v + so)[i];
+  const int64_t so = (l * S + p) * Hkv * per, dn = (l * S + s) * Hkv * per;
+  const int kv = hb * D / 8;                                          // K: hb * D contiguous
+  const int vv = ((hb + 31) & ~31) * D / 8;                           // V^T: ceil32(hb) slots
+  const int pv = static_cast<int>(per / 8);
+  const u32x4_t* sk = reinterpret_cast<const u32x4_t*>(src_k + so);
+  const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(src_v + so);
+  u32x4_t* dk = reinterpret_cast<u32x4_t*>(dst_k + dn);
+  u32x4_t* dv = reinterpret_cast<u32x4_t*>(dst_v + dn);
+  const int nk = Hkv * kv, n = nk + Hkv * vv;
+  constexpr int U = 8;
+  for (int i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
+    u32x4_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * 256;
+      if (i < nk) {
+        const int g = i / kv, j = i - g * kv;
+        x[u] = sk[g * pv + j];
+      } else if (i < n) {
+        const int iv = i - nk, g = iv / vv, j = iv - g * vv;
+        x[u] = sv[g * pv + j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * 256;
+      if (i < nk) {
+        const int g = i / kv, j = i - g * kv;
+        dk[g * pv + j] = x[u];
+      } else if (i < n) {
+        const int iv = i - nk, g = iv / vv, j = iv - g * vv;
+        dv[g * pv + j] = x[u];
+      }
+    }
+  }
 }
 
 // plan tunables (CS_ATTN_TARGET_WGS, CS_ATTN_MIN_ITEMS override; read once)
@@ -758,8 +788,9 @@ int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
     return fail(CS_ERR_INVALID, "cs_hist_gather: ld_hist and D must be positive multiples of 8");
   if (src_k == dst_k || src_vt == dst_vt)
     return fail(CS_ERR_INVALID, "cs_hist_gather: source and destination must differ (ping-pong)");
-  if (L * S * Hkv > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_hist_gather: grid too large");
-  hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S * Hkv)), dim3(256), 0,
+  if (L * S > 0x7fffffffLL || static_cast<int64_t>(Hkv) * ld_hist * D / 8 * 2 > 0x7fffffffLL)
+    return fail(CS_ERR_INVALID, "cs_hist_gather: grid too large");
+  hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), static_cast<const __bf16*>(src_k),
                      static_cast<__bf16*>(dst_k), static_cast<const __bf16*>(src_vt),
                      static_cast<__bf16*>(dst_vt), parent, hist_base, S, Hkv, ld_hist, D);
@@ -794,11 +825,9 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
   r.H = H;
   r.Hkv = Hkv;
   r.D = D;
-  if (D % 8 != 0) return fail(CS_ERR_INVALID, "cs_rope_place: head_dim must be a multiple of 8");
-  const int64_t total = r.n_tok * (D / 8);
-  const int64_t blocks = (total + 255) / 256;
-  if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many elements");
-  hipLaunchKernelGGL(rope_place_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+  if (D % 8 != 0 || D > 256) return fail(CS_ERR_INVALID, "cs_rope_place: head_dim must be a multiple of 8, <= 256");
+  if (r.n_tok > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many tokens");
+  hipLaunchKernelGGL(rope_place_kernel, dim3(static_cast<uint32_t>(r.n_tok)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), r);
   return check_launch("cs_rope_place");
 }

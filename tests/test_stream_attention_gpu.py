@@ -358,3 +358,25 @@ def test_gated_act_matches_torch(ops, dev, act):
     torch.cuda.synchronize()
     diff = (out.float() - ref.float()).abs()
     assert float(diff.max()) <= 2 ** -6 * float(ref.float().abs().max())
+
+
+@pytest.mark.parametrize("L,S,Hkv,ldh,D,hb", [(2, 5, 2, 32, 64, 7), (3, 16, 8, 64, 256, 33),
+                                             (1, 4, 8, 96, 128, 96), (2, 3, 1, 32, 64, 0)])
+def test_hist_gather_copies_filled_slots_of_the_parents(ops, dev, L, S, Hkv, ldh, D, hb):
+    """cs_hist_gather: dst[l][s] = src[l][parent[s]] for the filled slots (K rows j < hb,
+    V^T tiles up to ceil32(hb)); the rest of dst is left as it was."""
+    g = torch.Generator(device="cpu").manual_seed(L * 100 + S + hb)
+    bf = torch.bfloat16
+    sk = torch.randn(L, S, Hkv, ldh, D, generator=g).to(bf).to(dev)
+    sv = torch.randn(L, S, Hkv, ldh // 32, D, 32, generator=g).to(bf).to(dev)
+    dk = torch.full_like(sk, 7.0)
+    dv = torch.full_like(sv, 7.0)
+    parent = torch.randint(0, S, (S,), generator=g).to(dev)
+    ops.hist_gather(sk, dk, sv, dv, parent, torch.tensor([hb], dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    ek, ev = torch.full_like(sk, 7.0), torch.full_like(sv, 7.0)
+    if hb > 0:
+        ek[:, :, :, :hb] = sk[:, parent][:, :, :, :hb]
+        nt = (hb + 31) // 32
+        ev[:, :, :, :nt] = sv[:, parent][:, :, :, :nt]
+    assert torch.equal(dk, ek) and torch.equal(dv, ev)

@@ -18,6 +18,7 @@ import bench  # noqa: E402
 
 def main(name="c3", reps=100):
     R = importlib.import_module(bench.PKG_DIR + ".runtime")
+    R.use_gemm_tuning()
     mc = bench.METHOD_CONFIGS[name]
     dev = torch.device("cuda:0")
     eng, tok = R.random_engine(mc["preset"], dev, reuse_caches=0, tokenizer_dir=bench.BPE_FIXTURE)
