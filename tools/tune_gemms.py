@@ -31,6 +31,7 @@ def main() -> int:
     ap.add_argument("--legs", default="e2e,c1,c3,c5")
     ap.add_argument("--iters", default="10")
     ap.add_argument("--ms", default="20")
+    ap.add_argument("--rotating-mb", default="1024")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     # continue from the installed results (TunableOp reads its file at start and only tunes
@@ -38,11 +39,15 @@ def main() -> int:
     installed = os.path.join(REPO, PKG, "tuned", "gemm_mi355x.csv")
     first = os.path.splitext(args.out)[0] + "0.csv"
     if args.resume and os.path.exists(installed) and not os.path.exists(first):
+        # (--resume 0 re-measures every shape)
         shutil.copy(installed, first)
     env = dict(os.environ, PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="1",
                PYTORCH_TUNABLEOP_FILENAME=args.out, PYTORCH_TUNABLEOP_VERBOSE="1",
                PYTORCH_TUNABLEOP_MAX_TUNING_ITERATIONS=args.iters,
-               PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=args.ms)
+               PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=args.ms,
+               # rotate the operands through more memory than the 256 MB Infinity Cache, so
+               # each candidate is timed as the forward runs it: weights streamed from HBM
+               PYTORCH_TUNABLEOP_ROTATING_BUFFER_SIZE=args.rotating_mb)
     # one child per leg (each appends its new shapes to the same results file), a heartbeat
     # line every 30 s while a child tunes
     legs = [(m, ["--method", ""] if m == "e2e" else ["--e2e", "0", "--method", m])
