@@ -189,6 +189,11 @@ class BeamSearchGenerator(BaseGenerator):
         ref_user = BEAM["ref_user"].format(issue=issue, opinions_text=opinions_text(agent_opinions))
         ref_prefix = tok.render_raw(f"{BEAM['ref_system']}\n\n{ref_user}")
         all_prefixes = agent_prefixes + [ref_prefix]
+        # the agents' user prompts (text): the reference re-tokenizes prompt + statement +
+        # token on every call; candidates whose id-level append differs from that
+        # (tokenizers that are not merge-free) are scored on the text (_text_compat_patch)
+        self._agent_users = [BEAM["agent_user"].format(issue=issue, opinion=ops_all[a])
+                             for a in shard.local]
         bias = (runtime.bias_token_ids(tok, self.bias_against_tokens)
                 if self.use_token_biasing and self.bias_against_tokens else [])
         fused = (self.fused_decode and int(self.max_tokens) > 0 and int(self.beam_width) > 0
@@ -201,7 +206,8 @@ class BeamSearchGenerator(BaseGenerator):
         self.step_times = []
         self.step_log = []
         self.steps_run = 0
-        if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk:
+        merge_free = getattr(tok, "merge_free", True)
+        if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk and merge_free:
             self.decode_path = "fused-topk"
             st = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
                              max_steps=int(self.max_tokens))
@@ -222,6 +228,7 @@ class BeamSearchGenerator(BaseGenerator):
         """Per-step proposals on the host (sample / top-k / sharded), cs_beam_step scoring."""
         dev = engine.device
         beams: List[Tuple[str, List[float]]] = [("", [0.0] * A_loc)]
+        beam_ids: List[List[int]] = [[]]           # each beam's token ids as the streams hold them
         rewards = torch.zeros(A_loc, st.n_beams, dtype=torch.float32, device=dev)   # per beam
         completed: List[Tuple[str, List[float]]] = []
         for step in range(self.max_tokens):
@@ -275,15 +282,22 @@ class BeamSearchGenerator(BaseGenerator):
                     U = torch.empty(0, len(slots), dtype=torch.float32, device=dev)
                 W = parallel.combine_welfare(U, "min", shard)
                 order = ops.topk(W, len(slots))[0].cpu().tolist()
-            Uh = U.double().cpu().numpy()
             tstr = [tok.token_str(v) for v in ct]
+            if not getattr(tok, "merge_free", True):
+                U, W, order = self._text_compat_patch(engine, tok, U, W, order, rewards, cb, ct,
+                                                      tstr, beams, beam_ids, shard)
+            Uh = U.double().cpu().numpy()
             new_beams, new_idx = self._walk(order, lambda i: beams[cb[i]][0] + tstr[i],
                                             lambda i: tstr[i], lambda i: Uh[:, i].tolist(),
                                             completed)
+            par_t = torch.as_tensor(cb, dtype=torch.long, device=dev)
             self.step_log.append({"candidates": [(beams[b][0] + s) for b, s in zip(cb, tstr)],
                                   "min_rewards": W.double().cpu().tolist(),
+                                  # this rank's agents' log-prob of each candidate's token
+                                  "increments": (U - rewards[:, par_t]).double().cpu().tolist(),
                                   "kept": [s for s, _ in new_beams]})
             beams = new_beams
+            beam_ids = [beam_ids[cb[i]] + [ct[i]] for i in new_idx]
             if not beams:
                 break
             if step + 1 < self.max_tokens:
@@ -291,6 +305,44 @@ class BeamSearchGenerator(BaseGenerator):
                 keep = new_idx + [new_idx[0]] * (st.n_beams - len(new_idx))   # padded beams
                 rewards = U[:, torch.as_tensor(keep, device=dev)].contiguous()
         return completed, beams
+
+    def _text_compat_patch(self, engine, tok, U, W, order, rewards, cb, ct, tstr, beams,
+                           beam_ids, shard):
+        """Tokenizers that are not merge-free (BPE): the reference scores a candidate as the
+        last log-prob of the re-tokenized ``agent_user + statement + token``
+        (_get_agent_token_logprob, beam_search.py:335-404 via get_prompt_logprobs).  The
+        id-level score equals it only when that re-tokenization is the stream's ids plus the
+        candidate's id and the token strings spell the text; every other candidate (a merge
+        across the append, a byte fragment, a beam that already diverged) is scored on the
+        text in one batched pass, and the welfare and order are recomputed."""
+        from .. import utils
+        tail = BEAM["agent_user"].rsplit("\n\n", 1)[-1]
+        tail_ids = tok.encode(tail)
+        nt = len(tail_ids)
+        bad = []
+        for i, (b, v) in enumerate(zip(cb, ct)):
+            text = beams[b][0] + tstr[i]
+            ids = beam_ids[b] + [v]
+            api = text + utils.MARKER if text.endswith(("\n", " ")) else text
+            enc = tok.encode(tail + api)
+            if (enc[:nt] != tail_ids or enc[nt:nt + len(ids)] != ids
+                    or "".join(tok.tokens(ids)) != text):
+                bad.append(i)
+        if not bad:
+            return U, W, order
+        A_loc = U.shape[0]
+        users = [self._agent_users[a] + beams[cb[i]][0] + tstr[i] for a in range(A_loc) for i in bad]
+        lps = utils.text_compat_last(engine, tok, [BEAM["agent_system"]] * len(users), users)
+        dev = U.device
+        bi = torch.as_tensor(bad, dtype=torch.long, device=dev)
+        par = torch.as_tensor([cb[i] for i in bad], dtype=torch.long, device=dev)
+        lp = torch.as_tensor(lps, dtype=torch.float32, device=dev).view(A_loc, len(bad))
+        U = U.clone()
+        U[:, bi] = rewards[:, par] + lp
+        W = parallel.combine_welfare(U, "min", shard)
+        order = ops.topk(W, U.shape[1])[0].cpu().tolist()
+        self.text_compat_candidates = getattr(self, "text_compat_candidates", 0) + len(bad)
+        return U, W, order
 
     def _loop_fused_topk(self, engine, tok, st: DecodeState, A: int, bias):
         """Top-K proposer on one rank: after the host walk a decode step is ONE graph

@@ -180,12 +180,17 @@ def use_gemm_tuning(path: Optional[str] = None) -> Optional[str]:
         import tempfile
 
         import torch.cuda.tunable as tunable
-        tunable.enable(True)
-        tunable.tuning_enable(False)
-        tunable.record_untuned_enable(False)
-        # results are written back at exit to this file, never to the committed one
-        tunable.set_filename(os.path.join(tempfile.gettempdir(), f"cs_tunableop_{os.getpid()}.csv"))
-        if not tunable.read_file(path):
+        try:
+            tunable.enable(True)
+            tunable.tuning_enable(False)
+            tunable.record_untuned_enable(False)
+            # results are written back at exit to this file, never to the committed one
+            tunable.set_filename(os.path.join(tempfile.gettempdir(), f"cs_tunableop_{os.getpid()}.csv"))
+            ok = tunable.read_file(path)
+        except Exception as e:   # no usable device / TunableOp unavailable: library heuristic
+            logger.warning("GEMM tuning file %s not loaded: %s", path, e)
+            return None
+        if not ok:
             logger.warning("GEMM tuning file %s not usable here (versions differ?)", path)
             tunable.enable(False)
             return None
@@ -199,7 +204,6 @@ def get_engine(model_identifier: str) -> Tuple[ScoringEngine, CharTokenizer]:
             return _ENGINES[model_identifier]
         if not torch.cuda.is_available():
             raise ops.CSError("no HIP device: the scoring engine has no CPU path")
-        use_gemm_tuning()
         path = _model_dir(model_identifier)
         if path is not None:
             from .checkpoint import load_engine
@@ -219,6 +223,7 @@ def get_engine(model_identifier: str) -> Tuple[ScoringEngine, CharTokenizer]:
                 "*.safetensors, tokenizer.json) as the id, via runtime.register_model_dir or "
                 "under $CS_MODEL_ROOT, or use 'random:<preset>' for an architecture-exact "
                 "random-init benchmark model")
+        use_gemm_tuning()
         _ENGINES[model_identifier] = ent
         return ent
 

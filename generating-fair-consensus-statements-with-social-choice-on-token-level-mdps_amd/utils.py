@@ -225,6 +225,40 @@ def text_compat_span_sums(engine, tok, systems: Sequence[Optional[str]],
     return res
 
 
+@torch.no_grad()
+def text_compat_last(engine, tok, systems: Sequence[Optional[str]],
+                     users: Sequence[str], fallback: float = -10.0) -> List[float]:
+    """The LAST log-prob of the reference's user span, ``sum(get_prompt_logprobs(..)[1][-1:])``
+    (src/methods/beam_search.py:370-395), for many pairs in one batched prefill;
+    ``fallback`` where the reference's call gives nothing usable (empty span, None), as
+    its except branch does (:397-404)."""
+    n = len(users)
+    res = [float(fallback)] * n
+    idss, last = [], []
+    for s, u in zip(systems, users):
+        try:
+            api_user = u + MARKER if u.endswith(("\n", " ")) else u
+            ids, _ = tok.render_chat(s or None, api_user)
+            data = SimpleNamespace(tokens=tok.tokens(ids), token_logprobs=list(range(len(ids))))
+            _, keep = extract_user_prompt_logprobs(data, u)
+        except Exception as e:       # get_prompt_logprobs would return ([], [])
+            logger.error("get_prompt_logprobs failed: %s", e)
+            ids, keep = [], []
+        idss.append(list(ids))
+        last.append(keep[-1] if keep else -1)
+    todo = [j for j in range(n) if last[j] > 0]      # position 0 has no log-prob (None)
+    if not todo:
+        return res
+    dev = engine.device
+    cache = engine.prefill([idss[j][:last[j]] for j in todo])
+    rows = cache.last_hidden
+    tgt = torch.as_tensor([idss[j][last[j]] for j in todo], dtype=torch.int32, device=dev)
+    lp = engine.rows_logprobs(rows, tgt[:, None]).view(-1).double().cpu().tolist()
+    for j, v in zip(todo, lp):
+        res[j] = float(v)
+    return res
+
+
 def get_token_ids(model, text) -> Dict[str, int]:
     """{token string: id} of the chat-rendered single-message prompt (src/utils.py:466-525)."""
     try:

@@ -25,7 +25,7 @@ PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-md
 TOL = 1e-3
 
 
-TRACE_FILES = ["method_traces.json", "method_traces_gemma.json"]
+TRACE_FILES = ["method_traces.json", "method_traces_gemma.json", "method_traces_bpe.json"]
 # BASELINE C1 shape (Llama-3.2-1B widths and vocabulary, 2 layers; beam 4, BoN N = 8, FL
 # bf 3 / depth 2): replayed on the GPU (the CPU emulation of its 128,256-wide LM head
 # over ~700 reference scoring calls is too slow for the CPU suite)
@@ -90,6 +90,38 @@ def check_methods(traces):
         if stmt != run["statement"]:
             failures.append(f"{tag}: statement {stmt!r} != reference {run['statement']!r}")
     return failures
+
+
+def check_beam_increments(traces):
+    """Every beam candidate's per-agent log-prob increment (the product's U - R) against the
+    reference's own get_prompt_logprobs call for (agent prompt + statement + token): its
+    last log-prob (beam_search.py:386-395).  With a BPE tokenizer this pins the text path
+    for candidates whose re-tokenization differs from the id-level append."""
+    methods = importlib.import_module(PKG + ".methods")
+    prompts = importlib.import_module(PKG + ".methods.prompts")
+    failures, n_checked = [], 0
+    users = [prompts.BEAM["agent_user"].format(issue=traces["issue"], opinion=op)
+             for op in traces["agent_opinions"].values()]
+    for run in traces["runs"]:
+        if run["method"] != "beam_search":
+            continue
+        ref = {(c["system"], c["user"]): c["tail"][-1] for c in run["calls"] if c["tail"]}
+        gen = methods.get_method_generator("beam_search", dict(run["config"]), traces["model_id"])
+        gen.generate_statement(traces["issue"], dict(traces["agent_opinions"]))
+        for si, step in enumerate(gen.step_log):
+            inc = step.get("increments")
+            if inc is None:
+                continue
+            for i, cand in enumerate(step["candidates"]):
+                for a, u in enumerate(users):
+                    r = ref.get((prompts.BEAM["agent_system"], u + cand))
+                    if r is None:
+                        continue
+                    n_checked += 1
+                    if abs(inc[a][i] - r) > TOL:
+                        failures.append(f"beam step {si} candidate {cand[-16:]!r} agent {a}: "
+                                        f"{inc[a][i]:.5f} vs reference {r:.5f}")
+    return failures, n_checked
 
 
 def check_evaluations(traces):

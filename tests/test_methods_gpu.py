@@ -32,6 +32,12 @@ def test_methods_match_reference_traces(traces):
     assert not failures, "\n".join(failures)
 
 
+def test_beam_candidate_logprobs_match_reference_calls(traces):
+    failures, n = mp.check_beam_increments(traces)
+    assert n > 0 or not any(r["method"] == "beam_search" for r in traces["runs"])
+    assert not failures, "\n".join(failures[:20])
+
+
 def test_evaluator_matches_reference(traces):
     failures = mp.check_evaluations(traces)
     assert not failures, "\n".join(failures)

@@ -35,6 +35,12 @@ def test_methods_match_reference_traces(emulated):
     assert not failures, "\n".join(failures)
 
 
+def test_beam_candidate_logprobs_match_reference_calls(emulated):
+    failures, n = mp.check_beam_increments(emulated)
+    assert n > 0 or not any(r["method"] == "beam_search" for r in emulated["runs"])
+    assert not failures, "\n".join(failures[:20])
+
+
 def test_evaluator_matches_reference(emulated):
     failures = mp.check_evaluations(emulated)
     assert not failures, "\n".join(failures)
