@@ -166,6 +166,8 @@ def parse():
                          "0: kernel-only (the headline then reports the kernel leg, labelled)")
     ap.add_argument("--method", default="c1,c3,c5",
                     help="method-level beam_search decode configs ('' disables)")
+    ap.add_argument("--method-text-steps", type=int, default=4,
+                    help="steps of a short statement timed with the re-tokenized text semantics")
     ap.add_argument("--method-statements", type=int, default=1,
                     help="timed generate_statement calls per method config")
     ap.add_argument("--beam", default="c1,c3,c5",
@@ -435,8 +437,13 @@ def method_leg(name, args, world, rank, dev):
     model_id = "random:" + mc["preset"]
     R.register_engine(model_id, eng, tok)
     opinions = synthetic_opinions(mc["agents"])
+    # the timed statements score the appended token ids (retokenize "ids"); the BPE fixture
+    # gives the prompts their real token counts.  The reference's re-tokenized semantics
+    # ("text", the product default) are timed on a short statement below: with random-init
+    # weights most proposals are byte fragments that merge across the append, so the text
+    # path re-scores a far larger share of candidates than a trained model's would.
     gcfg = {"beam_width": mc["beam_width"], "max_tokens": mc["max_tokens"], "proposer": "topk",
-            "top_k": mc["top_k"], "seed": 1}
+            "top_k": mc["top_k"], "seed": 1, "retokenize": "ids"}
     warm = methods.get_method_generator("beam_search", dict(gcfg, max_tokens=4), model_id)
     warm.generate_statement(SCENARIO_ISSUE, opinions)
     runs = []
@@ -474,6 +481,22 @@ def method_leg(name, args, world, rank, dev):
     if graph_ms is not None:
         out["graph_step_ms"] = graph_ms
         out["host_overhead_frac"] = step_s * 1e3 / graph_ms - 1.0
+    if args.method_text_steps > 0:
+        gen = methods.get_method_generator(
+            "beam_search", dict(gcfg, retokenize="text", max_tokens=args.method_text_steps),
+            model_id)
+        _barrier_sync(world)
+        gen.generate_statement(SCENARIO_ISSUE, opinions)
+        _barrier_sync(world)
+        d = np.diff(np.asarray(gen.step_times))
+        ms = _max_over_ranks(float(np.median(d[1:] if d.size > 1 else d)) * 1e3, world, dev)
+        n_cand = sum(len(s_["candidates"]) for s_ in gen.step_log)
+        out["retokenize_text"] = {
+            "ms_per_step": ms, "steps": gen.steps_run, "decode_path": gen.decode_path,
+            "rescored_candidates": gen.text_compat_candidates, "candidates": n_cand,
+            "note": "the reference's re-tokenized last log-prob (product default): candidates "
+                    "whose BPE re-tokenization differs from the id append are re-scored on the "
+                    "text by a batched prefill; random-init proposals are mostly byte fragments"}
     del eng
     _free()
     return out
@@ -820,10 +843,36 @@ def read_traffic(path, config, rows, V):
     return None
 
 
+_LEG = ["start", time.time()]
+
+
+def _progress(name):
+    """Mark the start of a bench leg on stderr (the JSON line stays the only stdout line)."""
+    _LEG[0], _LEG[1] = name, time.time()
+    print(f"bench: leg {name}", file=sys.stderr, flush=True)
+
+
+def _heartbeat(period=45.0):
+    """A daemon thread that reports the running leg every `period` s on stderr, so a long
+    leg (a 70B model init, the first import on a fresh box) is visibly alive."""
+    import threading
+
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"bench: {time.time() - t0:.0f} s, leg {_LEG[0]} running for "
+                  f"{time.time() - _LEG[1]:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch(args))
+    _heartbeat()
     world, rank, local = init_dist(args)
     if args.selftest_launch:
         selftest_launch(world, rank, local)
@@ -845,6 +894,7 @@ def main():
             _free()
             return None
 
+    _progress("kernel_only")
     kern = c2_kernel_leg(args, world, rank, dev)
     _free()
     beam = {}
@@ -857,6 +907,7 @@ def main():
             print(f"bench: direct RCCL communicator unavailable ({e}); using the ProcessGroup",
                   file=sys.stderr, flush=True)
     for name in beams:
+        _progress("beam_kernel." + name)
         r = guarded("beam_kernel." + name, run_beam, name, world, rank, dev, args.beam_steps, 20,
                     comm, args.pmc_json)
         if r is not None:
@@ -864,15 +915,18 @@ def main():
     if comm is not None:
         comm.close()
     _free()
+    _progress("end_to_end")
     e2e = (guarded("end_to_end", c2_e2e_leg, args, world, rank, dev)
            if args.e2e and args.config == "c2" else None)
     method = {}
     for name in [m for m in args.method.split(",") if m]:
+        _progress("method_decode." + name)
         r = guarded("method_decode." + name, method_leg, name, args, world, rank, dev)
         if r is not None:
             method[name] = r
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        _progress("cpu_baseline")
         cpu = guarded("cpu_baseline", cpu_baseline, args.cpu_seconds)
 
     if rank == 0:

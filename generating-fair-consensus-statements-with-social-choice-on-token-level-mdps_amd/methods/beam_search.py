@@ -106,6 +106,15 @@ class BeamSearchGenerator(BaseGenerator):
         self.top_k = c.get("top_k", self.beam_width)
         self.fused_decode = c.get("fused_decode", True)
         self.fast_topk = c.get("fast_topk", True)
+        # how a candidate's log-prob is read with a tokenizer that is not merge-free (BPE):
+        # "text" (default) = the reference's re-tokenized prompt + statement + token, last
+        # log-prob (beam_search.py:358-390), candidates whose re-tokenization differs from
+        # the id append scored on the text; "ids" = the log-prob of the appended token id
+        # (standard token-level beam search; every step one captured graph)
+        self.retokenize = c.get("retokenize", "text")
+        if self.retokenize not in ("text", "ids"):
+            raise ValueError("retokenize must be 'text' or 'ids'")
+        self.text_compat_candidates = 0
         self.step_log: List[dict] = []
         self.decode_path = None
         self.steps_run = 0
@@ -206,7 +215,9 @@ class BeamSearchGenerator(BaseGenerator):
         self.step_times = []
         self.step_log = []
         self.steps_run = 0
-        merge_free = getattr(tok, "merge_free", True)
+        merge_free = getattr(tok, "merge_free", True) or self.retokenize == "ids"
+        self._merge_free = merge_free
+        self.text_compat_candidates = 0
         if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk and merge_free:
             self.decode_path = "fused-topk"
             st = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
@@ -283,7 +294,7 @@ class BeamSearchGenerator(BaseGenerator):
                 W = parallel.combine_welfare(U, "min", shard)
                 order = ops.topk(W, len(slots))[0].cpu().tolist()
             tstr = [tok.token_str(v) for v in ct]
-            if not getattr(tok, "merge_free", True):
+            if not self._merge_free:
                 U, W, order = self._text_compat_patch(engine, tok, U, W, order, rewards, cb, ct,
                                                       tstr, beams, beam_ids, shard)
             Uh = U.double().cpu().numpy()
@@ -341,7 +352,7 @@ class BeamSearchGenerator(BaseGenerator):
         U[:, bi] = rewards[:, par] + lp
         W = parallel.combine_welfare(U, "min", shard)
         order = ops.topk(W, U.shape[1])[0].cpu().tolist()
-        self.text_compat_candidates = getattr(self, "text_compat_candidates", 0) + len(bad)
+        self.text_compat_candidates += len(bad)
         return U, W, order
 
     def _loop_fused_topk(self, engine, tok, st: DecodeState, A: int, bias):

@@ -8,9 +8,9 @@ OUT="$R/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 STEP="${1:-all}"
-run_tests() { timeout -k 10 420 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/gpu_tests.log" 2>&1; }
+run_tests() { timeout -k 10 420 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread --capture=tee-sys ${PYTEST_ARGS:-} > "$OUT/gpu_tests.log" 2>&1; }
 run_smoke() { timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; }
-run_bench() { timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; }
+run_bench() { timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; }
 run_prof() {
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
      python3 "$R/bench.py" --cpu-seconds 0 > "$OUT/prof.log" 2>&1)

@@ -288,7 +288,11 @@ def test_beam_search_fast_topk_equals_host_loop(dev, family):
         gh = methods.get_method_generator("beam_search", dict(cfg, fast_topk=False), "test/fused-tiny")
         sh = gh.generate_statement("How should the city spend its budget?", ops_)
         assert gf.decode_path == "fused-topk" and gh.decode_path == "fused"
-        assert gf.step_log == gh.step_log
+        # the host loop also logs per-agent increments (the BPE log-prob check); compare the
+        # fields both paths record
+        common = ("candidates", "min_rewards", "kept")
+        assert ([{k: s[k] for k in common} for s in gf.step_log]
+                == [{k: s[k] for k in common} for s in gh.step_log])
         assert sf == sh
     finally:
         R.clear_engines()
