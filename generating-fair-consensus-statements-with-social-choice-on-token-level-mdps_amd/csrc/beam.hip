@@ -1,6 +1,4 @@
 // beam.hip — whole beam-search scoring / decode steps in one launch.
-#include <algorithm>
-
 #include "cs_kernels.cuh"
 
 namespace {
@@ -578,39 +576,6 @@ int decode_rows_first(int64_t row_blocks, int32_t block) {
   const int64_t slots = static_cast<int64_t>(n_cu) * (block >= 1024 ? 2 : 4);
   return row_blocks < slots ? 1 : 0;
 }
-// v2 grid plan.  Rows take blocks [0, n_items).  When they leave workgroup slots free
-// (C1: 256 row blocks of 256 threads; C3: 256 of 1024 threads on 512 slots) the proposer
-// runs on blocks of its own after them, as many as there are free slots, each taking
-// every n_pw-th chunk; when the rows fill the chip (C5: 512 row blocks) the first blocks
-// run one chunk each before their row.  CS_DECODE_P0 / CS_DECODE_PW override.
-int n_cus() {
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n_cu = v;
-    else
-      n_cu = 256;
-  }
-  return n_cu;
-}
-bool decode_v2() {
-  const char* e = getenv("CS_DECODE_V2");
-  return e && atoi(e) == 1;
-}
-void decode_v2_plan(int64_t n_items, int32_t n_prop, int32_t block, int32_t& p0, int32_t& n_pw) {
-  const int64_t slots = static_cast<int64_t>(n_cus()) * (block >= 1024 ? 2 : 4);
-  if (n_items < slots) {
-    p0 = static_cast<int32_t>(n_items);
-    n_pw = static_cast<int32_t>(std::min<int64_t>(n_prop, slots - n_items));
-  } else {
-    p0 = 0;
-    n_pw = static_cast<int32_t>(std::min<int64_t>(n_prop, n_items));
-  }
-  if (const char* e = getenv("CS_DECODE_P0")) p0 = std::max(0, atoi(e));
-  if (const char* e = getenv("CS_DECODE_PW")) n_pw = std::max(1, std::min(n_prop, atoi(e)));
-}
 #ifdef CS_TRACE_DECODE
 // slots: 0 first block start (min), 1 last proposer chunk start, 2 last proposer chunk
 // published, 3 last proposer merge done, 4 last row block start, 5 first row lse,
@@ -621,196 +586,6 @@ __device__ unsigned long long g_dec_ts[16];
 #define DEC_T(...)
 #endif
 constexpr int kBeamMaxBeams = 4096;
-
-// One proposer chunk of a decode step: the K best composite keys (value, ~id) of chunk
-// `chunk` of beam b's reference row (wave bound or radix select + rank counting, as
-// vocab_topk_chunk_kernel), handed off in ppart; the LAST chunk of the beam to finish
-// merges the chunk winners the same way and publishes the beam's K candidate ids (ids_ws,
-// out_ids, and sm_ids in LDS).  Returns true (block-uniform) in the merging block.
-template <int DT, bool CAP, int BLOCK, int KP>
-__device__ __forceinline__ bool propose_chunk(
-    int32_t b, int32_t chunk, const char* __restrict__ ref, int64_t ld_ref_bytes,
-    int32_t nchunk_p, int32_t ref_vec, int64_t vocab, int32_t K, float cap, float inv_cap,
-    unsigned long long* __restrict__ ppart, uint32_t* __restrict__ prop_cnt,
-    uint32_t* __restrict__ ids_ws, int32_t* __restrict__ out_ids, const BeamLds& L,
-    uint32_t* sm_ids, int& sm_last) {
-  const int tid = threadIdx.x;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(L.keys);  // 16 KB
-  unsigned long long* sel_cand = L.sel_cand;
-  uint32_t* sm_tw = L.sm_tw;
-  int* sm_res = L.sm_res;
-  uint32_t& sm_n = *L.sm_n;
-  DEC_T(if (tid == 0) atomicMax(&g_dec_ts[1], wall_clock64());)
-  constexpr int CH = KP * BLOCK;
-  const char* rp = ref + b * ld_ref_bytes;
-  const int64_t v0 = static_cast<int64_t>(chunk) * CH;
-  const int n = static_cast<int>(min(static_cast<int64_t>(CH), vocab - v0));
-  // 32-bit order keys in registers (the token id is implied by (j, lane)): half the
-  // registers of 64-bit composite keys, so the 1024-thread variant does not spill
-  uint32_t okey[KP];
-  constexpr int EPV = Elt<DT>::kPerVec;
-  const bool vec = KP % EPV == 0 && ref_vec && n == CH;
-  if (vec) {
-    // whole 16-byte-aligned chunk: KP / EPV non-temporal 16-byte loads per lane, all in
-    // flight at once (element (j / EPV * BLOCK + tid) * EPV + j % EPV in okey[j])
-    const u32x4* vp = reinterpret_cast<const u32x4*>(rp + v0 * Elt<DT>::kSize);
-    u32x4 q[KP / EPV > 0 ? KP / EPV : 1];
-#pragma unroll
-    for (int j = 0; j < KP / EPV; ++j) q[j] = __builtin_nontemporal_load(vp + j * BLOCK + tid);
-#pragma unroll
-    for (int j = 0; j < KP / EPV; ++j) {
-      float v[EPV];
-      unpack_vec<DT>(q[j], v);
-#pragma unroll
-      for (int e = 0; e < EPV; ++e)
-        okey[j * EPV + e] = order_key(CAP ? softcap_fn(v[e], cap, inv_cap) : v[e]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      const int i = tid + BLOCK * j;
-      float x = 0.0f;
-      if (i < n) x = load_one<DT>(rp, v0 + i);
-      okey[j] = order_key(CAP ? softcap_fn(x, cap, inv_cap) : x);
-    }
-  }
-  auto local = [&](int j) -> int {   // element of okey[j] within the chunk
-    return vec ? (j / EPV * BLOCK + tid) * EPV + j % EPV : tid + BLOCK * j;
-  };
-  auto key_of = [&](int j) -> unsigned long long {
-    return (static_cast<unsigned long long>(okey[j]) << 32) |
-           static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + local(j)));
-  };
-  if (tid == 0) sm_n = 0u;
-  DEC_T(if (tid == 0) atomicMax(&g_dec_ts[10], wall_clock64());)
-  bool have = false;   // candidates collected (block-uniform)
-  // (256-thread variants only: in the 1024-thread ones the extra code's registers slow
-  // the agent-row stream more than the bound saves; profiles/r01h_decode_wave_bound.jsonl)
-  if (CS_WB_ON(BLOCK, K)) {
-    uint32_t lm = 0u;
-#pragma unroll
-    for (int j = 0; j < KP; ++j)
-      if (local(j) < n) lm = max(lm, okey[j]);
-    const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      if (local(j) < n && okey[j] >= t) {
-        const uint32_t at = atomicAdd(&sm_n, 1u);
-        if (at < kTopkCand) sel_cand[at] = key_of(j);
-      }
-    }
-    __syncthreads();
-    have = sm_n <= static_cast<uint32_t>(kTopkCand);
-    if (!have) {   // massive ties at the bound: the radix path below
-      __syncthreads();
-      if (tid == 0) sm_n = 0u;
-    }
-  }
-  if (!have) {
-    const RadixCut cut = radix_select<BLOCK>(
-        [&](auto f) {
-#pragma unroll
-          for (int j = 0; j < KP; ++j)
-            if (local(j) < n) f(key_of(j));
-        },
-        static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      if (local(j) < n) {
-        const unsigned long long kj = key_of(j);
-        if ((kj >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = kj;
-      }
-    }
-    __syncthreads();
-  }
-  DEC_T(if (tid == 0) atomicMax(&g_dec_ts[11], wall_clock64());)
-  const int32_t nkeys = nchunk_p * K;
-  unsigned long long* pr = ppart + static_cast<int64_t>(b) * pad_line(nkeys, 8);
-  unsigned long long* out = pr + static_cast<int64_t>(chunk) * K;
-  const int nc = static_cast<int>(sm_n);
-  rank_candidates<BLOCK>(sel_cand, nc, K, [&](int r, unsigned long long kc) { st_sc1(out + r, kc); });
-  for (int r = nc + tid; r < K; r += BLOCK) st_sc1(out + r, 0ull);
-  wait_stores();
-  __syncthreads();
-  DEC_T(if (tid == 0) { const unsigned long long q = wall_clock64(); atomicMax(&g_dec_ts[2], q);
-                        atomicMin(&g_dec_ts[12], q); })
-  if (tid == 0) {
-    sm_last = arrive(&prop_cnt[b]) == static_cast<uint32_t>(nchunk_p - 1);
-    sm_n = 0u;
-  }
-  __syncthreads();
-  if (!sm_last) return false;  // block-uniform
-  if (tid == 0) st_sc1(prop_cnt + b, 0u);
-  // the beam's K best among the chunk winners -> its candidate ids.  The winners are
-  // read once (all loads in flight together) into registers when they fit, not again
-  // per radix level and for the collection.
-  constexpr int MR = 4;
-  unsigned long long mk[MR];
-  const bool cached = nkeys <= MR * BLOCK;
-  if (cached) {
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      const int i = tid + r * BLOCK;
-      mk[r] = i < nkeys ? ld_sc1(pr + i) : 0ull;
-    }
-  }
-  auto each_key = [&](auto f) {
-    if (cached) {
-#pragma unroll
-      for (int r = 0; r < MR; ++r)
-        if (mk[r]) f(mk[r]);
-    } else {
-      for (int i = tid; i < nkeys; i += BLOCK) {
-        const unsigned long long c = ld_sc1(pr + i);
-        if (c) f(c);
-      }
-    }
-  };
-  bool mhave = false;
-  if (CS_WB_ON(BLOCK, K) && cached) {
-    uint32_t lm = 0u;
-#pragma unroll
-    for (int r = 0; r < MR; ++r) lm = max(lm, static_cast<uint32_t>(mk[r] >> 32));
-    const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      if (mk[r] && static_cast<uint32_t>(mk[r] >> 32) >= t) {
-        const uint32_t at = atomicAdd(&sm_n, 1u);
-        if (at < kTopkCand) sel_cand[at] = mk[r];
-      }
-    }
-    __syncthreads();
-    mhave = sm_n <= static_cast<uint32_t>(kTopkCand);
-    if (!mhave) {
-      __syncthreads();
-      if (tid == 0) sm_n = 0u;
-    }
-  }
-  if (!mhave) {
-    const RadixCut mcut = radix_select<BLOCK>(
-        each_key, static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
-    each_key([&](unsigned long long c) {
-      if ((c >> mcut.shift) >= mcut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = c;
-    });
-    __syncthreads();
-  }
-  const int mc = static_cast<int>(sm_n);
-  // the ids also stay in LDS: when this block gathers the beam it reads them there
-  rank_candidates<BLOCK>(sel_cand, mc, K, [&](int r, unsigned long long c) {
-    const uint32_t id = 0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull);
-    st_sc1(ids_ws + b * pad_line(K, 4) + r, id);
-    sm_ids[r] = id;
-    out_ids[b * K + r] = static_cast<int32_t>(id);
-  });
-  for (int r = mc + tid; r < K; r += BLOCK) {
-    st_sc1(ids_ws + b * pad_line(K, 4) + r, 0xffffffffu);
-    sm_ids[r] = 0xffffffffu;
-    out_ids[b * K + r] = -1;
-  }
-  DEC_T(if (tid == 0) atomicMax(&g_dec_ts[3], wall_clock64());)
-  return true;
-}
-
 
 template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL, int KP>
 __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kernel(
@@ -846,6 +621,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   __shared__ int sm_res[2];
   __shared__ uint32_t sm_n;
   const BeamLds L{keys, keys2, sel_cand, sm_w, sm_ord, sm_tw, sm_res, &sm_n};
+  uint32_t* hist = reinterpret_cast<uint32_t*>(keys);  // 16 KB
   const int tid = threadIdx.x;
   const int32_t C = B * K;
   const int32_t n_prop = B * nchunk_p;
@@ -867,13 +643,178 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     // the proposer's short latency chain goes first when it shares a CU with a streaming
     // row block (instruction issue priority; the stream is bandwidth-bound, not issue-bound)
     __builtin_amdgcn_s_setprio(CS_PROP_PRIO);
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[1], q0);)
+    constexpr int CH = KP * BLOCK;
     const int32_t b = pblk / nchunk_p;
-    if (!propose_chunk<DT, CAP, BLOCK, KP>(b, pblk - b * nchunk_p, ref, ld_ref_bytes, nchunk_p,
-                                           ref_vec, vocab, K, cap, inv_cap, ppart, prop_cnt,
-                                           ids_ws, out_ids, L, reinterpret_cast<uint32_t*>(sm_ord),
-                                           sm_last))
-      return;  // block-uniform
+    const int32_t chunk = pblk - b * nchunk_p;
+    const char* rp = ref + b * ld_ref_bytes;
+    const int64_t v0 = static_cast<int64_t>(chunk) * CH;
+    const int n = static_cast<int>(min(static_cast<int64_t>(CH), vocab - v0));
+    // 32-bit order keys in registers (the token id is implied by (j, lane)): half the
+    // registers of 64-bit composite keys, so the 1024-thread variant does not spill
+    uint32_t okey[KP];
+    constexpr int EPV = Elt<DT>::kPerVec;
+    const bool vec = KP % EPV == 0 && ref_vec && n == CH;
+    if (vec) {
+      // whole 16-byte-aligned chunk: KP / EPV non-temporal 16-byte loads per lane, all in
+      // flight at once (element (j / EPV * BLOCK + tid) * EPV + j % EPV in okey[j])
+      const u32x4* vp = reinterpret_cast<const u32x4*>(rp + v0 * Elt<DT>::kSize);
+      u32x4 q[KP / EPV > 0 ? KP / EPV : 1];
+#pragma unroll
+      for (int j = 0; j < KP / EPV; ++j) q[j] = __builtin_nontemporal_load(vp + j * BLOCK + tid);
+#pragma unroll
+      for (int j = 0; j < KP / EPV; ++j) {
+        float v[EPV];
+        unpack_vec<DT>(q[j], v);
+#pragma unroll
+        for (int e = 0; e < EPV; ++e)
+          okey[j * EPV + e] = order_key(CAP ? softcap_fn(v[e], cap, inv_cap) : v[e]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        const int i = tid + BLOCK * j;
+        float x = 0.0f;
+        if (i < n) x = load_one<DT>(rp, v0 + i);
+        okey[j] = order_key(CAP ? softcap_fn(x, cap, inv_cap) : x);
+      }
+    }
+    auto local = [&](int j) -> int {   // element of okey[j] within the chunk
+      return vec ? (j / EPV * BLOCK + tid) * EPV + j % EPV : tid + BLOCK * j;
+    };
+    auto key_of = [&](int j) -> unsigned long long {
+      return (static_cast<unsigned long long>(okey[j]) << 32) |
+             static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + local(j)));
+    };
+    if (tid == 0) sm_n = 0u;
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[10], wall_clock64());)
+    bool have = false;   // candidates collected (block-uniform)
+    // (256-thread variants only: in the 1024-thread ones the extra code's registers slow
+    // the agent-row stream more than the bound saves; profiles/r01h_decode_wave_bound.jsonl)
+    if (CS_WB_ON(BLOCK, K)) {
+      uint32_t lm = 0u;
+#pragma unroll
+      for (int j = 0; j < KP; ++j)
+        if (local(j) < n) lm = max(lm, okey[j]);
+      const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        if (local(j) < n && okey[j] >= t) {
+          const uint32_t at = atomicAdd(&sm_n, 1u);
+          if (at < kTopkCand) sel_cand[at] = key_of(j);
+        }
+      }
+      __syncthreads();
+      have = sm_n <= static_cast<uint32_t>(kTopkCand);
+      if (!have) {   // massive ties at the bound: the radix path below
+        __syncthreads();
+        if (tid == 0) sm_n = 0u;
+      }
+    }
+    if (!have) {
+      const RadixCut cut = radix_select<BLOCK>(
+          [&](auto f) {
+#pragma unroll
+            for (int j = 0; j < KP; ++j)
+              if (local(j) < n) f(key_of(j));
+          },
+          static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        if (local(j) < n) {
+          const unsigned long long kj = key_of(j);
+          if ((kj >> cut.shift) >= cut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = kj;
+        }
+      }
+      __syncthreads();
+    }
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[11], wall_clock64());)
+    const int32_t nkeys = nchunk_p * K;
+    unsigned long long* pr = ppart + static_cast<int64_t>(b) * pad_line(nkeys, 8);
+    unsigned long long* out = pr + static_cast<int64_t>(chunk) * K;
+    const int nc = static_cast<int>(sm_n);
+    rank_candidates<BLOCK>(sel_cand, nc, K, [&](int r, unsigned long long kc) { st_sc1(out + r, kc); });
+    for (int r = nc + tid; r < K; r += BLOCK) st_sc1(out + r, 0ull);
+    wait_stores();
+    __syncthreads();
+    DEC_T(if (tid == 0) { const unsigned long long q = wall_clock64(); atomicMax(&g_dec_ts[2], q);
+                          atomicMin(&g_dec_ts[12], q); })
+    if (tid == 0) {
+      sm_last = arrive(&prop_cnt[b]) == static_cast<uint32_t>(nchunk_p - 1);
+      sm_n = 0u;
+    }
+    __syncthreads();
+    if (!sm_last) return;  // block-uniform
+    if (tid == 0) st_sc1(prop_cnt + b, 0u);
+    // the beam's K best among the chunk winners -> its candidate ids.  The winners are
+    // read once (all loads in flight together) into registers when they fit, not again
+    // per radix level and for the collection.
+    constexpr int MR = 4;
+    unsigned long long mk[MR];
+    const bool cached = nkeys <= MR * BLOCK;
+    if (cached) {
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        const int i = tid + r * BLOCK;
+        mk[r] = i < nkeys ? ld_sc1(pr + i) : 0ull;
+      }
+    }
+    auto each_key = [&](auto f) {
+      if (cached) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+          if (mk[r]) f(mk[r]);
+      } else {
+        for (int i = tid; i < nkeys; i += BLOCK) {
+          const unsigned long long c = ld_sc1(pr + i);
+          if (c) f(c);
+        }
+      }
+    };
+    bool mhave = false;
+    if (CS_WB_ON(BLOCK, K) && cached) {
+      uint32_t lm = 0u;
+#pragma unroll
+      for (int r = 0; r < MR; ++r) lm = max(lm, static_cast<uint32_t>(mk[r] >> 32));
+      const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        if (mk[r] && static_cast<uint32_t>(mk[r] >> 32) >= t) {
+          const uint32_t at = atomicAdd(&sm_n, 1u);
+          if (at < kTopkCand) sel_cand[at] = mk[r];
+        }
+      }
+      __syncthreads();
+      mhave = sm_n <= static_cast<uint32_t>(kTopkCand);
+      if (!mhave) {
+        __syncthreads();
+        if (tid == 0) sm_n = 0u;
+      }
+    }
+    if (!mhave) {
+      const RadixCut mcut = radix_select<BLOCK>(
+          each_key, static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+      each_key([&](unsigned long long c) {
+        if ((c >> mcut.shift) >= mcut.prefix) sel_cand[atomicAdd(&sm_n, 1u)] = c;
+      });
+      __syncthreads();
+    }
+    const int mc = static_cast<int>(sm_n);
+    // the ids also stay in LDS: when this block gathers the beam it reads them there
+    uint32_t* sm_ids = reinterpret_cast<uint32_t*>(sm_ord);
+    rank_candidates<BLOCK>(sel_cand, mc, K, [&](int r, unsigned long long c) {
+      const uint32_t id = 0xffffffffu - static_cast<uint32_t>(c & 0xffffffffull);
+      st_sc1(ids_ws + b * pad_line(K, 4) + r, id);
+      sm_ids[r] = id;
+      out_ids[b * K + r] = static_cast<int32_t>(id);
+    });
+    for (int r = mc + tid; r < K; r += BLOCK) {
+      st_sc1(ids_ws + b * pad_line(K, 4) + r, 0xffffffffu);
+      sm_ids[r] = 0xffffffffu;
+      out_ids[b * K + r] = -1;
+    }
     ids_in_lds = true;
+    DEC_T(if (tid == 0) atomicMax(&g_dec_ts[3], wall_clock64());)
     gb = b;
   } else {
     // ---- agent row stream ----
@@ -950,217 +891,6 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   __syncthreads();
   DEC_T(if (tid == 0) atomicMax(&g_dec_ts[7], wall_clock64());)
   if (tid == 0) sm_last = arrive(done_cnt) == static_cast<uint32_t>(B - 1);
-  __syncthreads();
-  if (!sm_last) return;  // block-uniform
-  if (tid == 0) st_sc1(done_cnt, 0u);
-  DEC_T(if (tid == 0) g_dec_ts[8] = wall_clock64();)
-  beam_tail<BLOCK>(L, Uw, wkey, W, A, C, kind, eps, n_order, n2, out_order, out_val, out_kept);
-  DEC_T(if (tid == 0) g_dec_ts[9] = wall_clock64();)
-}
-
-// U / welfare key of one candidate: agent a, beam b, slot j, token id t (row a * B + b).
-template <int DT, bool CAP>
-__device__ __forceinline__ void decode_gather_one(const char* __restrict__ logits, int64_t ld_bytes,
-                                                  int64_t vocab, int32_t a, int32_t b, int32_t B,
-                                                  int32_t K, int32_t j, int32_t t, float lse,
-                                                  const float* __restrict__ R, float cap,
-                                                  float inv_cap, bool order_free, bool is_min,
-                                                  uint32_t* Uw, uint32_t* wkey) {
-  const int64_t row = static_cast<int64_t>(a) * B + b;
-  float lp = __builtin_nanf("");
-  if (t >= 0 && t < vocab) {
-    float x = load_one<DT>(logits + row * ld_bytes, t);
-    if (CAP) x = softcap_fn(x, cap, inv_cap);
-    lp = x - lse;
-  }
-  const float u = R[row] + lp;
-  const int32_t c = b * K + j;
-  st_sc1(Uw + static_cast<int64_t>(a) * B * K + c, __float_as_uint(u));
-  if (order_free && __builtin_isfinite(u))
-    __hip_atomic_fetch_max(wkey + c, welfare_key(u, is_min), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint32_t claim(uint32_t* st, uint32_t bit) {
-  return __hip_atomic_fetch_or(st, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ---------------------------------------------------------------------------
-// beam decode step v2: proposer chunks on their own workgroups or ahead of a row, and
-// every agent row gathered by whichever side of (row lse, beam ids) comes second
-// ---------------------------------------------------------------------------
-// Grid: blocks [0, n_items) stream one (agent row, split) item each (rows first, so the
-// long streams start at once); blocks [p0, p0 + n_pw) run proposer chunks c = pw, pw +
-// n_pw, ... (before their row item, if they have one).  The hand-off per agent row is a
-// two-bit claim word rstate[row]: the row's finisher publishes its lse and sets bit 1, the
-// beam's proposer merge publishes the ids and sets bit 2 on each of the beam's rows; the
-// side whose fetch_or sees the other bit gathers that row's K candidates (U, welfare keys)
-// and clears the word.  Normally the proposer is done long before the rows, so every row
-// gathers its own K values right after its stream, in parallel, instead of one block per
-// beam gathering A x K values after the last row.  Each gathering block adds its row count
-// to done_cnt; the block that completes A * B runs beam_tail.  No block waits on another.
-// Same proposer selection, lse arithmetic and U formula as beam_decode_kernel.
-template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL, int KP>
-__global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode2_kernel(
-    const char* __restrict__ ref, int64_t ld_ref_bytes, int32_t nchunk_p, int32_t ref_vec,
-    int32_t p0, int32_t n_pw, const char* __restrict__ logits, int64_t vocab, int64_t ld_bytes,
-    int32_t nsplit, int64_t split_len, int32_t A, int32_t B, int32_t K,
-    const float* __restrict__ R, float cap, float inv_cap, int kind, double eps,
-    unsigned long long* __restrict__ part, unsigned long long* __restrict__ ppart,
-    uint32_t* __restrict__ row_cnt, uint32_t* __restrict__ prop_cnt,
-    uint32_t* __restrict__ rstate, uint32_t* __restrict__ done_cnt, uint32_t* __restrict__ wkey,
-    uint32_t* __restrict__ lse_ws, uint32_t* __restrict__ ids_ws, int32_t* __restrict__ out_ids,
-    float* __restrict__ U, float* __restrict__ W, int32_t n_order, int32_t n2,
-    int32_t* __restrict__ out_order, float* __restrict__ out_val, float* __restrict__ out_kept) {
-  __shared__ float sm_m[BLOCK / 64];
-  __shared__ float sm_s[BLOCK / 64];
-  __shared__ int sm_last;
-  __shared__ int sm_flag;
-  __shared__ float sm_lse;
-  constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
-  constexpr int kPoolTail = 2 * kFusedSort + kTopkCand + kFusedSort;  // u64 words
-  constexpr int kPool = TAB && kCapTab / 2 > kPoolTail ? kCapTab / 2 : kPoolTail;
-  __shared__ __attribute__((aligned(16))) unsigned long long pool[kPool];
-  unsigned long long* keys = pool;
-  unsigned long long* keys2 = keys + kFusedSort;
-  unsigned long long* sel_cand = pool + 2 * kFusedSort;
-  float* sm_w = reinterpret_cast<float*>(sel_cand + kTopkCand);
-  int32_t* sm_ord = reinterpret_cast<int32_t*>(sm_w + kFusedSort);
-  float* ctab = reinterpret_cast<float*>(pool);
-  __shared__ uint32_t sm_tw[2 * BLOCK / 64];
-  __shared__ int sm_res[2];
-  __shared__ uint32_t sm_n;
-  const BeamLds L{keys, keys2, sel_cand, sm_w, sm_ord, sm_tw, sm_res, &sm_n};
-  const int tid = threadIdx.x;
-  const int32_t rows = A * B;
-  const int32_t C = B * K;
-  const int32_t n_prop = B * nchunk_p;
-  const int64_t n_items = static_cast<int64_t>(rows) * nsplit;
-  const bool is_min = kind == CS_WELFARE_MIN;
-  const bool order_free = kind == CS_WELFARE_MIN || kind == CS_WELFARE_MAX;
-  uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
-  DEC_T(const unsigned long long q0 = wall_clock64(); if (tid == 0) atomicMin(&g_dec_ts[0], q0);)
-  int32_t gathered = 0;   // agent rows this block gathered (block-uniform)
-
-  // ---- proposer chunks ----
-  const int32_t pw = static_cast<int32_t>(blockIdx.x) - p0;
-  if (pw >= 0 && pw < n_pw) {
-    __builtin_amdgcn_s_setprio(CS_PROP_PRIO);
-    uint32_t* sm_ids = reinterpret_cast<uint32_t*>(sm_ord);
-    int32_t* list = reinterpret_cast<int32_t*>(keys);   // the merge's histogram is done
-    for (int32_t c = pw; c < n_prop; c += n_pw) {
-      const int32_t b = c / nchunk_p;
-      if (propose_chunk<DT, CAP, BLOCK, KP>(b, c - b * nchunk_p, ref, ld_ref_bytes, nchunk_p,
-                                            ref_vec, vocab, K, cap, inv_cap, ppart, prop_cnt,
-                                            ids_ws, out_ids, L, sm_ids, sm_last)) {
-        // ids published (sc1 stores): claim the beam's rows; gather those whose lse is out
-        wait_stores();
-        for (int32_t a0 = 0; a0 < A; a0 += BLOCK) {
-          __syncthreads();
-          if (tid == 0) sm_n = 0u;
-          __syncthreads();
-          const int32_t a = a0 + tid;
-          if (a < A) {
-            uint32_t* st = rstate + static_cast<int64_t>(a) * B + b;
-            if (claim(st, 2u) & 1u) {
-              list[atomicAdd(&sm_n, 1u)] = a;
-              st_sc1(st, 0u);
-            }
-          }
-          __syncthreads();
-          const int32_t np = static_cast<int32_t>(sm_n);
-          for (int32_t i = tid; i < np * K; i += BLOCK) {
-            const int32_t ag = list[i / K];
-            const int32_t j = i - (i / K) * K;
-            const float lse = __uint_as_float(ld_sc1(lse_ws + b * pad_line(A, 4) + ag));
-            decode_gather_one<DT, CAP>(logits, ld_bytes, vocab, ag, b, B, K, j,
-                                       static_cast<int32_t>(sm_ids[j]), lse, R, cap, inv_cap,
-                                       order_free, is_min, Uw, wkey);
-          }
-          gathered += np;
-        }
-      }
-      __syncthreads();
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-
-  // ---- agent row item ----
-  if (static_cast<int64_t>(blockIdx.x) < n_items) {
-    const int64_t item = blockIdx.x;
-    const int32_t row = static_cast<int32_t>(item / nsplit);
-    const int32_t split = static_cast<int32_t>(item - static_cast<int64_t>(row) * nsplit);
-    const char* rp = logits + row * ld_bytes;
-    const int64_t v0 = static_cast<int64_t>(split) * split_len;
-    const int64_t v1 = min(vocab, v0 + split_len);
-    if constexpr (TAB) {
-      build_cap_table<BLOCK>(ctab, cap, inv_cap);
-      __syncthreads();
-    }
-    const float2 ms = block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(
-        rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s, ctab);
-    bool fin = true;   // this block finishes the row (block-uniform)
-    if (nsplit > 1) {
-      if (tid == 0) {
-        st_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + split,
-               (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
-                   __float_as_uint(ms.x));
-        wait_stores();
-        sm_last = arrive(&row_cnt[row]) == static_cast<uint32_t>(nsplit - 1);
-      }
-      __syncthreads();
-      fin = sm_last;
-      if (fin && tid < 64) {
-        float m = -INFINITY, sum = 0.0f;
-        for (int j = tid; j < nsplit; j += 64) {
-          const unsigned long long pv = ld_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + j);
-          lse_merge(m, sum, __uint_as_float(static_cast<uint32_t>(pv)),
-                    __uint_as_float(static_cast<uint32_t>(pv >> 32)));
-        }
-        wave_lse_reduce(m, sum);
-        if (tid == 0) {
-          sm_lse = m + logf(sum);
-          st_sc1(row_cnt + row, 0u);
-        }
-      }
-    } else if (tid == 0) {
-      sm_lse = ms.x + logf(ms.y);
-    }
-    if (fin) {
-      const int32_t b = row % B;
-      const int32_t a = row / B;
-      if (tid == 0) {
-        st_sc1(lse_ws + b * pad_line(A, 4) + a, __float_as_uint(sm_lse));
-        wait_stores();
-        uint32_t* st = rstate + row;
-        const uint32_t s = claim(st, 1u);
-        sm_flag = (s & 2u) ? 1 : 0;
-        if (s & 2u) st_sc1(st, 0u);
-      }
-      __syncthreads();
-      DEC_T(if (tid == 0) { const unsigned long long q = wall_clock64(); atomicMin(&g_dec_ts[5], q);
-                            atomicMax(&g_dec_ts[6], q); })
-      if (sm_flag) {   // the ids are out: gather this row's K candidates now
-        const float lse = sm_lse;
-        for (int32_t j = tid; j < K; j += BLOCK)
-          decode_gather_one<DT, CAP>(logits, ld_bytes, vocab, a, b, B, K, j,
-                                     static_cast<int32_t>(ld_sc1(ids_ws + b * pad_line(K, 4) + j)),
-                                     lse, R, cap, inv_cap, order_free, is_min, Uw, wkey);
-        gathered += 1;
-      }
-    }
-  }
-
-  // ---- arrival; the block that completes every row runs the tail ----
-  if (gathered == 0) return;  // block-uniform
-  wait_stores();
-  __syncthreads();
-  DEC_T(if (tid == 0) atomicMax(&g_dec_ts[7], wall_clock64());)
-  if (tid == 0)
-    sm_last = __hip_atomic_fetch_add(done_cnt, static_cast<uint32_t>(gathered), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT) +
-                  static_cast<uint32_t>(gathered) ==
-              static_cast<uint32_t>(rows);
   __syncthreads();
   if (!sm_last) return;  // block-uniform
   if (tid == 0) st_sc1(done_cnt, 0u);
@@ -1315,13 +1045,13 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
 
 namespace {
 // cs_beam_decode_step workspace: [cs_beam_step counters | proposer counters | beam
-// counters | row claim words][row lse][beam ids][proposer chunk winners][split partials]
+// counters][row lse][proposer chunk winners][split partials]
 struct DecodeLayout {
   SplitPlan plan;
   int32_t block;
   int32_t kp;
   int32_t nchunk_p;
-  size_t lse_off, ids_off, ppart_off, part_off, rstate_off, total;
+  size_t lse_off, ids_off, ppart_off, part_off, total;
 };
 DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int dtype) {
   DecodeLayout d;
@@ -1331,10 +1061,7 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   d.kp = decode_kp(B, vocab, d.block, K);
   const int64_t ch = static_cast<int64_t>(d.kp) * d.block;
   d.nchunk_p = static_cast<int32_t>((vocab + ch - 1) / ch);
-  // counters at fixed offsets (every launch leaves them zero, whatever the shape): the
-  // cs_beam_step ones, proposer and beam arrivals, the per-row claim words of v2
-  d.rstate_off = kBeamCounterBytes + 2 * sizeof(uint32_t) * kBeamMaxBeams;
-  d.lse_off = d.rstate_off + sizeof(uint32_t) * kBeamMaxRows;
+  d.lse_off = kBeamCounterBytes + 2 * sizeof(uint32_t) * kBeamMaxBeams;
   d.ids_off = d.lse_off + sizeof(uint32_t) * static_cast<size_t>(B) * pad_line(A, 4);
   d.ppart_off = d.ids_off + sizeof(uint32_t) * static_cast<size_t>(B) * pad_line(K, 4);
   d.part_off = d.ppart_off + sizeof(unsigned long long) * static_cast<size_t>(B) *
@@ -1400,17 +1127,7 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
     return fail(CS_ERR_WORKSPACE, std::string(w) + "workspace smaller than cs_beam_decode_workspace_size()");
   if (reinterpret_cast<uintptr_t>(workspace) % 8 != 0)
     return fail(CS_ERR_WORKSPACE, std::string(w) + "workspace not 8-byte aligned");
-  // v2 (CS_DECODE_V2=1): rows first, proposer chunks on the free workgroup slots (or
-  // ahead of the first rows when the rows fill the chip), rows gathered by whichever side
-  // of the (lse, ids) hand-off comes second.  Default: the round-1 grid (faster so far:
-  // profiles/r02c_decode_v2_ab.jsonl).
-  const bool v2 = decode_v2();
-  const int64_t n_items = rows * d.plan.nsplit;
-  const int32_t n_prop = B * d.nchunk_p;
-  int32_t p0 = 0, n_pw = n_prop;
-  if (v2) decode_v2_plan(n_items, n_prop, d.block, p0, n_pw);
-  const int64_t grid = v2 ? std::max<int64_t>(n_items, static_cast<int64_t>(p0) + n_pw)
-                          : static_cast<int64_t>(n_prop) + n_items;
+  const int64_t grid = static_cast<int64_t>(B) * d.nchunk_p + rows * d.plan.nsplit;
   if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, std::string(w) + "grid too large");
   char* wsb = static_cast<char*>(workspace);
   auto* done_cnt = reinterpret_cast<uint32_t*>(wsb);
@@ -1422,7 +1139,6 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
   auto* ids_ws = reinterpret_cast<uint32_t*>(wsb + d.ids_off);
   auto* ppart = reinterpret_cast<unsigned long long*>(wsb + d.ppart_off);
   auto* part = reinterpret_cast<unsigned long long*>(wsb + d.part_off);
-  auto* rstate = reinterpret_cast<uint32_t*>(wsb + d.rstate_off);
   const int64_t esz = elt_size(dtype);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool cap = softcap > 0.0f;
@@ -1437,22 +1153,12 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
   const int32_t ref_vec = (reinterpret_cast<uintptr_t>(ref_logits) % 16 == 0 &&
                            (ld_ref * esz) % 16 == 0) ? 1 : 0;
 #define CS_DECODE_GO(DTV, CAPV, FIXV, BL, UN, KPV)                                                 \
-  do {                                                                                             \
-    if (v2)                                                                                        \
-      hipLaunchKernelGGL((beam_decode2_kernel<DTV, CAPV, FIXV, BL, UN, KPV>), dim3(grid),          \
-                         dim3(BL), 0, st, rg, ld_ref * esz, d.nchunk_p, ref_vec, p0, n_pw, lg,     \
-                         vocab, ld * esz, d.plan.nsplit, d.plan.split_len, A, B, K, rewards_in,    \
-                         softcap, inv_cap, welfare_kind, static_cast<double>(eps), part, ppart,    \
-                         row_cnt, prop_cnt, rstate, done_cnt, wkey, lse_ws, ids_ws, out_ids,       \
-                         out_U, out_W, n_order, n2, out_order, out_order_val, out_kept);           \
-    else                                                                                           \
-      hipLaunchKernelGGL((beam_decode_kernel<DTV, CAPV, FIXV, BL, UN, KPV>), dim3(grid),           \
-                         dim3(BL), 0, st, rg, ld_ref * esz, d.nchunk_p, rows_first, ref_vec, lg,   \
-                         vocab, ld * esz, d.plan.nsplit, d.plan.split_len, A, B, K, rewards_in,    \
-                         softcap, inv_cap, welfare_kind, static_cast<double>(eps), part, ppart,    \
-                         row_cnt, prop_cnt, beam_cnt, done_cnt, wkey, lse_ws, ids_ws, out_ids,     \
-                         out_U, out_W, n_order, n2, out_order, out_order_val, out_kept);           \
-  } while (0)
+  hipLaunchKernelGGL((beam_decode_kernel<DTV, CAPV, FIXV, BL, UN, KPV>), dim3(grid), dim3(BL), 0,  \
+                     st, rg, ld_ref * esz, d.nchunk_p, rows_first, ref_vec, lg, vocab, ld * esz,   \
+                     d.plan.nsplit, d.plan.split_len, A, B, K, rewards_in, softcap, inv_cap,       \
+                     welfare_kind, static_cast<double>(eps), part, ppart, row_cnt, prop_cnt,       \
+                     beam_cnt, done_cnt, wkey, lse_ws, ids_ws, out_ids, out_U, out_W, n_order, n2, \
+                     out_order, out_order_val, out_kept)
 #define CS_DECODE_LAUNCH(DTV, CAPV, FIXV)                                                          \
   do {                                                                                             \
     if (d.block == 256) {                                                                          \
