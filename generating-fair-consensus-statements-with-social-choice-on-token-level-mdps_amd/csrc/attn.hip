@@ -376,6 +376,225 @@ void prefix_attn_kernel(AttnParams a) {
   }
 }
 
+// Scoring chunks and prompt prefill (no plan, T > 1, >= 1024 cells): the workgroup's four
+// 16-row query tiles walk ONE key-block list — the agent's prefix blocks, then the history
+// blocks of every stream the 64 rows touch, up to the furthest query's causal limit — and
+// each 32-key block is staged through LDS once per workgroup (K rows padded to D + 8, V^T
+// rows to 40 keys: conflict-free fragment reads), double-buffered: the next block's 16-byte
+// global loads are in flight while the current one is attended from LDS.  The per-wave
+// kernel above loads every block once per tile (4x the L2 traffic for 64 rows of one
+// stream).  Blocks outside a tile's own stream or causal range are masked per lane, as
+// there; the arithmetic of a block is attend_block's, so the result matches the per-wave
+// kernel up to the order of the key blocks within a split (one split here).
+template <int D>
+struct LdsTile {
+  static constexpr int KROW = D + 8;                 // bf16 per staged K row
+  static constexpr int VROW = 40;                    // bf16 per staged V^T row (32 keys + pad)
+  static constexpr int KELEMS = kKeyBlock * KROW;
+  static constexpr int VELEMS = D * VROW;
+  static constexpr int ELEMS = KELEMS + VELEMS;      // one buffer
+  static constexpr int NCH = D / 64;                 // 16-byte chunks per thread per operand
+};
+
+template <int D>
+__global__ __launch_bounds__(kAttnThreads, D <= 128 ? 2 : 1)
+void prefix_attn_lds_kernel(AttnParams a) {
+  using LT = LdsTile<D>;
+  constexpr int NDS = D / 32;
+  constexpr int NDT = D / 16;
+  constexpr int LDSW = D + 2;
+  constexpr int kBufBytes = 2 * LT::ELEMS * 2;
+  constexpr int kCombBytes = 3 * 16 * LDSW * 4;
+  __shared__ __attribute__((aligned(16))) char lds[kBufBytes > kCombBytes ? kBufBytes : kCombBytes];
+  __bf16* buf = reinterpret_cast<__bf16*>(lds);
+  auto sm = reinterpret_cast<float (*)[16][LDSW]>(lds);   // the wave combine, after the loop
+
+  const int bid = logical_block(a.swizzle);
+  const int qg = bid % a.n_qg, pg = bid / a.n_qg;
+  const int gi = pg / a.Hkv, g = pg % a.Hkv;
+  const int p = a.gpfx ? a.gpfx[gi] : gi;
+  const int M = a.n_str * a.T * a.rep;
+  const int r0 = qg * kGroupRows;
+  const int nrows = min(kGroupRows, M - r0);
+  const int n_qt = (nrows + 15) >> 4;
+  const int kw = n_qt == 1 ? 4 : (n_qt == 2 ? 2 : 1);
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
+  const int qt = w % n_qt, ks = w / n_qt;
+  const bool active = ks < kw;
+  const int col = lane & 15, h4 = lane >> 4;
+
+  const int row = r0 + qt * 16 + col;
+  const bool vrow = active && row < M;
+  const int rr = row < M ? row : M - 1;
+  const int jh = rr % a.rep, bt = rr / a.rep;
+  const int t = bt % a.T, b = bt / a.T;
+  const int64_t tok = (static_cast<int64_t>(gi) * a.n_str + b) * a.T + t;
+  const int head = g * a.rep + jh;
+  const int hb = *a.hist_base;
+  const int pl = a.plen[p];
+  const int64_t po = a.poff[p];
+  const int hv = min(hb + t + 1, static_cast<int>(a.ldh));
+  const int kmin_pos = a.window > 0 ? pl + hb + t - a.window + 1 : INT32_MIN;
+
+  // the workgroup's key blocks (uniform): prefix, then nbh history blocks per stream b_lo..b_hi
+  const int rw1 = r0 + nrows - 1;
+  const int b_lo = (r0 / a.rep) / a.T, b_hi = (rw1 / a.rep) / a.T;
+  const int t_hi = b_lo == b_hi ? (rw1 / a.rep) % a.T : a.T - 1;
+  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
+  const int nbp = (pl + kKeyBlock - 1) / kKeyBlock;
+  const int n_items = nbp + (b_hi - b_lo + 1) * nbh;
+
+  // item it: global K rows / V^T tile of 32 keys (contiguous) and this lane's mask data
+  auto item_src = [&](int it, const __bf16*& ks_, const __bf16*& vs_) {
+    if (it < nbp) {
+      const int64_t k0 = static_cast<int64_t>(g) * a.ldp + po + it * kKeyBlock;
+      ks_ = a.kp + k0 * D;
+      vs_ = a.vtp + k0 * D;
+    } else {
+      const int ih = it - nbp;
+      const int bb = b_lo + ih / nbh;
+      const int64_t sh = (static_cast<int64_t>(gi) * a.n_str + bb) * a.Hkv + g;
+      const int64_t k0 = sh * a.ldh + (ih % nbh) * kKeyBlock;
+      ks_ = a.kh + k0 * D;
+      vs_ = a.vth + k0 * D;
+    }
+  };
+  auto item_mask = [&](int it) {
+    ItemRef r;
+    r.k = nullptr;
+    r.v = nullptr;
+    if (it < nbp) {
+      r.kb = it * kKeyBlock;
+      r.lim = vrow ? pl : 0;
+      r.pos0 = 0;
+    } else {
+      const int ih = it - nbp;
+      const int bb = b_lo + ih / nbh;
+      r.kb = (ih % nbh) * kKeyBlock;
+      r.lim = (vrow && bb == b) ? hv : 0;
+      r.pos0 = pl;
+    }
+    return r;
+  };
+  // staging: thread tid copies 16-byte chunks c = tid + 256 j of K (row c / (D/8)) and of
+  // V^T (d row c / 4, keys 8 (c % 4) ..)
+  u32x4 rk[LT::NCH], rv[LT::NCH];
+  auto fetch = [&](int it) {
+    const __bf16 *ksrc, *vsrc;
+    item_src(it, ksrc, vsrc);
+#pragma unroll
+    for (int j = 0; j < LT::NCH; ++j) {
+      const int c = tid + kAttnThreads * j;
+      rk[j] = *reinterpret_cast<const u32x4*>(ksrc + c * 8);
+      rv[j] = *reinterpret_cast<const u32x4*>(vsrc + c * 8);
+    }
+  };
+  auto stage = [&](int sbuf) {
+    __bf16* kd = buf + sbuf * LT::ELEMS;
+    __bf16* vd = kd + LT::KELEMS;
+#pragma unroll
+    for (int j = 0; j < LT::NCH; ++j) {
+      const int c = tid + kAttnThreads * j;
+      *reinterpret_cast<u32x4*>(kd + (c / (D / 8)) * LT::KROW + (c % (D / 8)) * 8) = rk[j];
+      *reinterpret_cast<u32x4*>(vd + (c >> 2) * LT::VROW + (c & 3) * 8) = rv[j];
+    }
+  };
+
+  bf16x8 qf[NDS];
+  {
+    const __bf16* qrow = a.q + (tok * a.H + head) * D + 8 * h4;
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds) {
+      if (vrow) {
+        qf[ds] = *reinterpret_cast<const bf16x8*>(qrow + ds * 32);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[ds][e] = static_cast<__bf16>(0.0f);
+      }
+    }
+  }
+  f32x4 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.0f;
+
+  if (n_items > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < n_items; ++it) {
+    const bool more = it + 1 < n_items;
+    if (more) fetch(it + 1);
+    if (active && (it % kw) == ks) {
+      const __bf16* kd = buf + (it & 1) * LT::ELEMS;
+      const __bf16* vd = kd + LT::KELEMS;
+      KeyBlock<D> f;
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) {
+        f.k0[ds] = *reinterpret_cast<const bf16x8*>(kd + col * LT::KROW + ds * 32 + 8 * h4);
+        f.k1[ds] = *reinterpret_cast<const bf16x8*>(kd + (16 + col) * LT::KROW + ds * 32 + 8 * h4);
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        f.vlo[dt] = *reinterpret_cast<const bf16x4*>(vd + (dt * 16 + col) * LT::VROW + 4 * h4);
+        f.vhi[dt] = *reinterpret_cast<const bf16x4*>(vd + (dt * 16 + col) * LT::VROW + 16 + 4 * h4);
+      }
+      attend_block<D>(a, f, item_mask(it), qf, kmin_pos, h4, o, m, l);
+    }
+    if (more) stage((it + 1) & 1);   // buffer (it + 1) & 1 was last read in iteration it - 1
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  // waves that share a query tile combine through LDS (fixed order: ks = 0, 1, ...)
+  if (kw > 1) {
+    if (active && ks > 0) {
+      const int sl = w - n_qt;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm[sl][col][dt * 16 + 4 * h4 + i] = o[dt][i];
+      if (h4 == 0) {
+        sm[sl][col][D] = m;
+        sm[sl][col][D + 1] = l;
+      }
+    }
+    __syncthreads();
+    if (active && ks == 0) {
+      float mt = m;
+      for (int k = 1; k < kw; ++k) mt = fmaxf(mt, sm[qt + n_qt * k - n_qt][col][D]);
+      const float c0 = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m - mt);
+      l *= c0;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] *= c0;
+      for (int k = 1; k < kw; ++k) {
+        const int sl = qt + n_qt * k - n_qt;
+        const float mk = sm[sl][col][D];
+        const float ck = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mk - mt);
+        l = fmaf(sm[sl][col][D + 1], ck, l);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[dt][i] = fmaf(sm[sl][col][dt * 16 + 4 * h4 + i], ck, o[dt][i]);
+      }
+      m = mt;
+    }
+  }
+  if (!vrow || ks != 0) return;
+  const float inv = l > 0.0f ? 1.0f / l : 0.0f;
+  __bf16* orow = a.out + (tok * a.H + head) * D + 4 * h4;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    bf16x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = static_cast<__bf16>(o[dt][i] * inv);
+    *reinterpret_cast<bf16x4*>(orow + dt * 16) = v;
+  }
+}
+
 // One workgroup per merge entry (kMergeRows rows of a split (group, head, query group)),
 // each wave two rows, one per 32-lane half: the half's lanes fold the splits' (m, l) into
 // per-split weights, then the wave sums the weighted partial outputs (f32x4 columns).
@@ -572,6 +791,11 @@ int attn_target_wgs() {
   static const int v = env_int("CS_ATTN_TARGET_WGS", kTargetWgsDefault, 1, 1 << 20);
   return v;
 }
+// scoring chunks / prompt prefill on the LDS-staged kernel (CS_ATTN_LDS=0: the per-wave one)
+bool attn_lds() {
+  const char* e = getenv("CS_ATTN_LDS");
+  return !(e && atoi(e) == 0);
+}
 int attn_min_items() {
   static const int v = env_int("CS_ATTN_MIN_ITEMS", kMinItemsDefault, 1, 4096);
   return v;
@@ -761,6 +985,8 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   do {                                                                                  \
     if (plan)                                                                           \
       hipLaunchKernelGGL((prefix_attn_kernel<DV, true>), grid, dim3(kAttnThreads), 0, st, a); \
+    else if (attn_lds())                                                                \
+      hipLaunchKernelGGL(prefix_attn_lds_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a); \
     else                                                                                \
       hipLaunchKernelGGL((prefix_attn_kernel<DV, false>), grid, dim3(kAttnThreads), 0, st, a); \
     if (plan)                                                                           \
