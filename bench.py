@@ -482,6 +482,10 @@ def method_leg(name, args, world, rank, dev):
         out["graph_step_ms"] = graph_ms
         out["host_overhead_frac"] = step_s * 1e3 / graph_ms - 1.0
     if args.method_text_steps > 0:
+        # the engine's prefix reuse as the product ships it (reuse_caches 4): a step's
+        # re-tokenized texts extend the previous step's rows (agent prompt + statement)
+        eng.reuse_caches = 4
+        eng.reset_prefix_store()
         gen = methods.get_method_generator(
             "beam_search", dict(gcfg, retokenize="text", max_tokens=args.method_text_steps),
             model_id)
@@ -494,6 +498,7 @@ def method_leg(name, args, world, rank, dev):
         out["retokenize_text"] = {
             "ms_per_step": ms, "steps": gen.steps_run, "decode_path": gen.decode_path,
             "rescored_candidates": gen.text_compat_candidates, "candidates": n_cand,
+            "prefix_reuse": dict(eng.reuse_stats),
             "note": "the reference's re-tokenized last log-prob (product default): candidates "
                     "whose BPE re-tokenization differs from the id append are re-scored on the "
                     "text by a batched prefill; random-init proposals are mostly byte fragments"}
@@ -539,7 +544,9 @@ def _graph_step_ms(eng, tok, opinions, mc, dev, reps=20):
     for _ in range(reps):
         st.advance(par, [5] * B, post=post)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) * 1e3 / reps
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    st.release()
+    return ms
 
 
 def _host_cores():

@@ -595,6 +595,207 @@ void prefix_attn_lds_kernel(AttnParams a) {
   }
 }
 
+// Decode steps (a plan: few (group, head) cells, key splits): the agent's PREFIX blocks
+// are shared by the workgroup's four 16-row tiles, so the split's prefix blocks (split,
+// split + n_used, ...) are staged through LDS once per workgroup and attended by every
+// tile (the per-wave kernel loads each one per tile: 4x the load instructions, 68 % issue
+// stalls at C5); each tile's own streams' history blocks are then loaded per wave as
+// there.  Every key block is attended exactly once per (query row, split) as in the
+// per-wave assignment, so the split partials and the merge are unchanged.
+template <int D>
+__global__ __launch_bounds__(kAttnThreads, D <= 128 ? 2 : 1)
+void prefix_attn_plan_lds_kernel(AttnParams a) {
+  using LT = LdsTile<D>;
+  constexpr int NDS = D / 32;
+  constexpr int NDT = D / 16;
+  constexpr int LDSW = D + 2;
+  constexpr int kBufBytes = 2 * LT::ELEMS * 2;
+  constexpr int kCombBytes = 3 * 16 * LDSW * 4;
+  __shared__ __attribute__((aligned(16))) char lds[kBufBytes > kCombBytes ? kBufBytes : kCombBytes];
+  __bf16* buf = reinterpret_cast<__bf16*>(lds);
+  auto sm = reinterpret_cast<float (*)[16][LDSW]>(lds);
+
+  const int4 e = a.plan[blockIdx.x];
+  const int pg = e.x, qg = e.y, split = e.z & 255, n_used = e.z >> 8, slot = e.w;
+  const int gi = pg / a.Hkv, g = pg % a.Hkv;
+  const int p = a.gpfx ? a.gpfx[gi] : gi;
+  const int M = a.n_str * a.T * a.rep;
+  const int r0 = qg * kGroupRows;
+  const int nrows = min(kGroupRows, M - r0);
+  const int n_qt = (nrows + 15) >> 4;
+  const int kw = n_qt == 1 ? 4 : (n_qt == 2 ? 2 : 1);
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
+  const int qt = w % n_qt, ks = w / n_qt;
+  const bool active = ks < kw;
+  const int col = lane & 15, h4 = lane >> 4;
+
+  const int row = r0 + qt * 16 + col;
+  const bool vrow = active && row < M;
+  const int rr = row < M ? row : M - 1;
+  const int jh = rr % a.rep, bt = rr / a.rep;
+  const int t = bt % a.T, b = bt / a.T;
+  const int64_t tok = (static_cast<int64_t>(gi) * a.n_str + b) * a.T + t;
+  const int head = g * a.rep + jh;
+  const int hb = *a.hist_base;
+  const int pl = a.plen[p];
+  const int64_t po = a.poff[p];
+  const int hv = min(hb + t + 1, static_cast<int>(a.ldh));
+  const int kmin_pos = a.window > 0 ? pl + hb + t - a.window + 1 : INT32_MIN;
+
+  const int nbp = (pl + kKeyBlock - 1) / kKeyBlock;
+  // this split's prefix blocks: split, split + n_used, ...  (workgroup-uniform)
+  const int npi = nbp > split ? (nbp - split + n_used - 1) / n_used : 0;
+
+  bf16x8 qf[NDS];
+  {
+    const __bf16* qrow = a.q + (tok * a.H + head) * D + 8 * h4;
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds) {
+      if (vrow) {
+        qf[ds] = *reinterpret_cast<const bf16x8*>(qrow + ds * 32);
+      } else {
+#pragma unroll
+        for (int e2 = 0; e2 < 8; ++e2) qf[ds][e2] = static_cast<__bf16>(0.0f);
+      }
+    }
+  }
+  f32x4 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.0f;
+
+  // ---- prefix blocks through LDS ----
+  u32x4 rk[LT::NCH], rv[LT::NCH];
+  auto fetch = [&](int j) {
+    const int64_t k0 = static_cast<int64_t>(g) * a.ldp + po + (split + j * n_used) * kKeyBlock;
+    const __bf16* ksrc = a.kp + k0 * D;
+    const __bf16* vsrc = a.vtp + k0 * D;
+#pragma unroll
+    for (int i = 0; i < LT::NCH; ++i) {
+      const int c = tid + kAttnThreads * i;
+      rk[i] = *reinterpret_cast<const u32x4*>(ksrc + c * 8);
+      rv[i] = *reinterpret_cast<const u32x4*>(vsrc + c * 8);
+    }
+  };
+  auto stage = [&](int sbuf) {
+    __bf16* kd = buf + sbuf * LT::ELEMS;
+    __bf16* vd = kd + LT::KELEMS;
+#pragma unroll
+    for (int i = 0; i < LT::NCH; ++i) {
+      const int c = tid + kAttnThreads * i;
+      *reinterpret_cast<u32x4*>(kd + (c / (D / 8)) * LT::KROW + (c % (D / 8)) * 8) = rk[i];
+      *reinterpret_cast<u32x4*>(vd + (c >> 2) * LT::VROW + (c & 3) * 8) = rv[i];
+    }
+  };
+  if (npi > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+  for (int j = 0; j < npi; ++j) {
+    const bool more = j + 1 < npi;
+    if (more) fetch(j + 1);
+    if (active && (j % kw) == ks) {
+      const __bf16* kd = buf + (j & 1) * LT::ELEMS;
+      const __bf16* vd = kd + LT::KELEMS;
+      KeyBlock<D> f;
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) {
+        f.k0[ds] = *reinterpret_cast<const bf16x8*>(kd + col * LT::KROW + ds * 32 + 8 * h4);
+        f.k1[ds] = *reinterpret_cast<const bf16x8*>(kd + (16 + col) * LT::KROW + ds * 32 + 8 * h4);
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        f.vlo[dt] = *reinterpret_cast<const bf16x4*>(vd + (dt * 16 + col) * LT::VROW + 4 * h4);
+        f.vhi[dt] = *reinterpret_cast<const bf16x4*>(vd + (dt * 16 + col) * LT::VROW + 16 + 4 * h4);
+      }
+      ItemRef r;
+      r.k = nullptr;
+      r.v = nullptr;
+      r.kb = (split + j * n_used) * kKeyBlock;
+      r.lim = vrow ? pl : 0;
+      r.pos0 = 0;
+      attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+    }
+    if (more) stage((j + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- the tile's own streams' history blocks, per wave (split * kw + ks, + nslot, ...) ----
+  const int rt0 = r0 + qt * 16, rt1 = min(rt0 + 15, M - 1);
+  const int b_lo = (rt0 / a.rep) / a.T, b_hi = (rt1 / a.rep) / a.T;
+  const int t_hi = b_lo == b_hi ? (rt1 / a.rep) % a.T : a.T - 1;
+  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
+  const int n_hist = (b_hi - b_lo + 1) * nbh;
+  const int nslot = n_used * kw;
+  if (active) {
+    for (int ih = split * kw + ks; ih < n_hist; ih += nslot) {
+      KeyBlock<D> f;
+      const ItemRef r = item_ref(a, nbp + ih, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D);
+      load_block<D>(f, r);
+      attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  if (kw > 1) {
+    if (active && ks > 0) {
+      const int sl = w - n_qt;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm[sl][col][dt * 16 + 4 * h4 + i] = o[dt][i];
+      if (h4 == 0) {
+        sm[sl][col][D] = m;
+        sm[sl][col][D + 1] = l;
+      }
+    }
+    __syncthreads();
+    if (active && ks == 0) {
+      float mt = m;
+      for (int k = 1; k < kw; ++k) mt = fmaxf(mt, sm[qt + n_qt * k - n_qt][col][D]);
+      const float c0 = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m - mt);
+      l *= c0;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] *= c0;
+      for (int k = 1; k < kw; ++k) {
+        const int sl = qt + n_qt * k - n_qt;
+        const float mk = sm[sl][col][D];
+        const float ck = mt == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mk - mt);
+        l = fmaf(sm[sl][col][D + 1], ck, l);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[dt][i] = fmaf(sm[sl][col][dt * 16 + 4 * h4 + i], ck, o[dt][i]);
+      }
+      m = mt;
+    }
+  }
+  if (!vrow || ks != 0) return;
+  if (n_used == 1) {
+    const float inv = l > 0.0f ? 1.0f / l : 0.0f;
+    __bf16* orow = a.out + (tok * a.H + head) * D + 4 * h4;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = static_cast<__bf16>(o[dt][i] * inv);
+      *reinterpret_cast<bf16x4*>(orow + dt * 16) = v;
+    }
+  } else {
+    float* pr = a.part + (static_cast<int64_t>(slot) * kGroupRows + qt * 16 + col) * LDSW;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+      *reinterpret_cast<f32x4*>(pr + dt * 16 + 4 * h4) = o[dt];
+    if (h4 == 0) {
+      pr[D] = m;
+      pr[D + 1] = l;
+    }
+  }
+}
+
 // One workgroup per merge entry (kMergeRows rows of a split (group, head, query group)),
 // each wave two rows, one per 32-lane half: the half's lanes fold the splits' (m, l) into
 // per-split weights, then the wave sums the weighted partial outputs (f32x4 columns).
@@ -669,6 +870,7 @@ struct RopeParams {
   int64_t ldh;
   int64_t n_tok;
   int32_t n_str, T, H, Hkv, D;
+  int32_t skip_v;           // V placed by v_tile_place_kernel instead
 };
 
 // one workgroup per token: the token's D/2 angles' sincos once into LDS, then every
@@ -701,6 +903,7 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
     const bf16x4 a = *reinterpret_cast<const bf16x4*>(src);
     const bf16x4 b = *reinterpret_cast<const bf16x4*>(src + half);
     if (hh >= r.H + r.Hkv) {                         // v: transposed placement, no rotation
+      if (r.skip_v) continue;
       const int g = hh - r.H - r.Hkv;
       __bf16* dst = vth + ((s * r.Hkv + g) * r.ldh + (slot & ~31)) * r.D +
                     static_cast<int64_t>(i0) * 32 + (slot & 31);
@@ -722,6 +925,51 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
                            : kh + ((s * r.Hkv + (hh - r.H)) * r.ldh + slot) * r.D;
     *reinterpret_cast<bf16x4*>(dst + i0) = y1;
     *reinterpret_cast<bf16x4*>(dst + half + i0) = y2;
+  }
+}
+
+// Multi-token streams (T >= 32: scoring chunks, prompt prefill): V placed by 32-slot tiles,
+// one workgroup per (stream, K/V head, slot tile): the tile's tokens' V rows (16-byte loads)
+// into LDS, then the tile's D rows of 32 slots written with 16-byte stores — the per-token
+// placement of rope_place_kernel writes 2-byte pieces 64 B apart, from workgroups on every
+// XCD.  Slots outside [hist_base, hist_base + T) are left as they are.
+__global__ __launch_bounds__(256) void v_tile_place_kernel(RopeParams r, int32_t n_tiles) {
+  __shared__ __attribute__((aligned(16))) __bf16 tile[32][256 + 8];   // [slot][d], D <= 256
+  const int D = r.D;
+  const int tid = threadIdx.x;
+  const int c = static_cast<int>(blockIdx.x % n_tiles);
+  const int64_t sg = blockIdx.x / n_tiles;            // s * Hkv + g
+  const int g = static_cast<int>(sg % r.Hkv);
+  const int64_t s = sg / r.Hkv;
+  const int hb = *r.hist_base;
+  const int slot0 = 32 * c;
+  if (slot0 + 32 <= hb || slot0 >= hb + r.T) return;  // no token of this stream lands here
+  const int dch = D >> 3;                              // 16-byte chunks per V row
+  for (int ch = tid; ch < 32 * dch; ch += 256) {
+    const int sl = ch / dch, dc = ch - sl * dch;
+    const int t = slot0 + sl - hb;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (t >= 0 && t < r.T)
+      v = *reinterpret_cast<const u32x4*>(r.qkv + (s * r.T + t) * r.ldqkv +
+                                          static_cast<int64_t>(r.H + r.Hkv + g) * D + dc * 8);
+    *reinterpret_cast<u32x4*>(&tile[sl][dc * 8]) = v;
+  }
+  __syncthreads();
+  __bf16* base = r.vth + ((s * r.Hkv + g) * r.ldh + slot0) * D;   // the tile's [D][32]
+  for (int ch = tid; ch < 4 * D; ch += 256) {
+    const int d = ch >> 2, q = ch & 3;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[q * 8 + e][d];
+    const int t0 = slot0 + q * 8 - hb;
+    __bf16* dst = base + d * 32 + q * 8;
+    if (t0 >= 0 && t0 + 8 <= r.T) {
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (t0 + e >= 0 && t0 + e < r.T) dst[e] = v[e];
+    }
   }
 }
 
@@ -794,6 +1042,11 @@ int attn_target_wgs() {
 // scoring chunks / prompt prefill on the LDS-staged kernel (CS_ATTN_LDS=0: the per-wave one)
 bool attn_lds() {
   const char* e = getenv("CS_ATTN_LDS");
+  return !(e && atoi(e) == 0);
+}
+// decode steps (a plan): the prefix blocks through LDS (CS_ATTN_PLAN_LDS=0: per wave)
+bool attn_plan_lds() {
+  const char* e = getenv("CS_ATTN_PLAN_LDS");
   return !(e && atoi(e) == 0);
 }
 int attn_min_items() {
@@ -983,7 +1236,9 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   const dim3 merge_grid(static_cast<uint32_t>(plan ? n_merge : 0));
 #define CS_ATTN_LAUNCH(DV)                                                              \
   do {                                                                                  \
-    if (plan)                                                                           \
+    if (plan && attn_plan_lds())                                                        \
+      hipLaunchKernelGGL(prefix_attn_plan_lds_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a); \
+    else if (plan)                                                                      \
       hipLaunchKernelGGL((prefix_attn_kernel<DV, true>), grid, dim3(kAttnThreads), 0, st, a); \
     else if (attn_lds())                                                                \
       hipLaunchKernelGGL(prefix_attn_lds_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a); \
@@ -1053,8 +1308,20 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
   r.D = D;
   if (D % 8 != 0 || D > 256) return fail(CS_ERR_INVALID, "cs_rope_place: head_dim must be a multiple of 8, <= 256");
   if (r.n_tok > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many tokens");
+  // V by 32-slot tiles when the streams carry many tokens (CS_ROPE_VTILE=0: per token)
+  const int64_t n_tiles = ld_hist / 32;
+  const int64_t n_vwg = static_cast<int64_t>(n_groups) * n_str * Hkv * n_tiles;
+  {
+    const char* e = getenv("CS_ROPE_VTILE");
+    r.skip_v = (T >= 32 && ld_hist % 32 == 0 && ld_qkv % 8 == 0 &&
+                reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && n_vwg <= 0x7fffffffLL &&
+                !(e && atoi(e) == 0)) ? 1 : 0;
+  }
   hipLaunchKernelGGL(rope_place_kernel, dim3(static_cast<uint32_t>(r.n_tok)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), r);
+  if (r.skip_v)
+    hipLaunchKernelGGL(v_tile_place_kernel, dim3(static_cast<uint32_t>(n_vwg)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), r, static_cast<int32_t>(n_tiles));
   return check_launch("cs_rope_place");
 }
 

@@ -19,6 +19,7 @@ Everything after the LM head runs in the HIP kernels (ops.*).
 """
 from __future__ import annotations
 
+import gc
 import os
 import threading
 from dataclasses import dataclass
@@ -754,12 +755,30 @@ class DecodeState:
                 g = torch.cuda.CUDAGraph()
                 s = torch.cuda.Stream(device=dev)
                 s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, pool=self._pool, stream=s):
-                        self._body(post)
+                # no cyclic garbage collection while capturing: an unreachable DecodeState
+                # of an earlier call freed by the collector mid-capture destroys its graphs,
+                # which HIP refuses during a capture (the destructor then aborts the process)
+                was_enabled = gc.isenabled()
+                gc.disable()
+                try:
+                    with torch.cuda.stream(s):
+                        with torch.cuda.graph(g, pool=self._pool, stream=s):
+                            self._body(post)
+                finally:
+                    if was_enabled:
+                        gc.enable()
                 torch.cuda.current_stream().wait_stream(s)
                 self._pool = g.pool()
                 self._graphs[key] = g
             g.replay()
         self.cur = 1 - self.cur
         self.steps += 1
+
+    def release(self) -> None:
+        """Drop the captured step graphs and their memory pool now (after the work that
+        replays them has finished), instead of whenever the garbage collector reaches the
+        state's reference cycles (its ``post`` closures)."""
+        if self._graphs:
+            torch.cuda.current_stream().synchronize()
+        self._graphs.clear()
+        self._pool = None

@@ -220,19 +220,27 @@ class BeamSearchGenerator(BaseGenerator):
         self.text_compat_candidates = 0
         if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk and merge_free:
             self.decode_path = "fused-topk"
-            st = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
+            ds = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
                              max_steps=int(self.max_tokens))
-            completed, beams = self._loop_fused_topk(engine, tok, st, A_loc, bias)
+            try:
+                completed, beams = self._loop_fused_topk(engine, tok, ds, A_loc, bias)
+            finally:
+                ds.release()
         else:
+            ds = None
             if fused:
                 self.decode_path = "fused"
-                st = _LiveBeams(DecodeState(engine, cache, n_prefix=A_loc + 1,
-                                            n_beams=int(self.beam_width),
-                                            max_steps=int(self.max_tokens)))
+                ds = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
+                                 max_steps=int(self.max_tokens))
+                st = _LiveBeams(ds)
             else:
                 self.decode_path = "eager"
                 st = BeamState(engine, cache, n_prefix=A_loc + 1)
-            completed, beams = self._loop(engine, tok, st, A, A_loc, shard, bias)
+            try:
+                completed, beams = self._loop(engine, tok, st, A, A_loc, shard, bias)
+            finally:
+                if ds is not None:
+                    ds.release()
         return self._final(completed, beams, engine.device, A_loc, shard)
 
     def _loop(self, engine, tok, st, A, A_loc, shard, bias):

@@ -189,3 +189,36 @@ def test_score_matches_full_forward_of_prefix_plus_continuation(traces):
         want = torch.log_softmax(z, -1)
         want = want[torch.arange(len(c)), torch.as_tensor(c, device=eng.device)].cpu()
         assert torch.max(torch.abs(lp[offs[r]:offs[r + 1]] - want)).item() < 1e-4, r
+
+
+@pytest.mark.parametrize("preset", ["tiny-llama", "tiny-gemma"])
+def test_bf16_methods_select_the_same_with_and_without_prefix_reuse(dev, preset):
+    """Prefix reuse (on by default) changes a prefill's bf16 rounding only at the level of
+    a different batch padding; on bf16 models Best-of-N and finite lookahead select the same
+    statement with reuse on and off, and their per-agent rewards agree within 2e-2 (bf16
+    forward, 150-token scale)."""
+    R = importlib.import_module(mp.PKG + ".runtime")
+    methods = importlib.import_module(mp.PKG + ".methods")
+    opinions = {"Agent 1": "We should fund public transit first.",
+                "Agent 2": "Lower the city's taxes before anything else.",
+                "Agent 3": "Protect parks and the environment above all."}
+    issue = "How should the city spend its budget?"
+    results = []
+    for reuse in (4, 0):
+        eng, tok = R.random_engine(preset, dev, dtype=torch.bfloat16, seed=3, reuse_caches=reuse)
+        R.register_engine("test/bf16-reuse", eng, tok)
+        try:
+            bon = methods.get_method_generator("best_of_n", {"n": 6, "max_tokens": 12, "seed": 5},
+                                               "test/bf16-reuse")
+            s_bon = bon.generate_statement(issue, opinions)
+            fl = methods.get_method_generator("finite_lookahead",
+                                              {"branching_factor": 2, "max_depth": 2,
+                                               "max_tokens": 6, "seed": 5}, "test/bf16-reuse")
+            s_fl = fl.generate_statement(issue, opinions)
+            results.append((s_bon, bon.last_welfare, s_fl, eng.reuse_stats["reused"]))
+        finally:
+            R.clear_engines()
+    (b1, w1, f1, used1), (b0, w0, f0, used0) = results
+    assert used0 == 0 and used1 > 0
+    assert b1 == b0 and f1 == f0
+    assert len(w1) == len(w0) and all(abs(x - y) < 2e-2 for x, y in zip(w1, w0))

@@ -136,7 +136,10 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
     assert torch.equal(out, run())          # deterministic: bit-identical relaunch
 
 
-@pytest.mark.parametrize("D,H,Hkv,T", [(64, 8, 2, 3), (128, 32, 8, 1), (256, 16, 8, 2)])
+@pytest.mark.parametrize("D,H,Hkv,T", [(64, 8, 2, 3), (128, 32, 8, 1), (256, 16, 8, 2),
+                                        # T >= 32: V placed by 32-slot tiles (partial tiles
+                                        # at both ends: slots 5 .. 5 + T)
+                                        (128, 32, 8, 40), (64, 8, 2, 64), (256, 16, 8, 33)])
 def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
     M = importlib.import_module(PKG + ".model")
     cfg = M.preset("tiny-llama", head_dim=D, n_heads=H, n_kv_heads=Hkv)
@@ -171,6 +174,7 @@ def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
             torch.testing.assert_close(kh[s, :, hb + t].float(), rot[tok, H:H + Hkv], atol=2e-2, rtol=1e-2)
             assert torch.equal(vrows[s, :, hb + t], qkv[tok].view(-1, D)[H + Hkv:])
     assert kh[:, :, :hb].abs().sum() == 0 and vrows[:, :, hb + T:].abs().sum() == 0
+    assert vrows[:, :, :hb].abs().sum() == 0
 
 
 def _tiny(family, dev, seed=3, dtype=torch.bfloat16, weights=None):
