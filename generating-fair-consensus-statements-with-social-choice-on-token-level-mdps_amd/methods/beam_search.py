@@ -339,13 +339,16 @@ class BeamSearchGenerator(BaseGenerator):
         tail_ids = tok.encode(tail)
         nt = len(tail_ids)
         bad = []
+        texts = [beams[b][0] + tstr[i] for i, b in enumerate(cb)]
+        apis = [t + utils.MARKER if t.endswith(("\n", " ")) else t for t in texts]
+        many = getattr(tok, "encode_many", None)
+        encs = many([tail + a for a in apis]) if many is not None else \
+            [tok.encode(tail + a) for a in apis]
         for i, (b, v) in enumerate(zip(cb, ct)):
-            text = beams[b][0] + tstr[i]
             ids = beam_ids[b] + [v]
-            api = text + utils.MARKER if text.endswith(("\n", " ")) else text
-            enc = tok.encode(tail + api)
+            enc = encs[i]
             if (enc[:nt] != tail_ids or enc[nt:nt + len(ids)] != ids
-                    or "".join(tok.tokens(ids)) != text):
+                    or "".join(tok.tokens(ids)) != texts[i]):
                 bad.append(i)
         if not bad:
             return U, W, order

@@ -315,6 +315,16 @@ class BPETokenizer:
         span = [i for i, (a, b) in enumerate(offs) if a < c1 and b > c0]
         return ids, ((span[0], span[-1] + 1) if span else (len(ids), len(ids)))
 
+    def render_chat_ids_many(self, systems, users, add_generation_prompt: bool = True):
+        """render_chat(system, user)[0] for many pairs: the prompts rendered one by one, then
+        encoded in ONE multi-threaded `tokenizers` batch (the per-call encode is most of a
+        text-compat scoring call's host time)."""
+        texts = [self.chat_text(s, u, add_generation_prompt) for s, u in zip(systems, users)]
+        return [e.ids for e in self.tk.encode_batch(texts, add_special_tokens=False)]
+
+    def encode_many(self, texts) -> List[List[int]]:
+        return [e.ids for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
+
     def chat_prefix(self, system: "str | None", user_prefix: str) -> List[int]:
         """Ids of the chat prompt up to the end of ``user_prefix`` (the part of the user
         turn shared by every candidate), with nothing of the template after it: the

@@ -20,6 +20,8 @@ batched id-level engine instead (engine.py), which scores the true user span.
 """
 from __future__ import annotations
 
+import bisect
+import itertools
 import logging
 from types import SimpleNamespace
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
@@ -111,6 +113,22 @@ def extract_user_prompt_logprobs(logprobs_data, user_prompt):
     if not keep:
         return [], []
     return [toks[i] for i in keep], [lps[i] for i in keep]
+
+
+def last_user_span_index(tokens: Sequence[str], user_prompt: str) -> int:
+    """Index of the LAST token ``extract_user_prompt_logprobs`` keeps (the last token whose
+    characters overlap the first occurrence of ``user_prompt`` in the joined token
+    strings), or -1 when it keeps none — by one C-speed find and a bisect over the tokens'
+    end offsets instead of the per-token loop."""
+    if not user_prompt:
+        return -1
+    lo = "".join(tokens).find(user_prompt)
+    if lo == -1:
+        return -1
+    ends = list(itertools.accumulate(map(len, tokens)))
+    # the first token ending at or after the span's end: it starts before the end (the
+    # first such token has a non-empty string) and is the last one that can overlap
+    return bisect.bisect_left(ends, lo + len(user_prompt))
 
 
 def span_found_at_user(tok, system_prompt, user_prompt) -> bool:
@@ -235,17 +253,23 @@ def text_compat_last(engine, tok, systems: Sequence[Optional[str]],
     n = len(users)
     res = [float(fallback)] * n
     idss, last = [], []
-    for s, u in zip(systems, users):
+    apis = [u + MARKER if u.endswith(("\n", " ")) else u for u in users]
+    many = getattr(tok, "render_chat_ids_many", None)
+    rendered = None
+    if many is not None:
+        try:    # one batched (multi-threaded) encode of every rendered prompt
+            rendered = many([s or None for s in systems], apis)
+        except Exception:   # noqa: BLE001 -- per-call path below reports the failure
+            rendered = None
+    for j, (s, u) in enumerate(zip(systems, users)):
         try:
-            api_user = u + MARKER if u.endswith(("\n", " ")) else u
-            ids, _ = tok.render_chat(s or None, api_user)
-            data = SimpleNamespace(tokens=tok.tokens(ids), token_logprobs=list(range(len(ids))))
-            _, keep = extract_user_prompt_logprobs(data, u)
+            ids = rendered[j] if rendered is not None else tok.render_chat(s or None, apis[j])[0]
+            k = last_user_span_index(tok.tokens(ids), u)
         except Exception as e:       # get_prompt_logprobs would return ([], [])
             logger.error("get_prompt_logprobs failed: %s", e)
-            ids, keep = [], []
+            ids, k = [], -1
         idss.append(list(ids))
-        last.append(keep[-1] if keep else -1)
+        last.append(k)
     todo = [j for j in range(n) if last[j] > 0]      # position 0 has no log-prob (None)
     if not todo:
         return res

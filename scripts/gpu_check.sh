@@ -12,14 +12,15 @@ run_tests() { timeout -k 10 420 python -u -m pytest tests -m gpu -v --timeout 15
 run_smoke() { timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; }
 run_bench() { timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1; }
 run_prof() {
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
-     python3 "$R/bench.py" --cpu-seconds 0 > "$OUT/prof.log" 2>&1)
+  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
+     python3 "$R/bench.py" --cpu-seconds 0 > "$OUT/prof.log" 2>&1) && \
+  rm -f "$OUT/prof/run_kernel_trace.csv"   # the per-dispatch trace exceeds gpurun's copy-back cap
 }
 run_pmc() {
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -f csv -- \
-     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --beam "" > "$OUT/pmc_fetch.log" 2>&1) && \
+     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --beam "" --e2e 0 --method "" > "$OUT/pmc_fetch.log" 2>&1) && \
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -f csv -- \
-     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --beam "" > "$OUT/pmc_write.log" 2>&1)
+     python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --beam "" --e2e 0 --method "" > "$OUT/pmc_write.log" 2>&1)
 }
 case "$STEP" in
   tests) run_tests ;;

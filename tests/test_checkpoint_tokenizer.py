@@ -113,3 +113,40 @@ def test_unregistered_real_model_id_raises(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
     with pytest.raises(ops.CSError, match="no weights for model"):
         R.get_engine("meta-llama/Meta-Llama-3.1-8B-Instruct-Turbo")
+
+
+def test_batched_text_compat_tokenization_equals_per_call():
+    """The text path's batched pieces (one multi-threaded encode for every rendered prompt,
+    the last user-span token by bisect) equal the per-call render_chat / encode and the
+    reference-semantics extract_user_prompt_logprobs, including byte-fragment appends,
+    the U+200B marker case and a user text the reference's find places elsewhere."""
+    import random
+    from types import SimpleNamespace
+    T = importlib.import_module(PKG + ".tokenizer")
+    U = importlib.import_module(PKG + ".utils")
+    tok = T.BPETokenizer(FIXTURE, "llama3")
+    rnd = random.Random(5)
+    system = "You are a helpful assistant. Answer."
+    users = []
+    for i in range(60):
+        base = "Participant opinion: genetic privacy matters. Statement: We should"
+        users.append(base + "".join(tok.token_str(rnd.randrange(1, tok.n_table)) for _ in range(i % 4)))
+    users += ["Answer", "Statement ends with a space ", "new line\n", ""]
+    apis = [u + U.MARKER if u.endswith(("\n", " ")) else u for u in users]
+    many = tok.render_chat_ids_many([system] * len(users), apis)
+    assert many == [tok.render_chat(system, a)[0] for a in apis]
+    assert tok.encode_many(apis) == [tok.encode(a) for a in apis]
+    for ids, u in zip(many, users):
+        toks = tok.tokens(ids)
+        _, keep = U.extract_user_prompt_logprobs(
+            SimpleNamespace(tokens=toks, token_logprobs=list(range(len(toks)))), u)
+        assert U.last_user_span_index(toks, u) == (keep[-1] if keep else -1)
+    # synthetic token lists with empty strings and spans at the edges
+    for _ in range(300):
+        toks = ["".join(rnd.choice("ab ") for _ in range(rnd.randrange(0, 3)))
+                for _ in range(rnd.randrange(1, 12))]
+        text = "".join(toks)
+        u = text[rnd.randrange(0, len(text) + 1):][:rnd.randrange(0, 5)] if text else "x"
+        _, keep = U.extract_user_prompt_logprobs(
+            SimpleNamespace(tokens=toks, token_logprobs=list(range(len(toks)))), u)
+        assert U.last_user_span_index(toks, u) == (keep[-1] if keep else -1), (toks, u)
