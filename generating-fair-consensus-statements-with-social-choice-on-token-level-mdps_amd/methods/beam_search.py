@@ -421,9 +421,8 @@ class BeamSearchGenerator(BaseGenerator):
                 return s
 
             new_beams, new_idx = self._walk_fast(live, beams, K, ts, U_h, completed)
-            self.step_log.append({"candidates": [beams[i // K][0] + ts(i) for i in range(n_live * K)],
-                                  "min_rewards": W_h[:n_live * K].astype(np.float64).tolist(),
-                                  "kept": [s for s, _ in new_beams]})
+            self.step_log.append(_StepRecord([s for s, _ in new_beams], beams, ids_f.copy(),
+                                             W_h[:n_live * K].copy(), n_live * K, K, tok))
             beams = new_beams
             if not beams or step + 1 >= self.max_tokens:
                 break
@@ -471,6 +470,27 @@ class BeamSearchGenerator(BaseGenerator):
             logger.warning("brushup (a remote LLM rewrite of the ending) is not part of the "
                            "local scoring path; returning the statement unchanged")
         return final
+
+
+class _StepRecord(dict):
+    """One step of the fast loop's log: "kept" now; "candidates" (every live candidate's
+    text) and "min_rewards" built on first access — building them for all B*K candidates
+    every step was a third of the host time of a C3 step."""
+
+    def __init__(self, kept, beams, ids, W, n, K, tok):
+        super().__init__(kept=kept)
+        self._src = (beams, ids, W, n, K, tok)
+
+    def __missing__(self, key):
+        beams, ids, W, n, K, tok = self._src
+        if key == "candidates":
+            v = [beams[i // K][0] + tok.token_str(int(ids[i])) for i in range(n)]
+        elif key == "min_rewards":
+            v = W.astype(np.float64).tolist()
+        else:
+            raise KeyError(key)
+        self[key] = v
+        return v
 
 
 class _HostCopy:
