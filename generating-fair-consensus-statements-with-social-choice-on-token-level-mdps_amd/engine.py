@@ -709,8 +709,13 @@ class DecodeState:
         self.cur = 0
         self.steps = 0                                   # tokens appended so far (host copy)
         self.hist_base = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.src = torch.arange(self.S, dtype=torch.long, device=dev)
-        self.tok = torch.zeros(self.S, dtype=torch.long, device=dev)
+        # a step's inputs (parent stream, new token per stream): ONE pinned host buffer and
+        # ONE device buffer, one asynchronous copy per step (the graphs read the device side)
+        self._in_h = [torch.empty(2 * self.S, dtype=torch.long, pin_memory=True) for _ in range(2)]
+        self._in_ev: List[Optional[torch.cuda.Event]] = [None, None]
+        self._in_d = torch.zeros(2 * self.S, dtype=torch.long, device=dev)
+        self._in_d[:self.S] = torch.arange(self.S, dtype=torch.long, device=dev)
+        self.src, self.tok = self._in_d[:self.S], self._in_d[self.S:]
         self.hidden = cache.last_hidden.repeat_interleave(self.B, dim=0).contiguous()   # [S, d]
         self.use_graphs = use_graphs
         self._graphs: dict = {}
@@ -740,12 +745,18 @@ class DecodeState:
         if self.steps >= self.ldh:
             raise ValueError("history capacity exhausted (max_steps)")
         dev = self.e.device
-        P, B = self.P, self.B
-        par = torch.as_tensor(list(parent), dtype=torch.long)
-        src = (torch.arange(P)[:, None] * B + par[None, :]).reshape(-1)
-        tok = torch.as_tensor(list(tokens), dtype=torch.long).repeat(P)
-        self.src.copy_(src.to(dev, non_blocking=True))
-        self.tok.copy_(tok.to(dev, non_blocking=True))
+        P, B, S = self.P, self.B, self.S
+        # two pinned staging buffers: the one written now was last copied two steps ago;
+        # wait for that copy only (back-to-back replays keep the queue full)
+        k = self.steps & 1
+        if self._in_ev[k] is not None:
+            self._in_ev[k].synchronize()
+        h = self._in_h[k].numpy()
+        h[:S] = (np.arange(P)[:, None] * B + np.asarray(parent, dtype=np.int64)[None, :]).reshape(-1)
+        h[S:] = np.tile(np.asarray(tokens, dtype=np.int64), P)
+        self._in_d.copy_(self._in_h[k], non_blocking=True)   # stream-ordered after the last replay
+        ev = self._in_ev[k] = torch.cuda.Event()
+        ev.record()
         key = (self.cur, post)
         if not self.use_graphs or self.steps == 0:
             self._body(post)                      # the first step runs eagerly (warm-up)

@@ -381,6 +381,7 @@ class BeamSearchGenerator(BaseGenerator):
         W_buf = torch.empty(C, dtype=torch.float32, device=dev)
         rewards = torch.zeros(A, B, dtype=torch.float32, device=dev)
         kidx = torch.zeros(B, dtype=torch.long, device=dev)
+        kidx_h = torch.zeros(B, dtype=torch.long, pin_memory=True)   # read back every step first
         ids_buf = torch.empty(B, K, dtype=torch.int32, device=dev)
         order_buf = torch.empty(C, dtype=torch.int32, device=dev)
         ws = ops.Workspace(zeroed=True)
@@ -420,7 +421,8 @@ class BeamSearchGenerator(BaseGenerator):
                     s = tstr[i] = tok.token_str(int(ids_f[i]))
                 return s
 
-            new_beams, new_idx = self._walk_fast(live, beams, K, ts, U_h, completed)
+            new_beams, new_idx = self._walk_fast(live, beams, K, ts, U_h, completed,
+                                                 ids_f, tok)
             self.step_log.append(_StepRecord([s for s, _ in new_beams], beams, ids_f.copy(),
                                              W_h[:n_live * K].copy(), n_live * K, K, tok))
             beams = new_beams
@@ -428,18 +430,28 @@ class BeamSearchGenerator(BaseGenerator):
                 break
             n = len(new_idx)
             kept = new_idx + [new_idx[0]] * (B - n)
-            kidx.copy_(torch.as_tensor(kept, dtype=torch.long).to(dev, non_blocking=True))
+            kidx_h.numpy()[:] = kept        # the last copy out of it finished before the fetch
+            kidx.copy_(kidx_h, non_blocking=True)
             st.advance([i // K for i in kept], [int(ids_f[i]) for i in kept], post=post)
             n_live = n
         return completed, beams
 
-    def _walk_fast(self, order, beams, K, ts, U_h, completed):
+    def _walk_fast(self, order, beams, K, ts, U_h, completed, ids=None, tok=None):
         """The reference walk (beam_search.py:562-600) over a full candidate order: once
         beam_width beams are kept only EOS candidates still matter, and only they are
-        visited."""
+        visited (found by token id through a per-generator id -> is-EOS cache, without
+        building the other candidates' strings)."""
         new_beams, new_idx, seen = [], [], set()
         eos = self.LLAMA3_EOS_TOKENS
-        for i in order.tolist():
+        rest = None
+        if ids is not None:
+            ido = np.asarray(ids)[order]
+            flags = self._eos_flags(ido, tok)
+        order = order.tolist()
+        for pos, i in enumerate(order):
+            if ids is not None and len(new_beams) >= self.beam_width:
+                rest = [order[p] for p in (np.nonzero(flags[pos:])[0] + pos).tolist()]
+                break
             s = ts(i)
             is_eos = s in eos
             if len(new_beams) >= self.beam_width and not is_eos:
@@ -453,7 +465,26 @@ class BeamSearchGenerator(BaseGenerator):
                 new_beams.append((seq, U_h[:, i].astype(np.float64).tolist()))
                 new_idx.append(i)
                 seen.add(seq)
+        for i in rest or ():      # the EOS candidates after the kept beams, in order
+            seq = beams[i // K][0] + ts(i)
+            if seq not in seen:
+                completed.append((seq, U_h[:, i].astype(np.float64).tolist()))
         return new_beams, new_idx
+
+    def _eos_flags(self, ids: np.ndarray, tok) -> np.ndarray:
+        """Whether each token id's string is an EOS string, from a per-generator table
+        filled on first sight of an id."""
+        tab = self.__dict__.get("_eos_tab")
+        top = int(ids.max()) + 1 if ids.size else 0
+        if tab is None or tab.shape[0] < top:
+            grown = np.full(max(top, 1024), -1, dtype=np.int8)
+            if tab is not None:
+                grown[:tab.shape[0]] = tab
+            tab = self._eos_tab = grown
+        f = tab[ids]
+        for v in np.unique(ids[f < 0]).tolist():
+            tab[v] = 1 if tok.token_str(int(v)) in self.LLAMA3_EOS_TOKENS else 0
+        return tab[ids] == 1
 
     def _final(self, completed, beams, dev, A_loc, shard) -> str:
         completed = completed + beams
