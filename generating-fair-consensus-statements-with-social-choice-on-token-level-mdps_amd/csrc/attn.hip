@@ -396,8 +396,11 @@ struct LdsTile {
   static constexpr int NCH = D / 64;                 // 16-byte chunks per thread per operand
 };
 
+#ifndef CS_ATTN_LDS_W256
+#define CS_ATTN_LDS_W256 1   // waves per SIMD of the D = 256 variant (2: 208 B/lane of spills)
+#endif
 template <int D>
-__global__ __launch_bounds__(kAttnThreads, D <= 128 ? 2 : 1)
+__global__ __launch_bounds__(kAttnThreads, D <= 128 ? 2 : CS_ATTN_LDS_W256)
 void prefix_attn_lds_kernel(AttnParams a) {
   using LT = LdsTile<D>;
   constexpr int NDS = D / 32;
@@ -602,8 +605,9 @@ void prefix_attn_lds_kernel(AttnParams a) {
 // stalls at C5); each tile's own streams' history blocks are then loaded per wave as
 // there.  Every key block is attended exactly once per (query row, split) as in the
 // per-wave assignment, so the split partials and the merge are unchanged.
+// two waves per SIMD at every D (D = 256: 237 VGPRs, no spills; 1 wave/SIMD before)
 template <int D>
-__global__ __launch_bounds__(kAttnThreads, D <= 128 ? 2 : 1)
+__global__ __launch_bounds__(kAttnThreads, 2)
 void prefix_attn_plan_lds_kernel(AttnParams a) {
   using LT = LdsTile<D>;
   constexpr int NDS = D / 32;
