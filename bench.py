@@ -459,7 +459,9 @@ def method_leg(name, args, world, rank, dev):
         steady = d[2:] if d.size > 4 else d           # past the two graph captures
         step_s = _max_over_ranks(float(np.median(steady)) if steady.size else el, world, dev)
         runs.append({"statement_s": el, "steps": gen.steps_run, "step_s": step_s,
-                     "path": gen.decode_path})
+                     "path": gen.decode_path,
+                     "speculation": {"hits": getattr(gen, "spec_hits", 0),
+                                     "misses": getattr(gen, "spec_misses", 0)}})
     step_s = float(np.median([r["step_s"] for r in runs]))
     steps = runs[-1]["steps"]
     A, B, K = mc["agents"], mc["beam_width"], mc["top_k"]
@@ -475,9 +477,12 @@ def method_leg(name, args, world, rank, dev):
            "statement_s": float(np.median([r["statement_s"] for r in runs])),
            "steps_per_statement": steps, "statements": len(runs), "model_init_s": init_s,
            "decode_path": runs[-1]["path"],
+           "speculative_steps": runs[-1]["speculation"],
            "timing": "median host step time of the generator's loop (forward + LM head + "
-                     "cs_beam_decode_step graph replay, device->host copy, reference walk), "
-                     "max over ranks; statement_s includes prefill and the graph captures"}
+                     "cs_beam_decode_step graph replay, device->host copy, reference walk; the "
+                     "next step queued before the walk when it is the order's top B, redone "
+                     "on a miss), max over ranks; statement_s includes prefill and the graph "
+                     "captures"}
     if graph_ms is not None:
         out["graph_step_ms"] = graph_ms
         out["host_overhead_frac"] = step_s * 1e3 / graph_ms - 1.0

@@ -757,6 +757,10 @@ class DecodeState:
         self._in_d.copy_(self._in_h[k], non_blocking=True)   # stream-ordered after the last replay
         ev = self._in_ev[k] = torch.cuda.Event()
         ev.record()
+        self._replay(post)
+
+    def _replay(self, post) -> None:
+        dev = self.e.device
         key = (self.cur, post)
         if not self.use_graphs or self.steps == 0:
             self._body(post)                      # the first step runs eagerly (warm-up)
@@ -784,6 +788,23 @@ class DecodeState:
             g.replay()
         self.cur = 1 - self.cur
         self.steps += 1
+
+    @torch.no_grad()
+    def advance_device(self, post=None) -> None:
+        """advance() with the step's inputs already in device memory (``src`` / ``tok``,
+        e.g. written by the previous step's ``post`` from its own candidate order): no
+        host input, so the step can be queued before the host has read the last one."""
+        if self.steps >= self.ldh:
+            raise ValueError("history capacity exhausted (max_steps)")
+        self._replay(post)
+
+    def rewind(self) -> None:
+        """Undo the last advance (queued after it on the stream): the ping-pong parity, the
+        step count and the device-side history base.  The other history buffer it wrote is
+        rewritten by the next advance (it reads only the buffer this one read)."""
+        self.cur = 1 - self.cur
+        self.steps -= 1
+        self.hist_base -= 1
 
     def release(self) -> None:
         """Drop the captured step graphs and their memory pool now (after the work that

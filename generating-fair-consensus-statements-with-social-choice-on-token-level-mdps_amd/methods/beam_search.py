@@ -106,6 +106,8 @@ class BeamSearchGenerator(BaseGenerator):
         self.top_k = c.get("top_k", self.beam_width)
         self.fused_decode = c.get("fused_decode", True)
         self.fast_topk = c.get("fast_topk", True)
+        # fast top-K loop: queue the next step before walking this one (redone on a miss)
+        self.speculate = c.get("speculative_steps", False)
         # how a candidate's log-prob is read with a tokenizer that is not merge-free (BPE):
         # "text" (default) = the reference's re-tokenized prompt + statement + token, last
         # log-prob (beam_search.py:358-390), candidates whose re-tokenization differs from
@@ -398,18 +400,43 @@ class BeamSearchGenerator(BaseGenerator):
                                  softcap=engine.softcap, workspace=ws, out_U=U_buf, out_W=W_buf,
                                  out_ids=ids_buf, out_order=order_buf)
 
+        P = st.P
+        p_base = torch.arange(P, device=dev)[:, None] * B
+
         def post():
             torch.index_select(U_buf, 1, kidx, out=rewards)
             score()
+            if spec:
+                # the next step's inputs as the walk will most often choose them: the B best
+                # candidates of this step's order (no duplicate text or EOS among them);
+                # the host overwrites them whenever its walk differs
+                k_s = order_buf[:B].long()
+                kidx.copy_(k_s)
+                st.src.copy_((p_base + torch.div(k_s, K, rounding_mode="floor")[None, :]).reshape(-1))
+                st.tok.copy_(ids_buf.view(-1)[k_s].repeat(P))
 
+        # speculative steps: the next step is queued from the device-side order before the
+        # host has walked this one, and redone (rewind + host inputs) when the walk differs
+        spec = bool(self.speculate) and st.use_graphs
+        self.spec_hits = self.spec_misses = 0
         score()                                   # step 0 (eager): every beam = the prefix
-        host = _HostCopy()
+        hosts = (_HostCopy(), _HostCopy())
+        pending = hosts[0].start(ids_buf, order_buf, W_buf, U_buf)
+        nxt = None                                # the queued speculative step's results
         beams: List[Tuple[str, List[float]]] = [("", [0.0] * A)]
         n_live = 1
         completed: List[Tuple[str, List[float]]] = []
         for step in range(self.max_tokens):
             self.steps_run += 1
-            ids_h, order_h, W_h, U_h = host.fetch(ids_buf, order_buf, W_buf, U_buf)
+            # queue step + 1 now when this step's beams will most likely be its B best
+            # candidates (every beam live; post() has written the inputs); the GPU runs it
+            # while the host walks this step
+            if spec and step >= 1 and n_live == B and step + 1 < self.max_tokens:
+                st.advance_device(post=post)
+                nxt = hosts[(step + 1) & 1].start(ids_buf, order_buf, W_buf, U_buf)
+            else:
+                nxt = None
+            ids_h, order_h, W_h, U_h = pending.wait()
             self.step_times.append(time.perf_counter())   # this step's results are on the host
             ids_f = ids_h.reshape(-1)
             live = order_h[order_h < n_live * K]                          # beams b < n_live
@@ -430,9 +457,19 @@ class BeamSearchGenerator(BaseGenerator):
                 break
             n = len(new_idx)
             kept = new_idx + [new_idx[0]] * (B - n)
-            kidx_h.numpy()[:] = kept        # the last copy out of it finished before the fetch
-            kidx.copy_(kidx_h, non_blocking=True)
-            st.advance([i // K for i in kept], [int(ids_f[i]) for i in kept], post=post)
+            if nxt is not None and n == B and new_idx == order_h[:B].tolist():
+                self.spec_hits += 1               # the queued step is this walk's step
+                pending = nxt
+            else:
+                if nxt is not None:
+                    self.spec_misses += 1
+                    st.rewind()
+                    # post() of the redo reads this step's U: restore it from the host copy
+                    U_buf.copy_(pending.outs[3], non_blocking=True)
+                kidx_h.numpy()[:] = kept    # its last copy finished before this step's results
+                kidx.copy_(kidx_h, non_blocking=True)
+                st.advance([i // K for i in kept], [int(ids_f[i]) for i in kept], post=post)
+                pending = hosts[(step + 1) & 1].start(ids_buf, order_buf, W_buf, U_buf)
             n_live = n
         return completed, beams
 
@@ -531,12 +568,23 @@ class _HostCopy:
         self.bufs = {}
 
     def fetch(self, *ts):
-        outs = []
+        self.start(*ts)
+        torch.cuda.current_stream().synchronize()
+        return [o.numpy() for o in self.outs]
+
+    def start(self, *ts):
+        """Queue the copies (after everything queued so far) and an event behind them."""
+        self.outs = []
         for j, t in enumerate(ts):
             b = self.bufs.get(j)
             if b is None or b.shape != t.shape or b.dtype != t.dtype:
                 b = self.bufs[j] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             b.copy_(t, non_blocking=True)
-            outs.append(b)
-        torch.cuda.current_stream().synchronize()
-        return [o.numpy() for o in outs]
+            self.outs.append(b)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        return self
+
+    def wait(self):
+        self.ev.synchronize()
+        return [o.numpy() for o in self.outs]

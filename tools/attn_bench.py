@@ -16,6 +16,13 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+LIB = None
+if "--lib" in sys.argv:   # A/B another build of the library: --lib path/to/lib.so
+    i = sys.argv.index("--lib")
+    LIB = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
+    _lib = importlib.import_module(PKG + "._lib")
+    _lib.LIB_NAME = os.path.relpath(os.path.abspath(LIB), os.path.join(REPO, PKG))
 
 SHAPES = {
     # name: (n agent prefixes, agent len, ref len, n_str, T, H, Hkv, D, hist G, softcap)
@@ -75,7 +82,7 @@ def run(name, reps=50):
     us = e0.elapsed_time(e1) * 1e3 / reps
     kv_bytes = 2 * Hkv * sum(lens) * D * 2 + 2 * S * Hkv * (G + T) * D * 2
     flops = 4 * S * T * H * D * (sum(lens) / n_grp + G + T / 2)
-    print(json.dumps({"shape": name, "us": us, "kv_bytes": kv_bytes,
+    print(json.dumps({"shape": name, "lib": LIB or "tree", "us": us, "kv_bytes": kv_bytes,
                       "gb_per_s": kv_bytes / us / 1e3, "tflops": flops / us / 1e6}), flush=True)
 
 
