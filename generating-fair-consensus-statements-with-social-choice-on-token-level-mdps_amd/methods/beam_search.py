@@ -30,6 +30,7 @@ order on every rank; rank 0's proposals are used everywhere.
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import List, Optional, Tuple
 
@@ -107,7 +108,8 @@ class BeamSearchGenerator(BaseGenerator):
         self.fused_decode = c.get("fused_decode", True)
         self.fast_topk = c.get("fast_topk", True)
         # fast top-K loop: queue the next step before walking this one (redone on a miss)
-        self.speculate = c.get("speculative_steps", False)
+        self.speculate = c.get("speculative_steps",
+                               os.environ.get("CS_SPECULATIVE_STEPS", "0") == "1")
         # how a candidate's log-prob is read with a tokenizer that is not merge-free (BPE):
         # "text" (default) = the reference's re-tokenized prompt + statement + token, last
         # log-prob (beam_search.py:358-390), candidates whose re-tokenization differs from
