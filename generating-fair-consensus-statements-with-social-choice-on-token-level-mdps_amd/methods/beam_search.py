@@ -110,6 +110,8 @@ class BeamSearchGenerator(BaseGenerator):
         # fast top-K loop: queue the next step before walking this one (redone on a miss)
         self.speculate = c.get("speculative_steps",
                                os.environ.get("CS_SPECULATIVE_STEPS", "0") == "1")
+        # test hook: treat every n-th step's speculation as a miss (rewind + redo)
+        self._force_miss = int(c.get("speculative_force_miss", 0))
         # how a candidate's log-prob is read with a tokenizer that is not merge-free (BPE):
         # "text" (default) = the reference's re-tokenized prompt + statement + token, last
         # log-prob (beam_search.py:358-390), candidates whose re-tokenization differs from
@@ -459,7 +461,8 @@ class BeamSearchGenerator(BaseGenerator):
                 break
             n = len(new_idx)
             kept = new_idx + [new_idx[0]] * (B - n)
-            if nxt is not None and n == B and new_idx == order_h[:B].tolist():
+            forced = self._force_miss > 0 and step % self._force_miss == 0
+            if nxt is not None and n == B and new_idx == order_h[:B].tolist() and not forced:
                 self.spec_hits += 1               # the queued step is this walk's step
                 pending = nxt
             else:

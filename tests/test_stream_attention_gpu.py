@@ -271,9 +271,9 @@ def test_forward_streams_scoring_chunk_matches_fp32(dev):
     assert e_fus <= 1.5 * e_eag + 1e-2, (e_fus, e_eag)
 
 
-@pytest.mark.parametrize("family,eos_bias", [("llama3", False), ("gemma2", False),
-                                             ("llama3", True)])
-def test_beam_search_fast_topk_equals_host_loop(dev, family, eos_bias):
+@pytest.mark.parametrize("family,force_miss", [("llama3", 0), ("gemma2", 0), ("llama3", 2),
+                                               ("gemma2", 1)])
+def test_beam_search_fast_topk_equals_host_loop(dev, family, force_miss):
     """The fast top-K loop (one graph replay per step ending in cs_beam_decode_step, one
     device->host copy) and the general host loop (cs_vocab_topk + cs_beam_step per step)
     on the SAME fused decode state: identical candidates, min-rewards and kept beams at
@@ -288,12 +288,12 @@ def test_beam_search_fast_topk_equals_host_loop(dev, family, eos_bias):
         ops_ = {"Agent 1": "We should fund public transit.", "Agent 2": "Lower taxes first.",
                 "Agent 3": "Protect the environment above all."}
         cfg = {"beam_width": 3, "max_tokens": 9, "proposer": "topk", "top_k": 6}
-        if eos_bias:
-            # the proposer always offers the EOS token (a +50 logit bias on the reference
-            # rows), so EOS candidates reach the order's top B and the walk completes them
-            # instead of keeping them: the fast loop's speculative steps miss and are redone
-            cfg.update(bias_against_tokens=["<|eot_id|>"], bias_value=50.0)
-        gf = methods.get_method_generator("beam_search", dict(cfg, speculative_steps=True),
+        # speculative steps; force_miss n: every n-th step's speculation is treated as a
+        # miss (rewind + redo with the walk's inputs), as a duplicate or EOS candidate in
+        # the order's top B would make it
+        gf = methods.get_method_generator("beam_search",
+                                          dict(cfg, speculative_steps=True,
+                                               speculative_force_miss=force_miss),
                                           "test/fused-tiny")
         sf = gf.generate_statement("How should the city spend its budget?", ops_)
         gh = methods.get_method_generator("beam_search", dict(cfg, fast_topk=False), "test/fused-tiny")
@@ -301,7 +301,7 @@ def test_beam_search_fast_topk_equals_host_loop(dev, family, eos_bias):
         assert gf.decode_path == "fused-topk" and gh.decode_path == "fused"
         # the fast loop queued steps speculatively (and redid any the walk rejected)
         assert gf.spec_hits + gf.spec_misses > 0
-        if eos_bias:
+        if force_miss:
             assert gf.spec_misses > 0 and len(gf.step_log) > 2
         # the host loop also logs per-agent increments (the BPE log-prob check); compare the
         # fields both paths record
