@@ -109,7 +109,7 @@ class BeamSearchGenerator(BaseGenerator):
         self.fast_topk = c.get("fast_topk", True)
         # fast top-K loop: queue the next step before walking this one (redone on a miss)
         self.speculate = c.get("speculative_steps",
-                               os.environ.get("CS_SPECULATIVE_STEPS", "0") == "1")
+                               os.environ.get("CS_SPECULATIVE_STEPS", "1") != "0")
         # test hook: treat every n-th step's speculation as a miss (rewind + redo)
         self._force_miss = int(c.get("speculative_force_miss", 0))
         # how a candidate's log-prob is read with a tokenizer that is not merge-free (BPE):
