@@ -77,7 +77,6 @@ struct AttnParams {
   const int4* plan;         // nullable: one workgroup per (group, head, query group), no split
   int64_t ldp, ldh;
   int32_t n_grp, n_str, T, H, Hkv, rep, n_qg, n_attn;
-  int32_t n_qg2;            // 128-row query groups (prefix_attn_lds2_kernel)
   float scale, softcap, inv_softcap;
   int32_t window;           // > 0: keys more than window - 1 positions back are masked
   int32_t swizzle;
@@ -599,180 +598,6 @@ void prefix_attn_lds_kernel(AttnParams a) {
   }
 }
 
-// The scoring-chunk kernel with TWO 16-row tiles per wave (128 query rows per workgroup):
-// each staged key block's K and V^T fragments are read from LDS once per wave and used for
-// both tiles, so a block costs half the LDS reads per MFMA of prefix_attn_lds_kernel (which
-// is bound by them: 256 B per lane per block for 16 MFMAs).  Same key-block list, masks and
-// attend_block arithmetic per tile.
-template <int D>
-__global__ __launch_bounds__(kAttnThreads, 2)
-void prefix_attn_lds2_kernel(AttnParams a) {
-  using LT = LdsTile<D>;
-  constexpr int NDS = D / 32;
-  constexpr int NDT = D / 16;
-  constexpr int ROWS = 2 * kGroupRows;                // 128 query rows per workgroup
-  __shared__ __attribute__((aligned(16))) __bf16 buf[2 * LT::ELEMS];
-
-  const int bid = logical_block(a.swizzle);
-  const int qg = bid % a.n_qg2, pg = bid / a.n_qg2;
-  const int gi = pg / a.Hkv, g = pg % a.Hkv;
-  const int p = a.gpfx ? a.gpfx[gi] : gi;
-  const int M = a.n_str * a.T * a.rep;
-  const int r0 = qg * ROWS;
-  const int nrows = min(ROWS, M - r0);
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
-  const int col = lane & 15, h4 = lane >> 4;
-  const int hb = *a.hist_base;
-  const int pl = a.plen[p];
-  const int64_t po = a.poff[p];
-
-  // this lane's query row in each of the wave's two tiles
-  int t_[2], b_[2], hv_[2], kmin_[2], head_[2];
-  int64_t tok_[2];
-  bool vrow_[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = r0 + (2 * w + u) * 16 + col;
-    vrow_[u] = row < M;
-    const int rr = row < M ? row : M - 1;
-    const int jh = rr % a.rep, bt = rr / a.rep;
-    t_[u] = bt % a.T;
-    b_[u] = bt / a.T;
-    tok_[u] = (static_cast<int64_t>(gi) * a.n_str + b_[u]) * a.T + t_[u];
-    head_[u] = g * a.rep + jh;
-    hv_[u] = min(hb + t_[u] + 1, static_cast<int>(a.ldh));
-    kmin_[u] = a.window > 0 ? pl + hb + t_[u] - a.window + 1 : INT32_MIN;
-  }
-  const bool wave_active = r0 + 2 * w * 16 < M;   // wave-uniform: any valid row in its tiles
-
-  const int rw1 = r0 + nrows - 1;
-  const int b_lo = (r0 / a.rep) / a.T, b_hi = (rw1 / a.rep) / a.T;
-  const int t_hi = b_lo == b_hi ? (rw1 / a.rep) % a.T : a.T - 1;
-  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
-  const int nbp = (pl + kKeyBlock - 1) / kKeyBlock;
-  const int n_items = nbp + (b_hi - b_lo + 1) * nbh;
-
-  auto item_src = [&](int it, const __bf16*& ks_, const __bf16*& vs_) {
-    if (it < nbp) {
-      const int64_t k0 = static_cast<int64_t>(g) * a.ldp + po + it * kKeyBlock;
-      ks_ = a.kp + k0 * D;
-      vs_ = a.vtp + k0 * D;
-    } else {
-      const int ih = it - nbp;
-      const int bb = b_lo + ih / nbh;
-      const int64_t sh = (static_cast<int64_t>(gi) * a.n_str + bb) * a.Hkv + g;
-      const int64_t k0 = sh * a.ldh + (ih % nbh) * kKeyBlock;
-      ks_ = a.kh + k0 * D;
-      vs_ = a.vth + k0 * D;
-    }
-  };
-  auto item_mask = [&](int it, int u) {
-    ItemRef r;
-    r.k = nullptr;
-    r.v = nullptr;
-    if (it < nbp) {
-      r.kb = it * kKeyBlock;
-      r.lim = vrow_[u] ? pl : 0;
-      r.pos0 = 0;
-    } else {
-      const int ih = it - nbp;
-      const int bb = b_lo + ih / nbh;
-      r.kb = (ih % nbh) * kKeyBlock;
-      r.lim = (vrow_[u] && bb == b_[u]) ? hv_[u] : 0;
-      r.pos0 = pl;
-    }
-    return r;
-  };
-  u32x4 rk[LT::NCH], rv[LT::NCH];
-  auto fetch = [&](int it) {
-    const __bf16 *ksrc, *vsrc;
-    item_src(it, ksrc, vsrc);
-#pragma unroll
-    for (int j = 0; j < LT::NCH; ++j) {
-      const int c = tid + kAttnThreads * j;
-      rk[j] = *reinterpret_cast<const u32x4*>(ksrc + c * 8);
-      rv[j] = *reinterpret_cast<const u32x4*>(vsrc + c * 8);
-    }
-  };
-  auto stage = [&](int sbuf) {
-    __bf16* kd = buf + sbuf * LT::ELEMS;
-    __bf16* vd = kd + LT::KELEMS;
-#pragma unroll
-    for (int j = 0; j < LT::NCH; ++j) {
-      const int c = tid + kAttnThreads * j;
-      *reinterpret_cast<u32x4*>(kd + (c / (D / 8)) * LT::KROW + (c % (D / 8)) * 8) = rk[j];
-      *reinterpret_cast<u32x4*>(vd + (c >> 2) * LT::VROW + (c & 3) * 8) = rv[j];
-    }
-  };
-
-  bf16x8 qf[2][NDS];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const __bf16* qrow = a.q + (tok_[u] * a.H + head_[u]) * D + 8 * h4;
-#pragma unroll
-    for (int ds = 0; ds < NDS; ++ds) {
-      if (vrow_[u]) {
-        qf[u][ds] = *reinterpret_cast<const bf16x8*>(qrow + ds * 32);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qf[u][ds][e] = static_cast<__bf16>(0.0f);
-      }
-    }
-  }
-  f32x4 o[2][NDT];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) o[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.0f, 0.0f};
-
-  if (n_items > 0) {
-    fetch(0);
-    stage(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < n_items; ++it) {
-    const bool more = it + 1 < n_items;
-    if (more) fetch(it + 1);
-    if (wave_active) {
-      const __bf16* kd = buf + (it & 1) * LT::ELEMS;
-      const __bf16* vd = kd + LT::KELEMS;
-      KeyBlock<D> f;
-#pragma unroll
-      for (int ds = 0; ds < NDS; ++ds) {
-        f.k0[ds] = *reinterpret_cast<const bf16x8*>(kd + col * LT::KROW + ds * 32 + 8 * h4);
-        f.k1[ds] = *reinterpret_cast<const bf16x8*>(kd + (16 + col) * LT::KROW + ds * 32 + 8 * h4);
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        f.vlo[dt] = *reinterpret_cast<const bf16x4*>(vd + (dt * 16 + col) * LT::VROW + 4 * h4);
-        f.vhi[dt] = *reinterpret_cast<const bf16x4*>(vd + (dt * 16 + col) * LT::VROW + 16 + 4 * h4);
-      }
-      attend_block<D>(a, f, item_mask(it, 0), qf[0], kmin_[0], h4, o[0], m[0], l[0]);
-      attend_block<D>(a, f, item_mask(it, 1), qf[1], kmin_[1], h4, o[1], m[1], l[1]);
-    }
-    if (more) stage((it + 1) & 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    float lu = l[u];
-    lu += __shfl_xor(lu, 16, 64);
-    lu += __shfl_xor(lu, 32, 64);
-    if (!vrow_[u]) continue;
-    const float inv = lu > 0.0f ? 1.0f / lu : 0.0f;
-    __bf16* orow = a.out + (tok_[u] * a.H + head_[u]) * D + 4 * h4;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      bf16x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = static_cast<__bf16>(o[u][dt][i] * inv);
-      *reinterpret_cast<bf16x4*>(orow + dt * 16) = v;
-    }
-  }
-}
-
 // Decode steps (a plan: few (group, head) cells, key splits): the agent's PREFIX blocks
 // are shared by the workgroup's four 16-row tiles, so the split's prefix blocks (split,
 // split + n_used, ...) are staged through LDS once per workgroup and attended by every
@@ -1223,11 +1048,6 @@ bool attn_lds() {
   const char* e = getenv("CS_ATTN_LDS");
   return !(e && atoi(e) == 0);
 }
-// scoring chunks: two query tiles per wave (CS_ATTN_LDS2=1; default off until measured)
-bool attn_lds2() {
-  const char* e = getenv("CS_ATTN_LDS2");
-  return e && atoi(e) == 1;
-}
 // decode steps (a plan): the prefix blocks through LDS (CS_ATTN_PLAN_LDS=0: per wave)
 bool attn_plan_lds() {
   const char* e = getenv("CS_ATTN_PLAN_LDS");
@@ -1415,13 +1235,6 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   (void)workspace_bytes;   // sized by cs_prefix_attention_plan for this plan
   const int64_t nwg = plan ? n_attn : base;
   a.swizzle = (!plan && nwg % 8 == 0 && nwg >= 64) ? 1 : 0;
-  // two 16-row tiles per wave for the no-plan launches (CS_ATTN_LDS2=1)
-  const int64_t n_qg2 = (M + 2 * kGroupRows - 1) / (2 * kGroupRows);
-  const int64_t nwg2 = static_cast<int64_t>(n_groups) * Hkv * n_qg2;
-  a.n_qg2 = static_cast<int32_t>(n_qg2);
-  const bool lds2 = !plan && attn_lds2() && D <= 128;
-  if (lds2) a.swizzle = (nwg2 % 8 == 0 && nwg2 >= 64) ? 1 : 0;
-  const dim3 grid2(static_cast<uint32_t>(nwg2));
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<uint32_t>(nwg));
   const dim3 merge_grid(static_cast<uint32_t>(plan ? n_merge : 0));
@@ -1431,8 +1244,6 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
       hipLaunchKernelGGL(prefix_attn_plan_lds_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a); \
     else if (plan)                                                                      \
       hipLaunchKernelGGL((prefix_attn_kernel<DV, true>), grid, dim3(kAttnThreads), 0, st, a); \
-    else if (attn_lds() && lds2)                                                        \
-      hipLaunchKernelGGL(prefix_attn_lds2_kernel<DV>, grid2, dim3(kAttnThreads), 0, st, a); \
     else if (attn_lds())                                                                \
       hipLaunchKernelGGL(prefix_attn_lds_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a); \
     else                                                                                \
