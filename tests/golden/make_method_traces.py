@@ -9,7 +9,8 @@ tests/golden/method_traces.json.  Nothing from the reference is copied: only the
 data its code produced.  The GPU tests replay the same configs through the
 product and compare.
 
-Usage:  python tests/golden/make_method_traces.py [--reference /root/reference] [--family llama3|gemma2]
+Usage:  python tests/golden/make_method_traces.py [--reference /root/reference]
+        [--family llama3|gemma2|c1|bpe|wide]
 """
 from __future__ import annotations
 
@@ -41,7 +42,12 @@ FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
             # API re-tokenizes every appended string, so beam candidates whose text merges
             # with the statement differently than the id-level append are scored on the
             # re-tokenized text by the reference
-            "bpe": ("tiny-llama-bpe-fixture", "method_traces_bpe.json")}
+            "bpe": ("tiny-llama-bpe-fixture", "method_traces_bpe.json"),
+            # wider than the appendix scenario: 16 agents (BASELINE C3's agent count; the
+            # scenario's 4 opinions cycled and tagged per participant, as bench.py's
+            # synthetic_opinions), beam width 8 (the top of the main-body sweep
+            # configs/main_body/scenario_1.yaml beam_width [2, 4, 6, 8]), BoN N = 8, FL bf 3
+            "wide": ("tiny-gemma-wide-fixture", "method_traces_wide.json")}
 BPE_DIR = os.path.join(HERE, "bpe_fixture")
 # untied LM head: with the random tied embedding a shallow model's residual stream makes
 # the last token's own logit ~45 sigma above the rest (every draw repeats it); an
@@ -60,7 +66,7 @@ def fixture_model(family: str = "llama3"):
         tok = T.BPETokenizer(BPE_DIR, family="llama3")
         cfg = Mm.preset("tiny-llama", vocab=tok.vocab_size)
     else:
-        tok = T.CharTokenizer(family)
+        tok = T.CharTokenizer("llama3" if family == "llama3" else "gemma2")
         name = "tiny-llama" if family == "llama3" else "tiny-gemma"
         cfg = Mm.preset(name, vocab=tok.vocab_size)
     model = Mm.Model(cfg, "cpu", torch.float32, seed=WEIGHT_SEED)
@@ -75,6 +81,17 @@ C1_RUNS = [
     ("best_of_n", {"n": 8, "max_tokens": 16, "seed": 7, "temperature": 1.0, "api_delay": 0,
                    "log_level": "WARNING"}),
     ("finite_lookahead", {"branching_factor": 3, "max_depth": 2, "max_tokens": 3, "seed": 11,
+                          "api_delay": 0, "log_level": "WARNING"}),
+]
+
+
+WIDE_AGENTS = 16
+WIDE_RUNS = [
+    ("beam_search", {"beam_width": 8, "max_tokens": 3, "max_sampling_attempts": 8, "seed": 21,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+    ("best_of_n", {"n": 8, "max_tokens": 8, "seed": 17, "temperature": 1.0, "api_delay": 0,
+                   "log_level": "WARNING"}),
+    ("finite_lookahead", {"branching_factor": 3, "max_depth": 2, "max_tokens": 2, "seed": 19,
                           "api_delay": 0, "log_level": "WARNING"}),
 ]
 
@@ -122,6 +139,10 @@ def main() -> None:
     scen = yaml.safe_load(open(os.path.join(args.reference, "configs", "appendix", "llama",
                                             "scenario_1", "beam_search.yaml")))["scenario"]
     issue, opinions = scen["issue"], dict(scen["agent_opinions"])
+    if args.family == "wide":
+        texts = list(opinions.values())
+        opinions = {f"Agent {i + 1}": f"{texts[i % len(texts)]} (participant {i + 1})"
+                    for i in range(WIDE_AGENTS)}
 
     from src import utils as rutils                      # noqa: E402  (reference)
     from src.methods import beam_search, best_of_n, finite_lookahead, mcts  # noqa: E402
@@ -145,14 +166,16 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
-           "family": "llama3" if args.family in ("c1", "bpe") else args.family,
+           "family": ("llama3" if args.family in ("c1", "bpe")
+                      else "gemma2" if args.family == "wide" else args.family),
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
     if args.family == "c1":
         out["preset_overrides"] = dict(C1_OVERRIDES)
         out["tokenizer_vocab"] = cfg.vocab
     if args.family == "bpe":
         out["tokenizer"] = "bpe_fixture"
-    runs = C1_RUNS if args.family == "c1" else BPE_RUNS if args.family == "bpe" else [
+    runs = (C1_RUNS if args.family == "c1" else BPE_RUNS if args.family == "bpe"
+            else WIDE_RUNS if args.family == "wide" else None) or [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,
                        "log_level": "WARNING"}),
         ("finite_lookahead", {"branching_factor": 2, "max_depth": 2, "max_tokens": 6, "seed": 11,
