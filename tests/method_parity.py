@@ -25,12 +25,14 @@ PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-md
 TOL = 1e-3
 
 
-TRACE_FILES = ["method_traces.json", "method_traces_gemma.json", "method_traces_bpe.json"]
+# + 16 agents on the Gemma-2 fixture with beam width 8, BoN N = 8, FL bf 3 (wider than the
+# appendix scenario; ~1 min of the CPU suite)
+TRACE_FILES = ["method_traces.json", "method_traces_gemma.json", "method_traces_bpe.json",
+               "method_traces_wide.json"]
 # BASELINE C1 shape (Llama-3.2-1B widths and vocabulary, 2 layers; beam 4, BoN N = 8, FL
 # bf 3 / depth 2): replayed on the GPU (the CPU emulation of its 128,256-wide LM head
-# over ~700 reference scoring calls is too slow for the CPU suite); and 16 agents on the
-# Gemma-2 fixture with beam width 8, BoN N = 8, FL bf 3 (wider than the appendix scenario)
-GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json", "method_traces_wide.json"]
+# over ~700 reference scoring calls is too slow for the CPU suite)
+GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json"]
 
 
 def load_traces(name: str = "method_traces.json"):
