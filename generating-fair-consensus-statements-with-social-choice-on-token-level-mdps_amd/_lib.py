@@ -27,6 +27,7 @@ EXPORTED = (
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
+    "cs_tree_gather",
 )
 
 
@@ -118,6 +119,8 @@ def load():
     L.cs_gated_act.restype = ctypes.c_int
     L.cs_hist_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, vp]
     L.cs_hist_gather.restype = ctypes.c_int
+    L.cs_tree_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i64, i32, i32, i32, vp]
+    L.cs_tree_gather.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -985,16 +985,16 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void hist_gather_kernel(
     const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
     __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
-    int64_t S, int32_t Hkv, int32_t ldh, int32_t D) {
-  // one workgroup per (layer, stream): all Hkv heads' K rows and V^T tiles, 16-byte
-  // vectors, 8 per thread in flight
+    int64_t S_src, int64_t S, int32_t Hkv, int32_t ldh, int32_t D) {
+  // one workgroup per (layer, destination stream): all Hkv heads' K rows and V^T tiles,
+  // 16-byte vectors, 8 per thread in flight; the source buffer holds S_src streams
   const int64_t ls = blockIdx.x;
   const int64_t l = ls / S, s = ls % S;
   const int hb = min(*hist_base, ldh);
   if (hb <= 0) return;
   const int64_t p = parent[s];
   const int64_t per = static_cast<int64_t>(ldh) * D;                 // elements per (l, s, g)
-  const int64_t so = (l * S + p) * Hkv * per, dn = (l * S + s) * Hkv * per;
+  const int64_t so = (l * S_src + p) * Hkv * per, dn = (l * S + s) * Hkv * per;
   const int kv = hb * D / 8;                                          // K: hb * D contiguous
   const int vv = ((hb + 31) & ~31) * D / 8;                           // V^T: ceil32(hb) slots
   const int pv = static_cast<int>(per / 8);
@@ -1262,24 +1262,41 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   return check_launch("cs_prefix_attention");
 }
 
-int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
-                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S,
-                   int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream) {
-  if (L < 0 || S < 0 || Hkv <= 0 || D <= 0) return fail(CS_ERR_INVALID, "cs_hist_gather: bad shape");
+static int hist_gather_launch(const char* name, const void* src_k, void* dst_k, const void* src_vt,
+                              void* dst_vt, const int64_t* parent, const int32_t* hist_base,
+                              int64_t L, int64_t S_src, int64_t S, int32_t Hkv, int32_t ld_hist,
+                              int32_t D, cs_stream_t stream) {
+  const std::string n(name);
+  if (L < 0 || S < 0 || S_src < 0 || Hkv <= 0 || D <= 0) return fail(CS_ERR_INVALID, n + ": bad shape");
   if (L == 0 || S == 0) return CS_OK;
+  if (S_src == 0) return fail(CS_ERR_INVALID, n + ": no source streams");
   if (!src_k || !dst_k || !src_vt || !dst_vt || !parent || !hist_base)
-    return fail(CS_ERR_INVALID, "cs_hist_gather: NULL pointer");
+    return fail(CS_ERR_INVALID, n + ": NULL pointer");
   if (ld_hist <= 0 || ld_hist % 8 || D % 8)
-    return fail(CS_ERR_INVALID, "cs_hist_gather: ld_hist and D must be positive multiples of 8");
+    return fail(CS_ERR_INVALID, n + ": ld_hist and D must be positive multiples of 8");
   if (src_k == dst_k || src_vt == dst_vt)
-    return fail(CS_ERR_INVALID, "cs_hist_gather: source and destination must differ (ping-pong)");
+    return fail(CS_ERR_INVALID, n + ": source and destination must differ (ping-pong)");
   if (L * S > 0x7fffffffLL || static_cast<int64_t>(Hkv) * ld_hist * D / 8 * 2 > 0x7fffffffLL)
-    return fail(CS_ERR_INVALID, "cs_hist_gather: grid too large");
+    return fail(CS_ERR_INVALID, n + ": grid too large");
   hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), static_cast<const __bf16*>(src_k),
                      static_cast<__bf16*>(dst_k), static_cast<const __bf16*>(src_vt),
-                     static_cast<__bf16*>(dst_vt), parent, hist_base, S, Hkv, ld_hist, D);
-  return check_launch("cs_hist_gather");
+                     static_cast<__bf16*>(dst_vt), parent, hist_base, S_src, S, Hkv, ld_hist, D);
+  return check_launch(name);
+}
+
+int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
+                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S,
+                   int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream) {
+  return hist_gather_launch("cs_hist_gather", src_k, dst_k, src_vt, dst_vt, parent, hist_base, L,
+                            S, S, Hkv, ld_hist, D, stream);
+}
+
+int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
+                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S_src,
+                   int64_t S_dst, int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream) {
+  return hist_gather_launch("cs_tree_gather", src_k, dst_k, src_vt, dst_vt, parent, hist_base, L,
+                            S_src, S_dst, Hkv, ld_hist, D, stream);
 }
 
 int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const int32_t* prefix_len,

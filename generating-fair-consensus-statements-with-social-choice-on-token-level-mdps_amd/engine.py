@@ -19,9 +19,9 @@ Everything after the LM head runs in the HIP kernels (ops.*).
 """
 from __future__ import annotations
 
-import gc
 import os
 import threading
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -718,8 +718,14 @@ class DecodeState:
         self.src, self.tok = self._in_d[:self.S], self._in_d[self.S:]
         self.hidden = cache.last_hidden.repeat_interleave(self.B, dim=0).contiguous()   # [S, d]
         self.use_graphs = use_graphs
+        # captured step graphs keyed by (parity, weak reference to ``post``): a ``post``
+        # closure usually references this state, so a strong key would make a reference
+        # cycle that only the cyclic collector frees -- possibly in the middle of a later
+        # capture, where destroying a graph is refused (and aborts the process)
         self._graphs: dict = {}
         self._pool = None
+        # the attention work plans the captured graphs point into (ops.retain_plans)
+        self._plans: dict = {}
 
     @property
     def n_beams(self) -> int:
@@ -761,27 +767,19 @@ class DecodeState:
 
     def _replay(self, post) -> None:
         dev = self.e.device
-        key = (self.cur, post)
+        key = (self.cur, None if post is None else weakref.ref(post))
         if not self.use_graphs or self.steps == 0:
-            self._body(post)                      # the first step runs eagerly (warm-up)
+            with ops.retain_plans(self._plans):
+                self._body(post)                  # the first step runs eagerly (warm-up)
         else:
             g = self._graphs.get(key)
             if g is None:
                 g = torch.cuda.CUDAGraph()
                 s = torch.cuda.Stream(device=dev)
                 s.wait_stream(torch.cuda.current_stream())
-                # no cyclic garbage collection while capturing: an unreachable DecodeState
-                # of an earlier call freed by the collector mid-capture destroys its graphs,
-                # which HIP refuses during a capture (the destructor then aborts the process)
-                was_enabled = gc.isenabled()
-                gc.disable()
-                try:
-                    with torch.cuda.stream(s):
-                        with torch.cuda.graph(g, pool=self._pool, stream=s):
-                            self._body(post)
-                finally:
-                    if was_enabled:
-                        gc.enable()
+                with torch.cuda.stream(s), ops.retain_plans(self._plans):
+                    with torch.cuda.graph(g, pool=self._pool, stream=s):
+                        self._body(post)
                 torch.cuda.current_stream().wait_stream(s)
                 self._pool = g.pool()
                 self._graphs[key] = g
@@ -814,3 +812,4 @@ class DecodeState:
             torch.cuda.current_stream().synchronize()
         self._graphs.clear()
         self._pool = None
+        self._plans.clear()

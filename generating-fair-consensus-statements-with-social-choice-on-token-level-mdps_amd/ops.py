@@ -10,7 +10,9 @@ Reference semantics each op restates are cited on the op.
 from __future__ import annotations
 
 import collections
+import contextlib
 import ctypes
+import threading
 from typing import Optional, Sequence
 
 import numpy as np
@@ -465,6 +467,29 @@ class AttnPlan:
 
 _attn_plans: "collections.OrderedDict" = collections.OrderedDict()
 _ATTN_PLAN_CACHE = 64
+_plan_sinks = threading.local()
+
+
+@contextlib.contextmanager
+def retain_plans(holder: dict):
+    """Every AttnPlan handed out inside the block is also stored in ``holder`` (keyed by
+    id).  A captured graph keeps the raw device pointers of its plans' entries and
+    workspace; the owner of the graph keeps the plans alive through ``holder`` so that
+    an eviction from the LRU cache above cannot free memory a later replay uses."""
+    stack = getattr(_plan_sinks, "stack", None)
+    if stack is None:
+        stack = _plan_sinks.stack = []
+    stack.append(holder)
+    try:
+        yield holder
+    finally:
+        stack.pop()
+
+
+def _retain(plan: "AttnPlan") -> "AttnPlan":
+    for holder in getattr(_plan_sinks, "stack", ()):
+        holder[id(plan)] = plan
+    return plan
 
 
 def attention_plan(prefix_len_host: Sequence[int], group_prefix_host: Optional[Sequence[int]],
@@ -478,7 +503,7 @@ def attention_plan(prefix_len_host: Sequence[int], group_prefix_host: Optional[S
     plan = _attn_plans.get(key)
     if plan is not None:
         _attn_plans.move_to_end(key)
-        return plan
+        return _retain(plan)
     if torch.cuda.is_current_stream_capturing():
         raise CSError("cs_prefix_attention: the work plan of this shape must be built before "
                       "graph capture (run the step once eagerly)")
@@ -506,7 +531,7 @@ def attention_plan(prefix_len_host: Sequence[int], group_prefix_host: Optional[S
     _attn_plans[key] = plan
     while len(_attn_plans) > _ATTN_PLAN_CACHE:
         _attn_plans.popitem(last=False)
-    return plan
+    return _retain(plan)
 
 
 def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.Tensor,
@@ -572,6 +597,8 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
             if len(lens_h) != n_prefix or (gp_h is not None and len(gp_h) != n_groups):
                 raise CSError("prefix_len_host / group_prefix_host sizes do not match")
         plan = attention_plan(lens_h, gp_h, n_groups, n_str, T, H, Hkv, D, ldh, q.device)
+    else:
+        _retain(plan)
     ws = plan.workspace
     rc = L.cs_prefix_attention(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), Lp,
                                prefix_off.data_ptr(), prefix_len.data_ptr(), mpl,

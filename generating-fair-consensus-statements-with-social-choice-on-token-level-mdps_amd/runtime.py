@@ -163,9 +163,13 @@ def use_gemm_tuning(path: Optional[str] = None) -> Optional[str]:
     """Pick each forward GEMM's hipBLASLt solution from a committed PyTorch TunableOp
     results file (measured on MI355X by tools/tune_gemms.py) instead of the library
     heuristic — read only, no tuning at run time; shapes not in the file keep the heuristic.
-    Returns the file in use (None: not used).  An explicit TunableOp session
-    (PYTORCH_TUNABLEOP_ENABLED in the environment, e.g. while tuning) is left alone;
-    CS_GEMM_TUNING=0 disables, CS_GEMM_TUNING=<file> selects another file."""
+    Returns the file in use (None: not used).
+
+    TunableOp is process-wide (every later matmul of the process, bf16 rounding included,
+    follows the file), so this is OPT-IN: call it (bench.py does), or set CS_GEMM_TUNING=1
+    (the committed file) / CS_GEMM_TUNING=<file> to have ``get_engine`` call it.  An
+    explicit TunableOp session (PYTORCH_TUNABLEOP_ENABLED in the environment, e.g. while
+    tuning) is left alone; CS_GEMM_TUNING=0 disables.  Nothing is written back on exit."""
     global _gemm_tuning, _gemm_tuning_tried
     with _lock:
         if _gemm_tuning_tried and path is None:
@@ -174,6 +178,8 @@ def use_gemm_tuning(path: Optional[str] = None) -> Optional[str]:
         env = os.environ.get("CS_GEMM_TUNING")
         if env == "0" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ or not torch.cuda.is_available():
             return None
+        if env == "1":
+            env = None
         path = path or env or GEMM_TUNING
         if not os.path.exists(path):
             return None
@@ -184,7 +190,9 @@ def use_gemm_tuning(path: Optional[str] = None) -> Optional[str]:
             tunable.enable(True)
             tunable.tuning_enable(False)
             tunable.record_untuned_enable(False)
-            # results are written back at exit to this file, never to the committed one
+            # the committed file is read only: no write-back at exit (and none to it)
+            if hasattr(tunable, "write_file_on_exit"):
+                tunable.write_file_on_exit(False)
             tunable.set_filename(os.path.join(tempfile.gettempdir(), f"cs_tunableop_{os.getpid()}.csv"))
             ok = tunable.read_file(path)
         except Exception as e:   # no usable device / TunableOp unavailable: library heuristic
@@ -195,37 +203,57 @@ def use_gemm_tuning(path: Optional[str] = None) -> Optional[str]:
             tunable.enable(False)
             return None
         _gemm_tuning = path
+        logger.info("GEMM solutions from %s (PyTorch TunableOp, process-wide, read only)", path)
         return path
 
 
+_LOADING: Dict[str, threading.Lock] = {}
+
+
 def get_engine(model_identifier: str) -> Tuple[ScoringEngine, CharTokenizer]:
+    """The engine serving ``model_identifier``; loaded on first use.  A load (minutes for a
+    70B checkpoint) holds only that identifier's loading lock, not the registry lock, so
+    threads working on already-loaded engines are not stalled by it."""
     with _lock:
         if model_identifier in _ENGINES:
             return _ENGINES[model_identifier]
         if not torch.cuda.is_available():
             raise ops.CSError("no HIP device: the scoring engine has no CPU path")
-        path = _model_dir(model_identifier)
-        if path is not None:
-            from .checkpoint import load_engine
-            ent = load_engine(path)
-        elif model_identifier.startswith("random:"):
-            ent = random_engine(model_identifier.split(":", 1)[1])
-        elif os.environ.get("CS_ALLOW_RANDOM_INIT") == "1":
-            name = resolve_preset(model_identifier)
-            logger.warning("model %r: no checkpoint found; using RANDOM-INIT %s weights "
-                           "(CS_ALLOW_RANDOM_INIT=1) -- statements will be meaningless",
-                           model_identifier, name)
-            ent = random_engine(name)
-        else:
-            raise ops.CSError(
-                f"no weights for model {model_identifier!r}: register an engine "
-                "(runtime.register_engine), give a local checkpoint directory (config.json, "
-                "*.safetensors, tokenizer.json) as the id, via runtime.register_model_dir or "
-                "under $CS_MODEL_ROOT, or use 'random:<preset>' for an architecture-exact "
-                "random-init benchmark model")
-        use_gemm_tuning()
-        _ENGINES[model_identifier] = ent
+        ld = _LOADING.setdefault(model_identifier, threading.Lock())
+    with ld:
+        with _lock:
+            if model_identifier in _ENGINES:     # loaded by another thread meanwhile
+                return _ENGINES[model_identifier]
+            path = _model_dir(model_identifier)
+        ent = _load_engine(model_identifier, path)
+        if os.environ.get("CS_GEMM_TUNING", "0") != "0":
+            use_gemm_tuning()
+        with _lock:
+            _ENGINES[model_identifier] = ent
         return ent
+
+
+def _load_engine(model_identifier: str, path: Optional[str]):
+    """Construct the engine of an identifier (no registry lock held)."""
+    if path is not None:
+        from .checkpoint import load_engine
+        ent = load_engine(path)
+    elif model_identifier.startswith("random:"):
+        ent = random_engine(model_identifier.split(":", 1)[1])
+    elif os.environ.get("CS_ALLOW_RANDOM_INIT") == "1":
+        name = resolve_preset(model_identifier)
+        logger.warning("model %r: no checkpoint found; using RANDOM-INIT %s weights "
+                       "(CS_ALLOW_RANDOM_INIT=1) -- statements will be meaningless",
+                       model_identifier, name)
+        ent = random_engine(name)
+    else:
+        raise ops.CSError(
+            f"no weights for model {model_identifier!r}: register an engine "
+            "(runtime.register_engine), give a local checkpoint directory (config.json, "
+            "*.safetensors, tokenizer.json) as the id, via runtime.register_model_dir or "
+            "under $CS_MODEL_ROOT, or use 'random:<preset>' for an architecture-exact "
+            "random-init benchmark model")
+    return ent
 
 
 # --- logit bias -------------------------------------------------------------------

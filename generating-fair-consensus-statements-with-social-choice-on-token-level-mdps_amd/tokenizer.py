@@ -25,9 +25,15 @@ EXTRA_CHARS = ["\u200b", "\u2018", "\u2019", "\u201c", "\u201d", "\u2013", "\u20
 UNK = "\ufffd"
 
 
-# ids past the character table map to single code points from here on (planes 1-4 are
-# outside every text the prompts contain and hold no surrogates), so a full-vocabulary
-# tokenizer stays merge-free: every id is one distinct character
+# ids past the character table map to single code points from here on (no surrogates in
+# planes 1+), so a full-vocabulary tokenizer stays merge-free: every id is one distinct
+# character.  BENCHMARK / FIXTURE USE ONLY: these planes hold real characters (emoji from
+# U+1F300, CJK Ext-B from U+20000), so with vocab_size > the table an opinion containing
+# one encodes to an arbitrary vocabulary id instead of <unk>, and sampled ids decode to such
+# characters.  Only the random-init benchmark engines (runtime.random_engine) and the
+# parity fixtures use a full-vocabulary CharTokenizer; real checkpoints bring their own
+# tokenizer.json (tokenizer.BPETokenizer).  The base is kept because the committed parity
+# traces (tests/golden/method_traces_c1.json) spell their statements in these characters.
 SYNTH_BASE = 0x10000
 
 

@@ -353,6 +353,22 @@ int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
                    int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
 
 /*
+ * cs_tree_gather — cs_hist_gather between buffers of different stream counts: the
+ * source holds S_src streams ([L][S_src][Hkv][ld_hist][D] / V^T tiles), the destination
+ * S_dst; destination stream s receives the filled slots j < *hist_base of source stream
+ * parent[s] (0 <= parent[s] < S_src).  Used level by level for a token tree: the streams of
+ * the nodes with t tokens inherit the K/V of their parent nodes' streams (t - 1 tokens).
+ *
+ * Replaces: every lookahead tree node re-encodes the prompt plus its whole path, once to
+ *   sample its children (src/methods/finite_lookahead.py:297-399 through generate_text) and
+ *   once per agent to score each path (finite_lookahead.py:464-524 through
+ *   src/utils.py:249-259); here a node's K/V is computed once and its children inherit it.
+ */
+int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
+                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S_src,
+                   int64_t S_dst, int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
+
+/*
  * cs_add_rms_norm — residual add + RMSNorm of bf16 rows in one pass:
  *     s = a + b (rounded to bf16; b NULL = none), written to s_out when non-NULL (may alias a)
  *     y = s * rsqrt(mean(s^2) + eps) * g,  g = weight (plus_one = 0, Llama-3) or

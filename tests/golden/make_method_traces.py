@@ -53,6 +53,9 @@ BPE_DIR = os.path.join(HERE, "bpe_fixture")
 # the last token's own logit ~45 sigma above the rest (every draw repeats it); an
 # independent head (std 0.02) gives logits of std ~1 and diverse samples
 C1_OVERRIDES = {"n_layers": 2, "tie_embeddings": False}
+# the 16-agent Gemma-2 fixture with 64-wide heads (the stream attention kernels serve head
+# dims 64 / 128 / 256), so the same trace also pins the bf16 stream-decode path
+WIDE_OVERRIDES = {"head_dim": 64, "query_pre_attn_scalar": 64.0}
 
 
 def fixture_model(family: str = "llama3"):
@@ -68,7 +71,8 @@ def fixture_model(family: str = "llama3"):
     else:
         tok = T.CharTokenizer("llama3" if family == "llama3" else "gemma2")
         name = "tiny-llama" if family == "llama3" else "tiny-gemma"
-        cfg = Mm.preset(name, vocab=tok.vocab_size)
+        cfg = Mm.preset(name, vocab=tok.vocab_size,
+                        **(WIDE_OVERRIDES if family == "wide" else {}))
     model = Mm.Model(cfg, "cpu", torch.float32, seed=WEIGHT_SEED)
     return cfg, model, tok
 
@@ -174,6 +178,8 @@ def main() -> None:
         out["tokenizer_vocab"] = cfg.vocab
     if args.family == "bpe":
         out["tokenizer"] = "bpe_fixture"
+    if args.family == "wide":
+        out["preset_overrides"] = dict(WIDE_OVERRIDES)
     runs = (C1_RUNS if args.family == "c1" else BPE_RUNS if args.family == "bpe"
             else WIDE_RUNS if args.family == "wide" else None) or [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,

@@ -40,7 +40,7 @@ def load_traces(name: str = "method_traces.json"):
         return json.load(f)
 
 
-def register_fixture_engine(traces, device):
+def register_fixture_engine(traces, device, dtype=torch.float32, model_id=None):
     Mm = importlib.import_module(PKG + ".model")
     T = importlib.import_module(PKG + ".tokenizer")
     E = importlib.import_module(PKG + ".engine")
@@ -55,11 +55,34 @@ def register_fixture_engine(traces, device):
     cpu = Mm.Model(cfg, "cpu", torch.float32, seed=traces["weight_seed"])
     if "embed_scale" in traces:          # the C1-shaped fixture (make_method_traces.py)
         cpu.w["embed"].mul_(traces["embed_scale"])
-    w = {k: v.to(device) for k, v in cpu.w.items()}
-    model = Mm.Model(cfg, device, torch.float32, weights=w)
+    # dtype=bfloat16: the same seeded fp32 weights rounded once to bf16 (the shipped path
+    # for bf16 checkpoints: stream kernels, DecodeState, _score_fused)
+    w = {k: v.to(device=device, dtype=dtype) for k, v in cpu.w.items()}
+    model = Mm.Model(cfg, device, dtype, weights=w)
     eng = E.ScoringEngine(model)
-    R.register_engine(traces["model_id"], eng, tok)
+    R.register_engine(model_id or traces["model_id"], eng, tok)
     return eng, tok
+
+
+def beam_reference_steps(traces, run, tok):
+    """The reference's beam search, step by step, rebuilt from its recorded scoring calls
+    (beam_search.py:462-538 calls get_prompt_logprobs for beam, then token, then agent):
+    [step][(candidate text, {agent: last log-prob})] in the reference's insertion order.
+    A candidate of step s is a beam text of s tokens plus one token."""
+    prompts = importlib.import_module(PKG + ".methods.prompts")
+    users = [prompts.BEAM["agent_user"].format(issue=traces["issue"], opinion=op)
+             for op in traces["agent_opinions"].values()]
+    steps = {}
+    for c in run["calls"]:
+        if c["system"] != prompts.BEAM["agent_system"]:
+            continue
+        a = next(i for i, u in enumerate(users) if c["user"].startswith(u))
+        cand = c["user"][len(users[a]):]
+        s = len(tok.encode(cand)) - 1
+        lp = c["tail"][-1] if c["tail"] else -10.0     # beam_search.py:384 fallback
+        step = steps.setdefault(s, {})
+        step.setdefault(cand, {})[a] = lp
+    return [list(steps[s].items()) for s in sorted(steps)], users
 
 
 def run_methods(traces):

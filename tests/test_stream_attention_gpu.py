@@ -399,3 +399,64 @@ def test_hist_gather_copies_filled_slots_of_the_parents(ops, dev, L, S, Hkv, ldh
         nt = (hb + 31) // 32
         ev[:, :, :, :nt] = sv[:, parent][:, :, :, :nt]
     assert torch.equal(dk, ek) and torch.equal(dv, ev)
+
+
+def test_captured_decode_state_is_freed_by_refcount_and_plans_survive_eviction(dev):
+    """A DecodeState whose ``post`` closure references it is freed as soon as its last
+    reference goes (no reference cycle through the graph keys), so the cyclic collector
+    can never destroy its graphs in the middle of a later capture -- checked by running
+    gc.collect() INSIDE the next state's capture.  And a captured graph's attention work
+    plans stay alive when more than the plan cache's 64 other shapes are built between its
+    replays (ops.retain_plans): the replays after the eviction storm still equal an eager
+    run bit for bit."""
+    import gc
+    import weakref
+    E = importlib.import_module(PKG + ".engine")
+    ops = importlib.import_module(PKG + ".ops")
+    eng = _tiny("llama3", dev, seed=13)
+    m = eng.model
+    g = torch.Generator().manual_seed(5)
+    prefixes = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (37, 20, 45)]
+    cache = eng.prefill(prefixes)
+    B = 3
+
+    def run(use_graphs, storm_at=None, collect_in_post=False):
+        st = E.DecodeState(eng, cache, n_prefix=3, n_beams=B, max_steps=10, use_graphs=use_graphs)
+        out = []
+
+        def post():                      # references st: the old cycle's shape
+            st.hidden.mul_(1.0)
+            if collect_in_post:
+                gc.collect()             # inside the capture on the graph steps
+        toks = torch.Generator().manual_seed(6)
+        for step in range(8):
+            if step == storm_at:
+                # > 64 new plan shapes: every cached plan of the state is evicted
+                for n in range(70):
+                    ops.attention_plan([40 + n, 21, 50], None, 3, B, 1, m.cfg.n_heads,
+                                       m.cfg.n_kv_heads, m.cfg.head_dim, 32, dev)
+                torch.cuda.empty_cache()
+                gc.collect()
+            par = [0] * B if step == 0 else [step % B, 0, (step + 1) % B]
+            st.advance(par, torch.randint(5, 500, (B,), generator=toks).tolist(), post=post)
+            out.append(st.hidden.clone())
+        torch.cuda.synchronize()
+        return st, out
+
+    st, _ = run(True)
+    ref = weakref.ref(st)
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        del st
+        assert ref() is None, "a captured DecodeState is only freed by the cyclic collector"
+    finally:
+        if was:
+            gc.enable()
+    # garbage to collect while capturing, then a capture that collects it
+    for _ in range(3):
+        run(True)
+    _, got = run(True, storm_at=4, collect_in_post=True)
+    _, want = run(False)
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
