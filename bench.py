@@ -88,6 +88,11 @@ METHOD_CONFIGS = {
     "c5": dict(preset="llama-3.3-70b", agents=64, beam_width=8, top_k=32, max_tokens=50,
                desc="C5 beam_search: 64 agents, beam 8 x top-32, 50 tokens, Llama-3.3-70B "
                     "(random init, bf16, full replica per GPU)"),
+    # BASELINE configs[3]: finite lookahead, 4-ary depth-4 trees (256 paths per step)
+    "c4": dict(preset="llama-3.1-8b", agents=32, method="finite_lookahead", branching_factor=4,
+               max_depth=4, max_tokens=24, welfare="nash",
+               desc="C4 finite_lookahead: depth 4, branching 4 (256 paths per step) x 32 agents, "
+                    "Nash welfare, Llama-3.1-8B (random init, bf16)"),
 }
 
 # scenario 1 of the reference's appendix configs (configs/appendix/llama/scenario_1/
@@ -164,8 +169,9 @@ def parse():
     ap.add_argument("--e2e", default=1, type=int,
                     help="1: the headline value is the forward-included C2 pass (default); "
                          "0: kernel-only (the headline then reports the kernel leg, labelled)")
-    ap.add_argument("--method", default="c1,c3,c5",
-                    help="method-level beam_search decode configs ('' disables)")
+    ap.add_argument("--method", default="c1,c3,c4,c5",
+                    help="method-level decode configs: beam_search c1/c3/c5, finite_lookahead c4 "
+                         "('' disables)")
     ap.add_argument("--method-text-steps", type=int, default=4,
                     help="steps of a short statement timed with the re-tokenized text semantics")
     ap.add_argument("--method-statements", type=int, default=1,
@@ -422,6 +428,72 @@ def c2_e2e_leg(args, world, rank, dev, prefix_len=200, seed=0):
     return out
 
 
+def method_leg_fl(name, args, world, rank, dev):
+    """BASELINE C4 as the product's finite_lookahead generator on a random-init model
+    (stream path: one prefill per statement, every step's 4-ary depth-4 tree decoded level
+    by level under all agents + the reference prompt, one cs_logsoftmax_gather launch over
+    the agent rows, Nash welfare): decode steps/s with the forward included, and the live
+    roofline of that launch (HIP events around it inside the generator)."""
+    R = importlib.import_module(PKG_DIR + ".runtime")
+    methods = importlib.import_module(PKG_DIR + ".methods")
+    mc = METHOD_CONFIGS[name]
+    t0 = time.perf_counter()
+    eng, tok = R.random_engine(mc["preset"], dev, reuse_caches=0, tokenizer_dir=BPE_FIXTURE)
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    model_id = "random:" + mc["preset"]
+    R.register_engine(model_id, eng, tok)
+    opinions = synthetic_opinions(mc["agents"])
+    # the committed token's id is appended (retokenize "ids", as the beam legs): with
+    # random-init weights most committed tokens are byte fragments whose re-tokenization
+    # merges, and the "text" semantics would re-encode every prompt every step
+    gcfg = {"branching_factor": mc["branching_factor"], "max_depth": mc["max_depth"],
+            "max_tokens": mc["max_tokens"], "seed": 1, "welfare": mc["welfare"],
+            "retokenize": "ids"}
+    warm = methods.get_method_generator("finite_lookahead", dict(gcfg, max_tokens=2), model_id)
+    warm.generate_statement(SCENARIO_ISSUE, opinions)
+    gen = methods.get_method_generator("finite_lookahead", dict(gcfg), model_id)
+    gen._lsg_events = []
+    _barrier_sync(world)
+    t0 = time.perf_counter()
+    gen.generate_statement(SCENARIO_ISSUE, opinions)
+    _barrier_sync(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    st = np.asarray(gen.step_times + [t0 + el])
+    d = np.diff(st)
+    steady = d[1:] if d.size > 2 else d
+    step_s = _max_over_ranks(float(np.median(steady)), world, dev)
+    steps = len(gen.trace)
+    n_paths = float(np.mean([len(t["paths"]) for t in gen.trace])) if gen.trace else 0.0
+    A = mc["agents"]
+    V = eng.model.cfg.vocab
+    ev = gen._lsg_events
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) if ev else None
+    rows = float(np.mean([r for _, _, r in ev])) if ev else 0.0
+    alg = rows * V * 2 + rows * 4 * 4 * 2
+    out = {"workload": mc["desc"], "agents": A, "agents_per_gpu": len(range(rank, A, world)),
+           "branching_factor": mc["branching_factor"], "max_depth": mc["max_depth"],
+           "decode_steps_per_s": 1.0 / step_s, "ms_per_step": step_s * 1e3,
+           "paths_per_step": n_paths, "scorings_per_s": A * n_paths / step_s,
+           "statement_s": el, "steps_per_statement": steps, "model_init_s": init_s,
+           "decode_path": gen.decode_path, "stream_stats": getattr(gen, "stream_stats", None),
+           "timing": "median host step time of the generator's loop (tree of the step: one LM "
+                     "head + reference draws + a forward segment per depth under every prompt; "
+                     "one cs_logsoftmax_gather over the agent rows; welfare; top-1; the "
+                     "committed token's K/V appended to every prompt), max over ranks; "
+                     "statement_s includes the one prefill",
+           "roofline": ({"bound": "hbm", "kernel": "lsg_stream_kernel (cs_logsoftmax_gather over "
+                         "every agent row of the step's tree, 4 targets per row)",
+                         "kernel_ms": k_ms, "rows": rows, "alg_bytes_per_launch": alg,
+                         "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "timing": "HIP events around the launch inside the generator, mean "
+                                   "over the statement's steps"} if k_ms else None)}
+    del eng, gen, warm
+    _free()
+    return out
+
+
 def method_leg(name, args, world, rank, dev):
     """A BASELINE beam configuration as the product's beam_search generator on a random-init
     model: decode steps/s with the forward included (one captured graph replay + one
@@ -430,6 +502,8 @@ def method_leg(name, args, world, rank, dev):
     E = importlib.import_module(PKG_DIR + ".engine")
     methods = importlib.import_module(PKG_DIR + ".methods")
     mc = METHOD_CONFIGS[name]
+    if mc.get("method") == "finite_lookahead":
+        return method_leg_fl(name, args, world, rank, dev)
     t0 = time.perf_counter()
     eng, tok = R.random_engine(mc["preset"], dev, reuse_caches=0, tokenizer_dir=BPE_FIXTURE)
     torch.cuda.synchronize()

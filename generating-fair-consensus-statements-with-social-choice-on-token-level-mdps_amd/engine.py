@@ -176,12 +176,13 @@ class ScoringEngine:
 
     @torch.no_grad()
     def prefill_streams(self, prefixes: Sequence[Sequence[int]], bucket_ratio: float = 1.25,
-                        bucket_tokens: int = 1 << 16) -> StreamPrefix:
+                        bucket_tokens: int = 1 << 16, reserve: int = 0) -> StreamPrefix:
         """Prefill for the stream decode (bf16 models): prompts of very different lengths
         (64 agent prompts of ~200 tokens and a reference prompt listing every opinion)
         are prefilled in length buckets (padding <= bucket_ratio, <= bucket_tokens padded
         tokens per forward) and their K/V written straight into the ragged FusedPrefix
-        buffers — nothing is padded to the longest prompt."""
+        buffers — nothing is padded to the longest prompt.  ``reserve``: key slots left
+        free after every prefix for tokens appended later (append_prefix_tokens)."""
         if any(len(p) == 0 for p in prefixes):
             raise ValueError("every prefix needs at least one token (BOS)")
         m = self.model
@@ -189,7 +190,7 @@ class ScoringEngine:
         dev = self.device
         lens = [len(p) for p in prefixes]
         n = len(prefixes)
-        off = _offsets32(lens)
+        off = _offsets32([x + int(reserve) for x in lens])
         Lp = off[-1]
         ks = [torch.zeros(c.n_kv_heads, Lp, c.head_dim, dtype=m.dtype, device=dev)
               for _ in range(c.n_layers)]
@@ -234,9 +235,48 @@ class ScoringEngine:
         del vrs
         fp = FusedPrefix(k=ks, vt=vts, off=torch.as_tensor(off[:-1], dtype=torch.int64, device=dev),
                          lengths=torch.as_tensor(lens, dtype=torch.int32, device=dev),
-                         max_len=max(lens), lens_host=list(lens))
+                         max_len=max(lens), lens_host=list(lens),
+                         cap_host=[off[i + 1] - off[i] for i in range(n)], off_host=off[:-1])
         return StreamPrefix(fused=fp, last_hidden=last,
                             lengths=torch.as_tensor(lens, dtype=torch.long, device=dev), lens=lens)
+
+    @torch.no_grad()
+    def append_prefix_tokens(self, sp: StreamPrefix, hist_k: torch.Tensor, hist_vt: torch.Tensor,
+                             streams: Sequence[int], slot: int, hidden: torch.Tensor,
+                             which: Optional[Sequence[int]] = None) -> None:
+        """Append one token to prefixes of ``sp`` in place: prefix p (every prefix, or those
+        in ``which``) takes the K/V that stream streams[i] holds in history slot ``slot`` of
+        hist_k [L, S, Hkv, ldh, D] / hist_vt [L, S, Hkv, ldh/32, D, 32] as its next key, and
+        hidden[i] (that stream's final-norm hidden) as its new last hidden.  The token's
+        K/V were computed by the stream forward that scored it, so committing a lookahead
+        token costs copies, not a forward (the reference re-encodes the grown prompt,
+        src/methods/finite_lookahead.py:99-153 via src/utils.py:249-259)."""
+        fp = sp.fused
+        which = list(range(len(sp.lens))) if which is None else list(which)
+        if len(streams) != len(which) or fp.cap_host is None:
+            raise ValueError("append_prefix_tokens needs a prefill_streams prefix and one stream "
+                             "per appended prefix")
+        for p in which:
+            if sp.lens[p] + 1 > fp.cap_host[p]:
+                raise ValueError("prefix capacity exhausted (prefill_streams reserve)")
+        dev = self.device
+        pw = torch.as_tensor(which, dtype=torch.long, device=dev)
+        rows = torch.as_tensor([fp.off_host[p] + sp.lens[p] for p in which], dtype=torch.long,
+                               device=dev)
+        st = torch.as_tensor(list(streams), dtype=torch.long, device=dev)
+        tile, lane = rows // 32, rows % 32
+        for li in range(len(fp.k)):
+            # K [Hkv, Lp, D] <- hist_k[l][s, :, slot, :]; V^T [Hkv, Lp/32, D, 32] column
+            fp.k[li][:, rows, :] = hist_k[li][st, :, slot, :].transpose(0, 1)
+            v = hist_vt[li][st, :, slot // 32, :, slot % 32]                # [n, Hkv, D]
+            fp.vt[li][:, tile, :, lane] = v          # (separated advanced indices: [n, Hkv, D])
+        for p in which:
+            sp.lens[p] += 1
+            fp.lens_host[p] += 1
+        fp.max_len = max(fp.max_len, max(sp.lens[p] for p in which))
+        fp.lengths[pw] += 1
+        sp.lengths[pw] += 1
+        sp.last_hidden[pw] = hidden.to(sp.last_hidden.dtype)
 
     def reset_prefix_store(self) -> None:
         with self._store_lock:
@@ -616,6 +656,8 @@ class FusedPrefix:
     lengths: torch.Tensor       # [n_prefix] int32 (device)
     max_len: int                # host copy of max(lengths)
     lens_host: Optional[List[int]] = None   # host copies of the lengths (or bounds), if known
+    cap_host: Optional[List[int]] = None    # key slots allotted to each prefix (prefill_streams)
+    off_host: Optional[List[int]] = None    # host copy of off
 
 
 @dataclass
@@ -813,3 +855,85 @@ class DecodeState:
         self._graphs.clear()
         self._pool = None
         self._plans.clear()
+
+
+class TokenTree:
+    """One token tree decoded under every prefix of a StreamPrefix on the stream kernels
+    (bf16 models), in SEGMENTS: a segment is a set of m sibling-level nodes forwarded
+    together, each carrying t tokens, whose parents all lie in one earlier segment (or are
+    the prefix itself, t = 1).  A node whose draw hit an end-of-sequence token carries its
+    parent's tokens and is not forwarded: it shares its parent's stream (``hidden`` of the
+    parent's segment and index).
+
+    ``forward(parent_seg, parents, tokens)`` forwards m new nodes: under each of the P
+    prefixes the segment's streams are s = p * m + j (one group of m streams per prefix, ONE
+    forward_streams over all P * m), history slots 0 .. t-2 inherited from the parent
+    streams (cs_tree_gather from the parent segment's buffer), slot t-1 written by the
+    forward.  ``hidden(seg, idx)`` is the final-norm hidden predicting each listed node's
+    children under every prefix ([P, len(idx), d]; seg = -1: the prefix's last position).
+
+    Restates what the reference does per lookahead node and per (path, agent): re-encode
+    the prompt plus the path (src/methods/finite_lookahead.py:297-399, 464-524 through
+    src/utils.py:77-198, 201-281) -- here each node is one token of one stream per prefix,
+    forwarded once."""
+
+    def __init__(self, engine: "ScoringEngine", sp: StreamPrefix, max_depth: int,
+                 pool: Optional[dict] = None):
+        """pool: reusable history buffers by segment number (kept by the caller across the
+        trees of one statement).  Buffers are zero-filled once when allocated: the
+        attention reads whole 32-slot tiles and weights the unfilled slots by 0, so they
+        must hold finite values (a stale earlier tree's K/V are fine, NaN garbage is not)."""
+        self.e = engine
+        self.sp = sp
+        self.P = len(sp.lens)
+        self.ldh = _ceil32(max_depth)
+        self.segs: List[dict] = []       # {t, m, k, vt, hidden}
+        self.pool = {} if pool is None else pool
+
+    def _buffers(self, n_seg: int, S: int):
+        c = self.e.model.cfg
+        dt = self.e.model.dtype
+        per = c.n_layers * S * c.n_kv_heads * self.ldh * c.head_dim
+        ent = self.pool.get(n_seg)
+        if ent is None or ent[0].numel() < per:
+            ent = (torch.zeros(per, dtype=dt, device=self.e.device),
+                   torch.zeros(per, dtype=dt, device=self.e.device))
+            self.pool[n_seg] = ent
+        k = ent[0][:per].view(c.n_layers, S, c.n_kv_heads, self.ldh, c.head_dim)
+        vt = ent[1][:per].view(c.n_layers, S, c.n_kv_heads, self.ldh // 32, c.head_dim, 32)
+        return k, vt
+
+    def forward(self, parent_seg: int, parents: Sequence[int], tokens: Sequence[int]) -> int:
+        """Forward m new nodes whose parents are nodes ``parents`` of segment parent_seg
+        (-1: the prefix); returns the new segment's id."""
+        m_ = self.e.model
+        c = m_.cfg
+        dev = self.e.device
+        P, m = self.P, len(tokens)
+        if m == 0:
+            raise ValueError("a tree segment needs at least one node")
+        t = 1 if parent_seg < 0 else self.segs[parent_seg]["t"] + 1
+        if t > self.ldh:
+            raise ValueError("tree deeper than max_depth")
+        S = P * m
+        k, vt = self._buffers(len(self.segs), S)
+        hb = torch.full((1,), t - 1, dtype=torch.int32, device=dev)
+        if t > 1:
+            prev = self.segs[parent_seg]
+            mp_ = prev["m"]
+            par = torch.as_tensor(list(parents), dtype=torch.long)
+            if par.numel() != m or int(par.min()) < 0 or int(par.max()) >= mp_:
+                raise ValueError("parents must index the parent segment's nodes")
+            src = (torch.arange(P)[:, None] * mp_ + par[None, :]).reshape(-1).to(dev)
+            ops.tree_gather(prev["k"], k, prev["vt"], vt, src, hb)
+        tok = torch.as_tensor(list(tokens), dtype=torch.long).repeat(P).to(dev)
+        h = m_.forward_streams(tok, self.sp.fused, list(k.unbind(0)), list(vt.unbind(0)), hb, m, 1)
+        self.segs.append({"t": t, "m": m, "k": k, "vt": vt, "hidden": h.view(P, m, -1)})
+        return len(self.segs) - 1
+
+    def hidden(self, seg: int, idx: Sequence[int]) -> torch.Tensor:
+        """[P, len(idx), d]: the hidden predicting the children of nodes idx of ``seg``."""
+        if seg < 0:
+            return self.sp.last_hidden[:, None, :].expand(self.P, len(idx), -1)
+        ii = torch.as_tensor(list(idx), dtype=torch.long, device=self.e.device)
+        return self.segs[seg]["hidden"][:, ii]

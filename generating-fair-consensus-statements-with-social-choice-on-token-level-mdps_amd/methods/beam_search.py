@@ -224,12 +224,12 @@ class BeamSearchGenerator(BaseGenerator):
         merge_free = getattr(tok, "merge_free", True) or self.retokenize == "ids"
         self._merge_free = merge_free
         self.text_compat_candidates = 0
-        if fused and self.proposer == "topk" and shard.world == 1 and self.fast_topk and merge_free:
-            self.decode_path = "fused-topk"
+        if fused and self.proposer == "topk" and self.fast_topk and merge_free:
+            self.decode_path = "fused-topk" if shard.world == 1 else "fused-topk-sharded"
             ds = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
                              max_steps=int(self.max_tokens))
             try:
-                completed, beams = self._loop_fused_topk(engine, tok, ds, A_loc, bias)
+                completed, beams = self._loop_fused_topk(engine, tok, ds, A_loc, bias, shard)
             finally:
                 ds.release()
         else:
@@ -372,15 +372,20 @@ class BeamSearchGenerator(BaseGenerator):
         self.text_compat_candidates += len(bad)
         return U, W, order
 
-    def _loop_fused_topk(self, engine, tok, st: DecodeState, A: int, bias):
-        """Top-K proposer on one rank: after the host walk a decode step is ONE graph
-        replay ending in cs_beam_decode_step; one device->host copy per step."""
+    def _loop_fused_topk(self, engine, tok, st: DecodeState, A: int, bias, shard=None):
+        """Top-K proposer: after the host walk a decode step is one graph replay ending in
+        cs_beam_decode_step on one rank; with the agents sharded over ranks it is the
+        step graph (advance + LM head + cs_vocab_topk), rank 0's proposals broadcast, a
+        scoring graph (cs_beam_step, no order), the MIN all-reduce of the welfare and a
+        selection graph (cs_beam_select: stable order of every candidate) -- the two
+        exchanges on the stream between graph replays.  One device->host copy per step."""
         dev = engine.device
         m = engine.model
         B, K = st.B, int(self.top_k)
         C = B * K
         if K > m.cfg.vocab:
             raise ValueError("top_k exceeds the vocabulary")
+        sharded = shard is not None and shard.world > 1
         bias_t = torch.as_tensor(bias, dtype=torch.long, device=dev) if bias else None
         bias_v = float(self.bias_value)
         U_buf = torch.empty(A, C, dtype=torch.float32, device=dev)
@@ -391,39 +396,124 @@ class BeamSearchGenerator(BaseGenerator):
         ids_buf = torch.empty(B, K, dtype=torch.int32, device=dev)
         order_buf = torch.empty(C, dtype=torch.int32, device=dev)
         ws = ops.Workspace(zeroed=True)
-        # every output the host reads is a persistent buffer: the two captured step graphs
+        # every output the host reads is a persistent buffer: the captured step graphs
         # (ping-pong parities) must write to the same storage
-
-        def score():
-            logits = m.lm_head(st.hidden)                                # [(A + 1) * B, V]
-            ref = logits[A * B:]
-            if bias_t is not None:
-                ref.index_add_(1, bias_t, torch.full((B, bias_t.numel()), bias_v, dtype=ref.dtype,
-                                                     device=dev))
-            ops.beam_decode_step(ref, logits[:A * B], rewards, K, "min", n_order=C,
-                                 softcap=engine.softcap, workspace=ws, out_U=U_buf, out_W=W_buf,
-                                 out_ids=ids_buf, out_order=order_buf)
-
         P = st.P
         p_base = torch.arange(P, device=dev)[:, None] * B
 
-        def post():
-            torch.index_select(U_buf, 1, kidx, out=rewards)
-            score()
-            if spec:
-                # the next step's inputs as the walk will most often choose them: the B best
-                # candidates of this step's order (no duplicate text or EOS among them);
-                # the host overwrites them whenever its walk differs
-                k_s = order_buf[:B].long()
-                kidx.copy_(k_s)
-                st.src.copy_((p_base + torch.div(k_s, K, rounding_mode="floor")[None, :]).reshape(-1))
-                st.tok.copy_(ids_buf.view(-1)[k_s].repeat(P))
+        def spec_inputs():
+            # the next step's inputs as the walk will most often choose them: the B best
+            # candidates of this step's order (no duplicate text or EOS among them); the
+            # host overwrites them whenever its walk differs
+            k_s = order_buf[:B].long()
+            kidx.copy_(k_s)
+            st.src.copy_((p_base + torch.div(k_s, K, rounding_mode="floor")[None, :]).reshape(-1))
+            st.tok.copy_(ids_buf.view(-1)[k_s].repeat(P))
+
+        if not sharded:
+            def score():
+                logits = m.lm_head(st.hidden)                                # [(A + 1) * B, V]
+                ref = logits[A * B:]
+                if bias_t is not None:
+                    ref.index_add_(1, bias_t, torch.full((B, bias_t.numel()), bias_v,
+                                                         dtype=ref.dtype, device=dev))
+                ops.beam_decode_step(ref, logits[:A * B], rewards, K, "min", n_order=C,
+                                     softcap=engine.softcap, workspace=ws, out_U=U_buf,
+                                     out_W=W_buf, out_ids=ids_buf, out_order=order_buf)
+
+            def post():
+                torch.index_select(U_buf, 1, kidx, out=rewards)
+                score()
+                if spec:
+                    spec_inputs()
+
+            def first_step():
+                score()
+
+            def launch(host=None):
+                if host is None:
+                    st.advance_device(post=post)
+                else:
+                    st.advance(*host, post=post)
+        else:
+            comm = parallel.StepComm(shard)
+            V = m.cfg.vocab
+            lg_buf = torch.empty(P * B, V, dtype=m.dtype, device=dev)
+            ws_p = ops.Workspace()
+            Wx = torch.empty(C, dtype=torch.float32, device=dev)
+            graphs = {}
+
+            def propose():                     # in the step graph: LM head + proposer
+                m.lm_head(st.hidden, out=lg_buf)
+                ref = lg_buf[A * B:]
+                if bias_t is not None:
+                    ref.index_add_(1, bias_t, torch.full((B, bias_t.numel()), bias_v,
+                                                         dtype=ref.dtype, device=dev))
+                ids, _ = ops.vocab_topk(ref, K, softcap=engine.softcap, workspace=ws_p)
+                ids_buf.copy_(ids)
+
+            def post():
+                torch.index_select(U_buf, 1, kidx, out=rewards)
+                propose()
+
+            def score_w():                     # this rank's agents, no order
+                if A:
+                    ops.beam_step(lg_buf[:A * B], ids_buf, rewards, "min", n_order=0,
+                                  softcap=engine.softcap, workspace=ws, out_U=U_buf, out_W=Wx)
+                    # a column with no usable utility here must not win the MIN all-reduce
+                    Wx.nan_to_num_(nan=float("inf"))
+                else:
+                    Wx.fill_(float("inf"))
+
+            def select():                      # after the all-reduce: the stable order
+                if C <= 1024:
+                    order, _ = ops.beam_select(Wx, C, unfill="min", W_out=W_buf)
+                else:
+                    W_buf.copy_(torch.where(torch.isinf(Wx) & (Wx > 0),
+                                            torch.full_like(Wx, float("nan")), Wx))
+                    order, _ = ops.topk(W_buf, C, with_values=False)
+                order_buf.copy_(order)
+                if spec:
+                    spec_inputs()
+
+            def replay(name, fn):
+                g = graphs.get(name)
+                if g is None and st.use_graphs and st.steps >= 2:
+                    g = torch.cuda.CUDAGraph()
+                    cs = torch.cuda.Stream(device=dev)
+                    cs.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(cs):
+                        with torch.cuda.graph(g, stream=cs):
+                            fn()
+                    torch.cuda.current_stream().wait_stream(cs)
+                    graphs[name] = g
+                if g is None:
+                    fn()                       # warm-up steps run eagerly
+                else:
+                    g.replay()
+
+            def exchange_and_select():
+                comm.bcast0(ids_buf)           # rank 0's proposals on every rank
+                replay("score", score_w)
+                comm.min_(Wx)                  # welfare over every agent
+                replay("select", select)
+
+            def first_step():
+                propose()
+                exchange_and_select()
+
+            def launch(host=None):
+                if host is None:
+                    st.advance_device(post=post)
+                else:
+                    st.advance(*host, post=post)
+                exchange_and_select()
 
         # speculative steps: the next step is queued from the device-side order before the
         # host has walked this one, and redone (rewind + host inputs) when the walk differs
         spec = bool(self.speculate) and st.use_graphs
         self.spec_hits = self.spec_misses = 0
-        score()                                   # step 0 (eager): every beam = the prefix
+        first_step()                              # step 0 (eager): every beam = the prefix
         hosts = (_HostCopy(), _HostCopy())
         pending = hosts[0].start(ids_buf, order_buf, W_buf, U_buf)
         nxt = None                                # the queued speculative step's results
@@ -433,10 +523,10 @@ class BeamSearchGenerator(BaseGenerator):
         for step in range(self.max_tokens):
             self.steps_run += 1
             # queue step + 1 now when this step's beams will most likely be its B best
-            # candidates (every beam live; post() has written the inputs); the GPU runs it
-            # while the host walks this step
+            # candidates (every beam live; the inputs are written on the device); the GPU
+            # runs it while the host walks this step
             if spec and step >= 1 and n_live == B and step + 1 < self.max_tokens:
-                st.advance_device(post=post)
+                launch()
                 nxt = hosts[(step + 1) & 1].start(ids_buf, order_buf, W_buf, U_buf)
             else:
                 nxt = None
@@ -473,7 +563,7 @@ class BeamSearchGenerator(BaseGenerator):
                     U_buf.copy_(pending.outs[3], non_blocking=True)
                 kidx_h.numpy()[:] = kept    # its last copy finished before this step's results
                 kidx.copy_(kidx_h, non_blocking=True)
-                st.advance([i // K for i in kept], [int(ids_f[i]) for i in kept], post=post)
+                launch(([i // K for i in kept], [int(ids_f[i]) for i in kept]))
                 pending = hosts[(step + 1) & 1].start(ids_buf, order_buf, W_buf, U_buf)
             n_live = n
         return completed, beams

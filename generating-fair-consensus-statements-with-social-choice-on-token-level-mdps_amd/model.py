@@ -355,8 +355,10 @@ class Model:
             new.append((k, v))
         return self._rms(h, self.w["norm"]), new
 
-    def lm_head(self, h: torch.Tensor) -> torch.Tensor:
+    def lm_head(self, h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         W = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
+        if out is not None:
+            return torch.matmul(h.to(W.dtype), W.t(), out=out)
         return h.to(W.dtype) @ W.t()
 
     # --- stream forward over shared prefixes (HIP attention) ----------------------

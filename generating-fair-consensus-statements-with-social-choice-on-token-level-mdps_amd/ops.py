@@ -714,6 +714,32 @@ def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
     _lib.check(rc, "cs_hist_gather")
 
 
+def tree_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
+                dst_vt: torch.Tensor, parent: torch.Tensor, hist_base: torch.Tensor) -> None:
+    """dst[l][s] = src[l][parent[s]] over the filled history slots between buffers of
+    different stream counts (cs_tree_gather): K [L, S_src|S_dst, Hkv, ldh, D], V^T
+    [L, S_src|S_dst, Hkv, ldh/32, D, 32] bf16, parent [S_dst] int64 in [0, S_src)."""
+    L_ = _lib.load()
+    if src_k.dim() != 5 or dst_k.dim() != 5:
+        raise CSError("history buffers must be [L, S, Hkv, ldh, D]")
+    Ln, Ss, Hkv, ldh, D = src_k.shape
+    Sd = dst_k.shape[1]
+    if tuple(dst_k.shape) != (Ln, Sd, Hkv, ldh, D) or \
+            tuple(src_vt.shape) != (Ln, Ss, Hkv, ldh // 32, D, 32) or \
+            tuple(dst_vt.shape) != (Ln, Sd, Hkv, ldh // 32, D, 32):
+        raise CSError("tree_gather: K / V^T history layouts do not match")
+    for t in (src_k, dst_k, src_vt, dst_vt):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise CSError("history buffers must be contiguous bfloat16")
+    if parent.dtype != torch.int64 or parent.numel() != Sd or hist_base.dtype != torch.int32:
+        raise CSError("parent must be int64 [S_dst], hist_base int32 [1]")
+    _require_cuda(src_k, dst_k, src_vt, dst_vt, parent, hist_base)
+    rc = L_.cs_tree_gather(src_k.data_ptr(), dst_k.data_ptr(), src_vt.data_ptr(), dst_vt.data_ptr(),
+                           parent.data_ptr(), hist_base.data_ptr(), Ln, Ss, Sd, Hkv, ldh, D,
+                           _stream())
+    _lib.check(rc, "cs_tree_gather")
+
+
 def blocked_vt(v: torch.Tensor) -> torch.Tensor:
     """V rows [..., keys, D] (keys a multiple of 32) -> the kernels' V^T in 32-key tiles
     [..., keys/32, D, 32] (contiguous)."""

@@ -77,6 +77,16 @@ def same_on_all_ranks(obj, shard: AgentShard, group: Optional[dist.ProcessGroup]
     return box[0]
 
 
+def broadcast_from_rank0(t: torch.Tensor, shard: AgentShard,
+                         group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Rank 0's tensor on every rank, in place (e.g. the token ids rank 0 drew for a
+    lookahead level: the replicated reference-policy rows of different ranks are computed
+    in GEMMs of different shapes, so their bf16 roundings -- and draws -- may differ)."""
+    if shard.world > 1:
+        dist.broadcast(t, src=0, group=group)
+    return t
+
+
 def any_rank(flags: torch.Tensor, shard: AgentShard,
              group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """Element-wise OR of a bool tensor over the ranks (all_reduce MAX); identity on one rank."""
@@ -159,6 +169,8 @@ class RcclComm:
                                        ctypes.c_int]
         L.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.ncclBroadcast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.ncclCommDestroy.argtypes = [ctypes.c_void_p]
         L.ncclGetErrorString.restype = ctypes.c_char_p
         L.ncclGetErrorString.argtypes = [ctypes.c_int]
@@ -189,7 +201,51 @@ class RcclComm:
                                           self._DTYPES[t.dtype], op, self._comm, st),
                     "ncclAllReduce")
 
+    def broadcast(self, t: torch.Tensor, root: int = 0, stream: Optional[torch.cuda.Stream] = None):
+        """In-place broadcast of the contiguous device tensor ``t`` from ``root``."""
+        if not t.is_contiguous() or t.dtype not in self._DTYPES:
+            raise ValueError("RcclComm.broadcast: need a contiguous f32/f64/i32/i64 tensor")
+        st = (stream or torch.cuda.current_stream(t.device)).cuda_stream
+        self._check(self._L.ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(),
+                                          self._DTYPES[t.dtype], root, self._comm, st),
+                    "ncclBroadcast")
+
     def close(self):
         if self._comm:
             self._L.ncclCommDestroy(self._comm)
             self._comm = ctypes.c_void_p()
+
+
+class StepComm:
+    """The two per-step exchanges of an agent-sharded decode loop, on the current stream:
+    ``min_(W)`` (all-reduce MIN of the per-candidate welfare) and ``bcast0(ids)`` (rank 0's
+    proposals).  Over RCCL (the default process group's backend is nccl) they go through
+    one process-wide direct communicator (RcclComm: a few us of host time per call; built
+    once, CS_DIRECT_RCCL=0 disables), otherwise through the ProcessGroup (gloo rehearsals)."""
+
+    _direct: Optional[RcclComm] = None
+
+    def __init__(self, shard: AgentShard):
+        self.shard = shard
+        self.comm = None
+        if (shard.world > 1 and dist.get_backend() == "nccl"
+                and os.environ.get("CS_DIRECT_RCCL", "1") != "0"):
+            if StepComm._direct is None or StepComm._direct.world != shard.world:
+                StepComm._direct = RcclComm()
+            self.comm = StepComm._direct
+
+    def min_(self, t: torch.Tensor) -> None:
+        if self.shard.world == 1:
+            return
+        if self.comm is not None:
+            self.comm.all_reduce(t, RcclComm.MIN)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+
+    def bcast0(self, t: torch.Tensor) -> None:
+        if self.shard.world == 1:
+            return
+        if self.comm is not None:
+            self.comm.broadcast(t, 0)
+        else:
+            dist.broadcast(t, src=0)

@@ -460,3 +460,55 @@ def test_captured_decode_state_is_freed_by_refcount_and_plans_survive_eviction(d
     _, want = run(False)
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("L,Ss,Sd,Hkv,ldh,D,hb", [(2, 5, 12, 2, 32, 64, 3), (3, 33, 132, 8, 32, 128, 1),
+                                                 (1, 7, 2, 4, 64, 256, 40), (2, 4, 9, 1, 32, 64, 0)])
+def test_tree_gather_copies_parent_streams_between_levels(ops, dev, L, Ss, Sd, Hkv, ldh, D, hb):
+    """cs_tree_gather: dst[l][s] = src[l][parent[s]] (filled slots) with source and
+    destination buffers of different stream counts (one lookahead tree level to the next)."""
+    g = torch.Generator(device="cpu").manual_seed(L * 1000 + Ss * 10 + Sd + hb)
+    bf = torch.bfloat16
+    sk = torch.randn(L, Ss, Hkv, ldh, D, generator=g).to(bf).to(dev)
+    sv = torch.randn(L, Ss, Hkv, ldh // 32, D, 32, generator=g).to(bf).to(dev)
+    dk = torch.full((L, Sd, Hkv, ldh, D), 7.0, dtype=bf, device=dev)
+    dv = torch.full((L, Sd, Hkv, ldh // 32, D, 32), 7.0, dtype=bf, device=dev)
+    parent = torch.randint(0, Ss, (Sd,), generator=g).to(dev)
+    ops.tree_gather(sk, dk, sv, dv, parent, torch.tensor([hb], dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    ek, ev = torch.full_like(dk, 7.0), torch.full_like(dv, 7.0)
+    if hb > 0:
+        ek[:, :, :, :hb] = sk[:, parent][:, :, :, :hb]
+        nt = (hb + 31) // 32
+        ev[:, :, :, :nt] = sv[:, parent][:, :, :, :nt]
+    assert torch.equal(dk, ek) and torch.equal(dv, ev)
+
+
+def test_append_prefix_tokens_equals_prefill_of_the_longer_prompts(dev):
+    """engine.append_prefix_tokens (a token's K/V copied from the stream that forwarded it
+    into the ragged prefix buffers) then a TokenTree level == the same level over a fresh
+    prefill_streams of the prompts with the token appended (bf16 rounding of differently
+    batched forwards)."""
+    E = importlib.import_module(PKG + ".engine")
+    eng = _tiny("llama3", dev, seed=21)
+    g = torch.Generator().manual_seed(6)
+    prompts = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (31, 64, 17)]
+    sp = eng.prefill_streams(prompts, reserve=3)
+    tree = E.TokenTree(eng, sp, 2)
+    toks = [77, 301, 12]
+    seg = tree.forward(-1, [0, 0, 0], toks)
+    sg = tree.segs[seg]
+    j = 1                                           # commit token 301
+    eng.append_prefix_tokens(sp, sg["k"], sg["vt"], [p * 3 + j for p in range(3)], 0,
+                             sg["hidden"][:, j])
+    assert sp.lens == [32, 65, 18]
+    sp2 = eng.prefill_streams([p + [toks[j]] for p in prompts])
+    torch.testing.assert_close(sp.last_hidden.float(), sp2.last_hidden.float(), atol=5e-2, rtol=5e-2)
+    nxt = [5, 9, 400, 33]
+    t1 = E.TokenTree(eng, sp, 1)
+    t2 = E.TokenTree(eng, sp2, 1)
+    h1 = t1.segs[t1.forward(-1, [0] * 4, nxt)]["hidden"]
+    h2 = t2.segs[t2.forward(-1, [0] * 4, nxt)]["hidden"]
+    tgt = torch.randint(0, 512, (12, 6), generator=g).to(dev).to(torch.int32)
+    d = (eng.rows_logprobs(h1.reshape(12, -1), tgt) - eng.rows_logprobs(h2.reshape(12, -1), tgt)).abs().max()
+    assert float(d) < 5e-2
