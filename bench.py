@@ -639,53 +639,87 @@ def _host_cores():
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
 
 
-def cpu_baseline(seconds, V=128_256, T=150):
-    """The reference's scoring path restated on the host cores.
-
-    Headline (`value`): the reference scores every (agent, candidate) with a
-    get_prompt_logprobs call that re-encodes the whole prompt (src/utils.py:249-259): here
-    one CPU forward of prompt + candidate through Llama-3.2-1B in fp32 (BASELINE configs[0]:
-    "Llama-3.2-1B logprobs on CPU"), log-softmax over the vocabulary at every candidate
-    position and the gather, per scoring, on all host cores.  Also reported: the fp64 C
-    oracle (the scoring arithmetic after the LM head) and torch.log_softmax + gather on a
-    C2 logits sample, both on the same cores."""
-    M = importlib.import_module(PKG_DIR + ".model")
-    cores = _host_cores()
-    torch.set_num_threads(cores)
-    out = {"unit": "scorings/s", "cores": cores, "kind": "port"}
-    # (1) forward-included per-call scoring, 1B fp32
-    cfg = M.preset("llama-3.2-1b")
-    t0 = time.perf_counter()
-    # constant-filled fp32 weights of the exact shapes: a CPU forward's time does not
-    # depend on the values, and filling is seconds where sampling 1.2 G normals is minutes
+def _const_model(M, name):
+    """An architecture-exact fp32 CPU model with constant weights: a CPU forward's time does
+    not depend on the values, and filling is seconds where sampling normals is minutes."""
+    cfg = M.preset(name)
     model = M.Model.__new__(M.Model)
     model.cfg = cfg
     w = {n: torch.full(shp, 1.0 if "norm" in n else 0.01, dtype=torch.float32)
          for n, shp in model.shapes().items()}
-    model = M.Model(cfg, "cpu", torch.float32, weights=w)
-    init_s = time.perf_counter() - t0
-    g = torch.Generator().manual_seed(3)
-    P, Tc = 200, 10
+    return M.Model(cfg, "cpu", torch.float32, weights=w)
+
+
+def _per_call_scoring(model, P, Tc, seconds, seed=3, min_calls=1):
+    """The reference's scoring primitive restated on the host: every (agent, candidate)
+    scoring is one forward of the whole prompt + candidate (get_prompt_logprobs re-encodes
+    every call, src/utils.py:249-259), then log-softmax over the vocabulary and the gather at
+    the candidate tokens.  Returns (calls, seconds)."""
+    cfg = model.cfg
+    g = torch.Generator().manual_seed(seed)
     n, t0 = 0, time.perf_counter()
     with torch.no_grad():
         while True:
             ids = torch.randint(300, cfg.vocab, (1, P + Tc), generator=g)
-            kv, h, _ = model.prefill(ids, torch.tensor([P + Tc]))
+            _, h, _ = model.prefill(ids, torch.tensor([P + Tc]))
             lg = model.lm_head(h[0, P - 1:P + Tc - 1]).float()
             lp = torch.log_softmax(lg, dim=-1).gather(1, ids[0, P:P + Tc, None])
             float(lp.mean())
             n += 1
             el = time.perf_counter() - t0
-            if el >= seconds:
-                break
+            if el >= seconds and n >= min_calls:
+                return n, el
+
+
+def _np_log_softmax_rows(M):
+    """core.log_softmax_rows (core.py:64-68) restated in NumPy fp64: M - max - log sum exp."""
+    mx = M.max(axis=1, keepdims=True)
+    Z = M - mx
+    return Z - np.log(np.exp(Z).sum(axis=1, keepdims=True))
+
+
+def cpu_baseline(seconds, V=128_256, T=150):
+    """The reference's scoring path restated on the host cores (kind "port").
+
+    ``value`` (BASELINE C2's config): Llama-3.1-8B fp32, one forward of a 200-token agent
+    prompt + a 150-token candidate per (agent, candidate) scoring, as get_prompt_logprobs
+    re-encodes the prompt every call, log-softmax + gather at the candidate's tokens -- the
+    same workload the GPU headline (`value`) scores, on all host cores.  Also: the same per
+    call at BASELINE C1's model (Llama-3.2-1B fp32, 200 + 10 tokens; C1 names "Llama-3.2-1B
+    logprobs on CPU"), and the post-LM-head arithmetic on a C2 logits sample three ways: the
+    fp64 C oracle, core.log_softmax_rows restated in NumPy fp64 (single thread), and
+    torch.log_softmax(x.float()).gather."""
+    M = importlib.import_module(PKG_DIR + ".model")
+    cores = _host_cores()
+    torch.set_num_threads(cores)
+    out = {"unit": "scorings/s", "cores": cores, "kind": "port"}
+    # (1) C2 config: 8B fp32, 200-token prompt + 150-token candidate per call
+    t0 = time.perf_counter()
+    model = _const_model(M, "llama-3.1-8b")
+    init_s = time.perf_counter() - t0
+    n, el = _per_call_scoring(model, 200, T, seconds, min_calls=2)
     out["value"] = n / el
-    out["sample"] = (f"{n} scorings in {el:.1f} s: Llama-3.2-1B fp32 (constant weights) forward of a "
-                     f"{P}-token prompt + {Tc}-token candidate, log-softmax over {cfg.vocab} + "
-                     f"gather at the candidate tokens, per (agent, candidate) as "
-                     f"get_prompt_logprobs re-encodes every call; torch {cores} threads "
-                     f"(model init {init_s:.1f} s, not timed)")
+    out["sample"] = (f"{n} scorings in {el:.1f} s: Llama-3.1-8B fp32 (constant weights) forward of a "
+                     f"200-token agent prompt + {T}-token candidate (BASELINE C2's shape), "
+                     f"log-softmax over {V} + gather at the candidate's tokens, per (agent, "
+                     f"candidate) as get_prompt_logprobs re-encodes every call; torch {cores} "
+                     f"threads (model init {init_s:.1f} s, not timed)")
     del model
-    # (2) the post-LM-head arithmetic: fp64 C oracle and torch fp32, C2 rows
+    import gc
+    gc.collect()
+    # (2) C1 config: 1B fp32, 200 + 10 tokens per call
+    t0 = time.perf_counter()
+    model = _const_model(M, "llama-3.2-1b")
+    init_s = time.perf_counter() - t0
+    n, el = _per_call_scoring(model, 200, 10, seconds / 2)
+    out["c1_per_call"] = {
+        "value": n / el, "unit": "scorings/s",
+        "sample": f"{n} scorings in {el:.1f} s: Llama-3.2-1B fp32 (constant weights) forward of a "
+                  f"200-token prompt + 10-token candidate, log-softmax + gather, per call; torch "
+                  f"{cores} threads (model init {init_s:.1f} s, not timed)"}
+    del model
+    gc.collect()
+    # (3) the post-LM-head arithmetic on C2 rows
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc
     orc.set_threads(cores)
@@ -704,20 +738,38 @@ def cpu_baseline(seconds, V=128_256, T=150):
         orc.topk(orc.welfare(U, orc.MIN), 1)
         iters += 1
         el = time.perf_counter() - t0
-        if el >= seconds / 2:
+        if el >= seconds / 4:
             break
     out["oracle_post_lm_head"] = {"value": a_s * n_s * iters / el, "unit": "scorings/s",
                                   "sample": f"{a_s} agents x {n_s} candidates x T={T} rows of "
                                             f"V={V} bf16, oracle/cs_oracle.c fp64, {iters} passes"}
-    xt = torch.from_numpy(x32).to(torch.bfloat16)
-    tt = torch.from_numpy(tgt.astype(np.int64))
+    # core.log_softmax_rows (NumPy fp64) + gather + the reference's per-candidate mean / min
+    xb = torch.from_numpy(x32).to(torch.bfloat16)
+    x64 = xb.double().numpy()
+    tg = tgt[:, 0].astype(np.int64)
     iters, t0 = 0, time.perf_counter()
     while True:
-        lp = torch.log_softmax(xt.float(), dim=-1).gather(1, tt)
+        ls = _np_log_softmax_rows(x64)
+        lp = ls[np.arange(rows), tg]
+        U = lp.reshape(a_s, n_s, T).mean(axis=2)
+        int(np.argmax(U.min(axis=0)))
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds / 4:
+            break
+    out["numpy_fp64_log_softmax_rows"] = {
+        "value": a_s * n_s * iters / el, "unit": "scorings/s",
+        "gb_per_s": rows * V * 2 * iters / el / 1e9,
+        "sample": f"core.log_softmax_rows (core.py:64-68) restated in NumPy fp64 + gather + mean "
+                  f"+ min + argmax on [{rows}, {V}] (bf16 values), {iters} passes, NumPy threads"}
+    iters, t0 = 0, time.perf_counter()
+    tt = torch.from_numpy(tgt.astype(np.int64))
+    while True:
+        lp = torch.log_softmax(xb.float(), dim=-1).gather(1, tt)
         float(lp.sum())
         iters += 1
         el = time.perf_counter() - t0
-        if el >= seconds / 2:
+        if el >= seconds / 4:
             break
     out["torch_log_softmax_gather"] = {
         "value": a_s * n_s * iters / el, "unit": "scorings/s",
@@ -1033,7 +1085,12 @@ def main():
             "decode_steps_per_s": 1000.0 / ms,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            # same-config pair: C2 forward-included scorings/s on the GPU over the same
+            # workload's per-call scorings/s on the host cores (cpu_baseline.value, 8B fp32)
+            "vs_baseline": (value / cpu["value"]) if (cpu and cpu.get("value") and e2e is not None)
+            else None,
+            "vs_baseline_is": "value / cpu_baseline.value (BASELINE C2 config on this box's host "
+                              "cores; BASELINE.md publishes no number for this metric)",
             "dtype": "bf16",
             "data": "synthetic (random-init weights of the named architectures, synthetic token "
                     "ids / scenario-1 prompt texts)",
@@ -1051,6 +1108,8 @@ def main():
         if e2e is not None:
             line["end_to_end"] = e2e
         if method:
+            if cpu and cpu.get("c1_per_call") and "c1" in method:
+                method["c1"]["vs_cpu"] = method["c1"]["scorings_per_s"] / cpu["c1_per_call"]["value"]
             line["method_decode"] = method
         if beam:
             line["beam_kernel"] = beam

@@ -56,6 +56,7 @@ constexpr int kMaxSplit = 32;       // key splits of one (group, head, query gro
 constexpr int kPlanMinBase = 1024;  // from this many (group, head, query group) workgroups on,
                                     // the chip is full without key splits: no plan
 constexpr int kMergeRows = 8;       // query rows per merge workgroup (2 per wave)
+constexpr int64_t kPlanImbalance = 4;   // ... or from a longest cell 4x the mean on (T = 1)
 constexpr int kTargetWgsDefault = 512;    // plan: split cells until about this many workgroups
 constexpr int kMinItemsDefault = 3;       // ... but never below this many key blocks per wave
 
@@ -982,6 +983,13 @@ __global__ __launch_bounds__(256) void v_tile_place_kernel(RopeParams r, int32_t
 // stream), 16-byte vectors; the unfilled capacity is never moved.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
+// 16-byte unit j of a head's filled V^T region -> its offset in the head's [tiles][D][4] units
+__device__ __forceinline__ int vt_unit(int j, int full_units, int ur) {
+  if (j < full_units) return j;
+  const int r = j - full_units;
+  return full_units + (r / ur) * 4 + (r % ur);
+}
+
 __global__ __launch_bounds__(256) void hist_gather_kernel(
     const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
     __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
@@ -996,7 +1004,11 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
   const int64_t per = static_cast<int64_t>(ldh) * D;                 // elements per (l, s, g)
   const int64_t so = (l * S_src + p) * Hkv * per, dn = (l * S + s) * Hkv * per;
   const int kv = hb * D / 8;                                          // K: hb * D contiguous
-  const int vv = ((hb + 31) & ~31) * D / 8;                           // V^T: ceil32(hb) slots
+  // V^T [ldh/32][D][32]: the full 32-slot tiles below hb whole, then in the last tile only
+  // the 16-byte units (8 slots) of each row that hold slots < hb (the rest of a row is
+  // weighted 0 by the attention and keeps the destination's earlier finite contents)
+  const int v_full = (hb / 32) * D * 4, v_ur = ((hb & 31) + 7) / 8;
+  const int vv = v_full + D * v_ur;
   const int pv = static_cast<int>(per / 8);
   const u32x4_t* sk = reinterpret_cast<const u32x4_t*>(src_k + so);
   const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(src_v + so);
@@ -1014,7 +1026,7 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
         x[u] = sk[g * pv + j];
       } else if (i < n) {
         const int iv = i - nk, g = iv / vv, j = iv - g * vv;
-        x[u] = sv[g * pv + j];
+        x[u] = sv[g * pv + vt_unit(j, v_full, v_ur)];
       }
     }
 #pragma unroll
@@ -1025,7 +1037,7 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
         dk[g * pv + j] = x[u];
       } else if (i < n) {
         const int iv = i - nk, g = iv / vv, j = iv - g * vv;
-        dv[g * pv + j] = x[u];
+        dv[g * pv + vt_unit(j, v_full, v_ur)] = x[u];
       }
     }
   }
@@ -1084,7 +1096,11 @@ int64_t cs_prefix_attention_plan(const int32_t* prefix_len, int32_t n_prefix,
   const int64_t M = static_cast<int64_t>(n_str) * T * rep;
   const int64_t n_qg = (M + kGroupRows - 1) / kGroupRows;
   const int64_t base = static_cast<int64_t>(n_groups) * Hkv * n_qg;
-  if (base >= kPlanMinBase) return 0;   // enough workgroups without key splits
+  // enough workgroups without key splits -- unless (single-token streams) some cells are
+  // far longer than the rest: a lookahead tree level whose reference prompt lists every
+  // opinion (thousands of keys) beside ~250-key agent prompts makes the reference cells
+  // the launch's long pole (cells checked below)
+  if (base >= kPlanMinBase && T > 1) return 0;
   const int64_t nbh_max = ld_hist / kKeyBlock;
   // every cell's key blocks per query tile (an upper bound: history at capacity)
   struct Cell { int32_t gi, qg; int64_t items, kw, nrows; };
@@ -1108,6 +1124,14 @@ int64_t cs_prefix_attention_plan(const int32_t* prefix_len, int32_t n_prefix,
       }
       cl.push_back({gi, static_cast<int32_t>(qg), items, kw, nrows});
     }
+  }
+  if (base >= kPlanMinBase) {
+    int64_t sum = 0, mx = 0;
+    for (const Cell& c : cl) {
+      sum += c.items;
+      mx = std::max(mx, c.items);
+    }
+    if (mx * static_cast<int64_t>(cl.size()) <= kPlanImbalance * sum) return 0;
   }
   // one per-wave budget q for all cells (a cell of `items` blocks on kw waves takes
   // ceil(items / (q kw)) splits, at most kMaxSplit): the whole launch's wave-serial work

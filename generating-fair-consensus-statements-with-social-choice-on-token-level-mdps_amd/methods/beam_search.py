@@ -121,6 +121,11 @@ class BeamSearchGenerator(BaseGenerator):
         if self.retokenize not in ("text", "ids"):
             raise ValueError("retokenize must be 'text' or 'ids'")
         self.text_compat_candidates = 0
+        self.text_rows_candidates = 0
+        # text path on the stream state: candidates whose re-tokenization changes only their
+        # last token are scored from rows the decode already has (False: every unstable
+        # candidate re-encoded as the reference's whole prompt)
+        self.text_incremental = c.get("text_incremental", True)
         self.step_log: List[dict] = []
         self.decode_path = None
         self.steps_run = 0
@@ -224,6 +229,7 @@ class BeamSearchGenerator(BaseGenerator):
         merge_free = getattr(tok, "merge_free", True) or self.retokenize == "ids"
         self._merge_free = merge_free
         self.text_compat_candidates = 0
+        self.text_rows_candidates = 0
         if fused and self.proposer == "topk" and self.fast_topk and merge_free:
             self.decode_path = "fused-topk" if shard.world == 1 else "fused-topk-sharded"
             ds = DecodeState(engine, cache, n_prefix=A_loc + 1, n_beams=int(self.beam_width),
@@ -256,6 +262,12 @@ class BeamSearchGenerator(BaseGenerator):
         beam_ids: List[List[int]] = [[]]           # each beam's token ids as the streams hold them
         rewards = torch.zeros(A_loc, st.n_beams, dtype=torch.float32, device=dev)   # per beam
         completed: List[Tuple[str, List[float]]] = []
+        # the re-tokenized text path on the stream state: every step's final hidden of every
+        # stream and each beam's ancestry, so a candidate whose re-tokenization only changes
+        # its last token is scored from the row of the context it keeps (no forward)
+        inc = None
+        if (not self._merge_free and isinstance(st, _LiveBeams) and self.text_incremental):
+            inc = {"h0": st.st.hidden.clone(), "hid_log": [], "anc": [[]], "B": st.n_beams}
         for step in range(self.max_tokens):
             if not beams:
                 break
@@ -310,7 +322,7 @@ class BeamSearchGenerator(BaseGenerator):
             tstr = [tok.token_str(v) for v in ct]
             if not self._merge_free:
                 U, W, order = self._text_compat_patch(engine, tok, U, W, order, rewards, cb, ct,
-                                                      tstr, beams, beam_ids, shard)
+                                                      tstr, beams, beam_ids, shard, inc)
             Uh = U.double().cpu().numpy()
             new_beams, new_idx = self._walk(order, lambda i: beams[cb[i]][0] + tstr[i],
                                             lambda i: tstr[i], lambda i: Uh[:, i].tolist(),
@@ -329,10 +341,13 @@ class BeamSearchGenerator(BaseGenerator):
                 st.advance([cb[i] for i in new_idx], [ct[i] for i in new_idx])
                 keep = new_idx + [new_idx[0]] * (st.n_beams - len(new_idx))   # padded beams
                 rewards = U[:, torch.as_tensor(keep, device=dev)].contiguous()
+                if inc is not None:
+                    inc["hid_log"].append(st.st.hidden.clone())
+                    inc["anc"] = [inc["anc"][cb[i]] + [j] for j, i in enumerate(new_idx)]
         return completed, beams
 
     def _text_compat_patch(self, engine, tok, U, W, order, rewards, cb, ct, tstr, beams,
-                           beam_ids, shard):
+                           beam_ids, shard, inc=None):
         """Tokenizers that are not merge-free (BPE): the reference scores a candidate as the
         last log-prob of the re-tokenized ``agent_user + statement + token``
         (_get_agent_token_logprob, beam_search.py:335-404 via get_prompt_logprobs).  The
@@ -359,18 +374,82 @@ class BeamSearchGenerator(BaseGenerator):
         if not bad:
             return U, W, order
         A_loc = U.shape[0]
-        users = [self._agent_users[a] + beams[cb[i]][0] + tstr[i] for a in range(A_loc) for i in bad]
-        lps = utils.text_compat_last(engine, tok, [BEAM["agent_system"]] * len(users), users)
         dev = U.device
-        bi = torch.as_tensor(bad, dtype=torch.long, device=dev)
-        par = torch.as_tensor([cb[i] for i in bad], dtype=torch.long, device=dev)
-        lp = torch.as_tensor(lps, dtype=torch.float32, device=dev).view(A_loc, len(bad))
         U = U.clone()
-        U[:, bi] = rewards[:, par] + lp
+        self.text_compat_candidates += len(bad)
+        rest = bad
+        if inc is not None and A_loc:
+            rest = self._text_rows(engine, U, rewards, cb, encs, nt, tail_ids, apis, texts,
+                                   beam_ids, bad, inc)
+        if rest:
+            users = [self._agent_users[a] + beams[cb[i]][0] + tstr[i] for a in range(A_loc)
+                     for i in rest]
+            lps = utils.text_compat_last(engine, tok, [BEAM["agent_system"]] * len(users), users)
+            bi = torch.as_tensor(rest, dtype=torch.long, device=dev)
+            par = torch.as_tensor([cb[i] for i in rest], dtype=torch.long, device=dev)
+            lp = torch.as_tensor(lps, dtype=torch.float32, device=dev).view(A_loc, len(rest))
+            U[:, bi] = rewards[:, par] + lp
         W = parallel.combine_welfare(U, "min", shard)
         order = ops.topk(W, U.shape[1])[0].cpu().tolist()
-        self.text_compat_candidates += len(bad)
         return U, W, order
+
+    def _text_rows(self, engine, U, rewards, cb, encs, nt, tail_ids, apis, texts, beam_ids,
+                   bad, inc):
+        """The text path's common case without any forward: when the re-tokenized user text
+        keeps the first j ids of the beam and then ends in ONE token t (a merge of the
+        appended token into the last ones: " the" + "ir" -> " their"), the reference's
+        last log-prob is log p(t | agent prompt + beam ids[:j]) -- a row the stream decode
+        already computed (the prefix's last hidden for j = 0, else the hidden the beam's
+        ancestor stream had after its j-th token).  All such candidates of a step share
+        one LM head over their distinct (agent, beam, j) rows and one
+        cs_logsoftmax_gather.  Returns the candidates left for the full text path
+        (re-tokenizations that change two or more tokens, marker texts)."""
+        dev = U.device
+        A_loc = U.shape[0]
+        B = inc["B"]
+        groups, rest = {}, []
+        for i in bad:
+            enc = encs[i]
+            if apis[i] != texts[i] or enc[:nt] != tail_ids:
+                rest.append(i)
+                continue
+            suf, bid = enc[nt:], beam_ids[cb[i]]
+            j = 0
+            n = min(len(suf), len(bid))
+            while j < n and suf[j] == bid[j]:
+                j += 1
+            if len(suf) - j != 1:
+                rest.append(i)
+                continue
+            groups.setdefault((cb[i], j), []).append((i, suf[-1]))
+        if not groups:
+            return rest
+        keys = list(groups)
+        rows = []
+        for b, j in keys:
+            if j == 0:
+                src, sidx = inc["h0"], [a * B for a in range(A_loc)]
+            else:
+                src = inc["hid_log"][j - 1]
+                sidx = [a * B + inc["anc"][b][j - 1] for a in range(A_loc)]
+            rows.append(src[torch.as_tensor(sidx, dtype=torch.long, device=dev)])   # [A_loc, d]
+        H = torch.stack(rows, dim=1).reshape(A_loc * len(keys), -1)            # row a, key g
+        kmax = max(len(v) for v in groups.values())
+        tgt = torch.full((len(keys), kmax), -1, dtype=torch.int32)
+        for g, key in enumerate(keys):
+            tgt[g, :len(groups[key])] = torch.as_tensor([t for _, t in groups[key]], dtype=torch.int32)
+        lp = engine.rows_logprobs(H, tgt.to(dev).repeat(A_loc, 1)).view(A_loc, len(keys), kmax)
+        cand, par, col = [], [], []
+        for g, key in enumerate(keys):
+            for k, (i, _t) in enumerate(groups[key]):
+                cand.append(i)
+                par.append(key[0])
+                col.append(g * kmax + k)
+        ci = torch.as_tensor(cand, dtype=torch.long, device=dev)
+        U[:, ci] = rewards[:, torch.as_tensor(par, dtype=torch.long, device=dev)] + \
+            lp.reshape(A_loc, -1)[:, torch.as_tensor(col, dtype=torch.long, device=dev)]
+        self.text_rows_candidates += len(cand)
+        return rest
 
     def _loop_fused_topk(self, engine, tok, st: DecodeState, A: int, bias, shard=None):
         """Top-K proposer: after the host walk a decode step is one graph replay ending in

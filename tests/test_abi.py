@@ -133,6 +133,8 @@ def _plan(L, lens, gmap, n_str, T, H, Hkv, D, ldh):
     ([600] + [210] * 4, None, 4, 1, 32, 8, 64, 64),         # C1 decode
     ([3000, 700], [1, 0, 1], 4, 1, 32, 8, 64, 96),          # group -> prefix map
     ([0], [0, 0], 1, 300, 32, 8, 128, 320),                 # prompts as streams: no prefix
+    ([4100] + [250] * 32, None, 64, 1, 32, 8, 128, 32),     # C4 tree level 3: >= 1024 cells,
+                                                            # the reference cells 16x longer
 ])
 def test_prefix_attention_plan_covers_every_cell(pkg, shape):
     """cs_prefix_attention_plan (host): every (group, head, query group) cell is covered by
@@ -147,6 +149,7 @@ def test_prefix_attention_plan_covers_every_cell(pkg, shape):
     n_qg = -(-M // 64)
     if plan is None:                      # enough cells without splits
         assert total == 0 and n_groups * Hkv * n_qg >= 1024 or total == 0
+        assert lens[0] <= 4 * max(lens[-1], 1) or T > 1, "imbalanced cells need a plan"
         return
     assert total == na + nm and nm > 0
     att, mer = plan[:na], plan[na:]

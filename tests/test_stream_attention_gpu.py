@@ -66,6 +66,9 @@ CASES = [
     (3, 8, 1, 16, 8, 256, [500, 64, 250], 30, 50.0, None, 100),        # window, decode shape
     (5, 8, 1, 64, 8, 128, [2000, 100, 90, 210, 150], 25, 0.0, None),   # C5 mix: long ref prompt
     (2, 4, 1, 32, 8, 64, [3000, 700], 60, 0.0, [1, 0]),                # long prefixes, mapped
+    # C4 lookahead tree level: >= 1024 cells, the reference prompt 16x the agents' (a plan
+    # with key splits for the imbalanced cells)
+    (33, 64, 1, 32, 8, 128, [4100] + [250 + 3 * i for i in range(32)], 2, 0.0, None),
 ]
 
 
@@ -380,10 +383,11 @@ def test_gated_act_matches_torch(ops, dev, act):
 
 
 @pytest.mark.parametrize("L,S,Hkv,ldh,D,hb", [(2, 5, 2, 32, 64, 7), (3, 16, 8, 64, 256, 33),
-                                             (1, 4, 8, 96, 128, 96), (2, 3, 1, 32, 64, 0)])
+                                             (1, 4, 8, 96, 128, 96), (2, 3, 1, 32, 64, 0),
+                                             (2, 6, 4, 64, 128, 41), (1, 3, 2, 64, 64, 64)])
 def test_hist_gather_copies_filled_slots_of_the_parents(ops, dev, L, S, Hkv, ldh, D, hb):
     """cs_hist_gather: dst[l][s] = src[l][parent[s]] for the filled slots (K rows j < hb,
-    V^T tiles up to ceil32(hb)); the rest of dst is left as it was."""
+    V^T slots j < ceil8(hb)); the rest of dst is left as it was."""
     g = torch.Generator(device="cpu").manual_seed(L * 100 + S + hb)
     bf = torch.bfloat16
     sk = torch.randn(L, S, Hkv, ldh, D, generator=g).to(bf).to(dev)
@@ -393,12 +397,7 @@ def test_hist_gather_copies_filled_slots_of_the_parents(ops, dev, L, S, Hkv, ldh
     parent = torch.randint(0, S, (S,), generator=g).to(dev)
     ops.hist_gather(sk, dk, sv, dv, parent, torch.tensor([hb], dtype=torch.int32, device=dev))
     torch.cuda.synchronize()
-    ek, ev = torch.full_like(sk, 7.0), torch.full_like(sv, 7.0)
-    if hb > 0:
-        ek[:, :, :, :hb] = sk[:, parent][:, :, :, :hb]
-        nt = (hb + 31) // 32
-        ev[:, :, :, :nt] = sv[:, parent][:, :, :, :nt]
-    assert torch.equal(dk, ek) and torch.equal(dv, ev)
+    _check_gathered(sk, sv, dk, dv, parent, hb, ldh)
 
 
 def test_captured_decode_state_is_freed_by_refcount_and_plans_survive_eviction(dev):
@@ -476,12 +475,20 @@ def test_tree_gather_copies_parent_streams_between_levels(ops, dev, L, Ss, Sd, H
     parent = torch.randint(0, Ss, (Sd,), generator=g).to(dev)
     ops.tree_gather(sk, dk, sv, dv, parent, torch.tensor([hb], dtype=torch.int32, device=dev))
     torch.cuda.synchronize()
-    ek, ev = torch.full_like(dk, 7.0), torch.full_like(dv, 7.0)
+    _check_gathered(sk, sv, dk, dv, parent, hb, ldh)
+
+
+def _check_gathered(sk, sv, dk, dv, parent, hb, ldh):
+    """K rows j < hb and V^T slots j < ceil8(hb) are the parent's; K rows from hb and V^T
+    slots from ceil8(hb) on are untouched (7.0)."""
+    ek = torch.full_like(dk, 7.0)
     if hb > 0:
         ek[:, :, :, :hb] = sk[:, parent][:, :, :, :hb]
-        nt = (hb + 31) // 32
-        ev[:, :, :, :nt] = sv[:, parent][:, :, :, :nt]
-    assert torch.equal(dk, ek) and torch.equal(dv, ev)
+    assert torch.equal(dk, ek)
+    slot = torch.arange(ldh, device=dv.device).view(ldh // 32, 1, 32)     # [tile, 1, lane]
+    copied = slot < ((hb + 7) // 8) * 8
+    want = torch.where(copied, sv[:, parent], torch.full_like(dv, 7.0))
+    assert torch.equal(dv, want)
 
 
 def test_append_prefix_tokens_equals_prefill_of_the_longer_prompts(dev):

@@ -1,0 +1,70 @@
+"""The re-tokenized text path of beam search (the product default, retokenize "text") on the
+stream decode state, with a tokenizer that is not merge-free (the byte-level BPE fixture):
+
+the incremental scoring (candidates whose re-tokenization changes only their last token
+read the row the decode already has for the context they keep) against the full text path
+(every unstable (agent, candidate) prompt re-encoded, the reference's per-call semantics,
+src/methods/beam_search.py:335-404 through src/utils.py:201-373) on the same bf16 model:
+the same candidates at every step, per-agent increments within the bf16 tolerance, and the
+same kept beams wherever no near tie decides."""
+import importlib
+import os
+
+import pytest
+import torch
+
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+TOL = 5e-2
+
+
+def _engine(dev, family):
+    M = importlib.import_module(PKG + ".model")
+    E = importlib.import_module(PKG + ".engine")
+    T = importlib.import_module(PKG + ".tokenizer")
+    if family == "llama3":
+        cfg = M.preset("tiny-llama", vocab=4096, d_model=256, n_heads=8, n_kv_heads=2, head_dim=64,
+                       d_ff=512, n_layers=3, init_std=0.05)
+    else:
+        cfg = M.preset("tiny-gemma", vocab=4096, d_model=256, n_heads=4, n_kv_heads=2,
+                       head_dim=128, d_ff=512, n_layers=3, sliding_window=4096,
+                       query_pre_attn_scalar=128.0, init_std=0.05)
+    model = M.Model(cfg, dev, torch.bfloat16, seed=5)
+    tok = T.BPETokenizer(os.path.join(HERE, "golden", "bpe_fixture"), family, vocab_size=cfg.vocab,
+                         use_config=family == "llama3")
+    return E.ScoringEngine(model, reuse_caches=0), tok
+
+
+@pytest.mark.parametrize("family", ["llama3", "gemma2"])
+def test_incremental_text_path_matches_full_text_path(dev, family):
+    R = importlib.import_module(PKG + ".runtime")
+    methods = importlib.import_module(PKG + ".methods")
+    eng, tok = _engine(dev, family)
+    R.register_engine("test/text-path", eng, tok)
+    opinions = {"Agent 1": "Genetic data is private and must stay with the person.",
+                "Agent 2": "Sharing genes helps research cure illnesses.",
+                "Agent 3": "Families should decide together about genetic tests."}
+    issue = "Should a person's genetic code be considered private information?"
+    try:
+        logs, gens = [], []
+        for incremental in (True, False):
+            g = methods.get_method_generator("beam_search", {
+                "beam_width": 3, "max_tokens": 6, "max_sampling_attempts": 5, "seed": 3,
+                "text_incremental": incremental}, "test/text-path")
+            g.generate_statement(issue, opinions)
+            assert g.decode_path == "fused"
+            logs.append(g.step_log)
+            gens.append(g)
+        gi, gf = gens
+        assert gi.text_rows_candidates > 0, "no candidate took the incremental rows"
+        assert gi.text_compat_candidates == gf.text_compat_candidates
+        for k, (a, b) in enumerate(zip(*logs)):
+            assert a["candidates"] == b["candidates"], k
+            d = max(abs(x - y) for ra, rb in zip(a["increments"], b["increments"])
+                    for x, y in zip(ra, rb))
+            assert d <= TOL, (k, d)
+            if a["kept"] != b["kept"]:
+                break                    # a near tie (within TOL) decided differently
+    finally:
+        R.clear_engines()
