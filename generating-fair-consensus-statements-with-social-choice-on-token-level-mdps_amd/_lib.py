@@ -27,7 +27,7 @@ EXPORTED = (
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
-    "cs_tree_gather",
+    "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits",
 )
 
 
@@ -121,6 +121,11 @@ def load():
     L.cs_hist_gather.restype = ctypes.c_int
     L.cs_tree_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i64, i32, i32, i32, vp]
     L.cs_tree_gather.restype = ctypes.c_int
+    L.cs_gemm_bf16.argtypes = [vp, i64, vp, i64, vp, i64, i64, i64, i64, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_int, vp, vp]
+    L.cs_gemm_bf16.restype = ctypes.c_int
+    L.cs_gemm_splits.argtypes = [i64, i64, i64, ctypes.c_int]
+    L.cs_gemm_splits.restype = i64
     _lib = L
     return L
 

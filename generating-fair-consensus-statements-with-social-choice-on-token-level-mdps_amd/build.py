@@ -1,6 +1,6 @@
 """In-tree build of the gfx950 HIP library (no JIT cache: the .so travels with the repo).
 
-Six translation units (csrc/*.hip, sharing csrc/cs_kernels.cuh) compile in parallel to
+Seven translation units (csrc/*.hip, sharing csrc/cs_kernels.cuh) compile in parallel to
 objects, then link into libconsensus_scoring.so."""
 from __future__ import annotations
 
@@ -12,7 +12,7 @@ from concurrent.futures import ThreadPoolExecutor
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
 _CSRC = os.path.join(_HERE, "csrc")
-SOURCES = [os.path.join(_CSRC, n) for n in ("stream.hip", "fold.hip", "proposer.hip", "beam.hip", "attn.hip", "norm.hip")]
+SOURCES = [os.path.join(_CSRC, n) for n in ("stream.hip", "fold.hip", "proposer.hip", "beam.hip", "attn.hip", "norm.hip", "gemm.hip")]
 HEADERS = [os.path.join(_CSRC, "cs_kernels.cuh"), os.path.join(_REPO, "include", "consensus_scoring.h")]
 OUT = os.path.join(_HERE, "libconsensus_scoring.so")
 ARCH = os.environ.get("CS_OFFLOAD_ARCH", "gfx950")

@@ -1,0 +1,346 @@
+// gemm.hip — the projection GEMMs of a decode step, Y[M, N] = X[M, K] · W[N, K]^T in bf16
+// with fp32 accumulation, for the row counts a step has (M = agents x beams + reference
+// rows: C1 20, C3 272, C5 520): too many rows for a GEMV, too few for a square tile.
+//
+// What it replaces: the remote forward behind every get_prompt_logprobs call
+// (src/utils.py:249-259) re-encodes each (agent, candidate) text; here one step of all
+// (agent, beam) streams runs the weights of every layer once, so the layer's time is a
+// weight stream (C3: 397 MB per layer) with M MACs per weight element — balanced between
+// HBM (8 TB/s) and MFMA (2.5 PF dense) at M ~ 272.
+//
+// ws_gemm_kernel<MW>: one workgroup (8 waves: 2 row groups x 4 column groups) owns 128
+// output features x 32*MW rows (all of a step's rows up to 288) over a K range:
+//   * W (the streamed operand, read from HBM exactly once per row block) goes straight
+//     from global memory into MFMA A-fragments (16 B per lane, 16 rows x 64 B per wave
+//     instruction), a three-stage register ring per 64-deep K step;
+//   * X (L2-resident: 2-8 MB, re-read by every column tile) is staged through LDS in
+//     three buffers by plain 16-byte loads + ds_write_b128, 128-B rows with a 16-B chunk
+//     XOR swizzle (chunk ^ (row >> 1) & 7) so the B-fragment ds_read_b128 of 16 rows is
+//     bank-conflict free;
+//   * v_mfma_f32_16x16x32_bf16 computes the transposed tile D[n][m] (A = W rows, B = X^T):
+//     each lane ends with 4 consecutive features of one row -> one 8-byte store.
+// Split-K (grid splits x column tiles) writes fp32 partials [split][M][N], folded in split
+// order by splitk_reduce_kernel: the result does not depend on scheduling.  The gated
+// variant (GATED = 1) pairs gate feature f with up feature F + f in the same wave and
+// writes act(gate) * up (the rounding of cs_gated_act) instead of both halves.
+#include "cs_kernels.cuh"
+
+namespace {
+
+typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+typedef float gf32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t gu32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t gu16x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t gu16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kGemmThreads = 512;   // 8 waves: 2 row groups x 4 column groups
+constexpr int kGemmBN = 128;        // output features (W rows) per workgroup
+constexpr int kGemmBK = 64;         // K per stage (one 128-B row of X per stage)
+constexpr int kGemmMaxMW = 9;       // 16-row tiles per wave: up to 288 rows per workgroup
+
+__device__ __forceinline__ float gbf(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+
+__device__ __forceinline__ uint16_t gto_bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40);
+  return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float g_silu(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float g_gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+// byte offset of 16-B chunk c (0..7) of X-tile row r in one LDS stage
+__device__ __forceinline__ int x_swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int MW>
+struct WsShape {
+  static constexpr int kRows = 32 * MW;
+  static constexpr int kStageBytes = kRows * 128;
+  static constexpr int kChunks = kRows * 8;
+  static constexpr int kCPT = (kChunks + kGemmThreads - 1) / kGemmThreads;
+};
+
+// grid: n_tiles x splits x m_blocks (flattened, column tile fastest).  nk = K steps per split.
+// GATED: W rows [0, F) gate, [F, 2F) up (F = N / 2 = gate_off); a tile covers 64 features of
+// each; Y is [M, F].  P != nullptr: fp32 partial [split][M][n_out] instead of Y.
+template <int MW, int GATED>
+__global__ __launch_bounds__(kGemmThreads, 1) void ws_gemm_kernel(
+    const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
+    uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
+    int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+  using S = WsShape<MW>;
+  __shared__ __align__(16) unsigned char lds[3 * S::kStageBytes];
+
+  const int bid = blockIdx.x;
+  const int nt = bid % n_tiles;
+  const int sp = (bid / n_tiles) % splits;
+  const int mb = bid / (n_tiles * splits);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int wm = wv >> 2;          // row group (MW tiles of 16 rows)
+  const int wn = wv & 3;           // column group
+  const int64_t m0 = static_cast<int64_t>(mb) * S::kRows;
+  const int64_t kbase = static_cast<int64_t>(sp) * nk * kGemmBK;
+
+  // this lane's two W rows (A-fragment rows) and its k offset inside a 32-deep sub-step
+  int64_t wrow[2];
+  if (GATED) {
+    const int64_t f = static_cast<int64_t>(nt) * 64 + wn * 16 + (lane & 15);
+    wrow[0] = f;
+    wrow[1] = gate_off + f;
+  } else {
+    const int64_t n = static_cast<int64_t>(nt) * kGemmBN + wn * 32 + (lane & 15);
+    wrow[0] = n;
+    wrow[1] = n + 16;
+  }
+  const uint16_t* wp0 = W + wrow[0] * ldw + kbase + 8 * (lane >> 4);
+  const uint16_t* wp1 = W + wrow[1] * ldw + kbase + 8 * (lane >> 4);
+
+  // X staging: chunk q = tid + u * 512 -> tile row q >> 3, chunk q & 7.  Every lane loads
+  // and stores (chunks past the tile repeat its last chunk: the same bytes to the same LDS
+  // address), and every load is unconditional (K steps past the end re-read the last one,
+  // from cache): straight-line code, so the compiler's counted vmcnt waits keep the loads
+  // of later stages in flight instead of draining them at each branch join.
+  const uint16_t* xp[S::kCPT];
+  int xoff[S::kCPT];
+#pragma unroll
+  for (int u = 0; u < S::kCPT; ++u) {
+    int q = tid + u * kGemmThreads;
+    if (q > S::kChunks - 1) q = S::kChunks - 1;
+    const int r = q >> 3;
+    const int c = q & 7;
+    int64_t gr = m0 + r;
+    if (gr > M - 1) gr = M - 1;     // padded rows read a real row; their results are dropped
+    xp[u] = X + gr * ldx + kbase + c * 8;
+    xoff[u] = x_swz(r, c);
+  }
+
+  gf32x4 acc[MW][2];
+#pragma unroll
+  for (int i = 0; i < MW; ++i) {
+    acc[i][0] = gf32x4{0.f, 0.f, 0.f, 0.f};
+    acc[i][1] = gf32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  auto load_x = [&](gu32x4 (&xs)[S::kCPT], int kt) {
+    kt = kt < nk ? kt : nk - 1;
+#pragma unroll
+    for (int u = 0; u < S::kCPT; ++u) xs[u] = *reinterpret_cast<const gu32x4*>(xp[u] + kt * kGemmBK);
+  };
+  auto store_x = [&](const gu32x4 (&xs)[S::kCPT], int buf) {
+#pragma unroll
+    for (int u = 0; u < S::kCPT; ++u)
+      *reinterpret_cast<gu32x4*>(lds + buf * S::kStageBytes + xoff[u]) = xs[u];
+  };
+  auto load_w = [&](gbf16x8 (&w)[2][2], int kt) {
+    kt = kt < nk ? kt : nk - 1;
+    const int64_t o = static_cast<int64_t>(kt) * kGemmBK;
+    w[0][0] = *reinterpret_cast<const gbf16x8*>(wp0 + o);
+    w[0][1] = *reinterpret_cast<const gbf16x8*>(wp0 + o + 32);
+    w[1][0] = *reinterpret_cast<const gbf16x8*>(wp1 + o);
+    w[1][1] = *reinterpret_cast<const gbf16x8*>(wp1 + o + 32);
+  };
+  const int xr = wm * 16 * MW + (lane & 15);   // this lane's B-fragment row in tile 0
+  auto compute = [&](int buf, const gbf16x8 (&w)[2][2]) {
+    const unsigned char* base = lds + buf * S::kStageBytes;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int i = 0; i < MW; ++i) {
+        const gbf16x8 xf =
+            *reinterpret_cast<const gbf16x8*>(base + x_swz(xr + 16 * i, s * 4 + (lane >> 4)));
+        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][s], xf, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][s], xf, acc[i][1], 0, 0, 0);
+      }
+    }
+  };
+
+  // Step t computes stage t (LDS buffer t % 3, W register set t % 3), stores X(t + 1)
+  // (register set (t + 1) % 3, loaded two steps earlier) into buffer (t + 1) % 3 — last
+  // read in step t - 2 — then issues X(t + 3) into set t % 3 (stored by step t - 1) and
+  // W(t + 3) into set t % 3; one barrier per step.  W loads (HBM) have three steps to land,
+  // X loads (L2) two.
+  gbf16x8 w0[2][2], w1[2][2], w2[2][2];
+  gu32x4 xs0[S::kCPT], xs1[S::kCPT], xs2[S::kCPT];
+  load_x(xs0, 0);
+  load_w(w0, 0);
+  load_w(w1, 1);
+  load_w(w2, 2);
+  load_x(xs1, 1);
+  load_x(xs2, 2);
+  store_x(xs0, 0);
+  __syncthreads();
+#define CS_WS_STEP(T, B, WB, XST, XLD) \
+  compute(B, WB);                      \
+  store_x(XST, ((B) + 1) % 3);         \
+  load_x(XLD, (T) + 3);                \
+  load_w(WB, (T) + 3);                 \
+  __syncthreads();
+  int t = 0;
+  for (; t + 3 <= nk; t += 3) {
+    CS_WS_STEP(t, 0, w0, xs1, xs0)
+    CS_WS_STEP(t + 1, 1, w1, xs2, xs1)
+    CS_WS_STEP(t + 2, 2, w2, xs0, xs2)
+  }
+#undef CS_WS_STEP
+  if (t < nk) {                      // tail: 1 or 2 steps, nothing left to prefetch
+    compute(0, w0);
+    if (t + 1 < nk) {
+      store_x(xs1, 1);
+      __syncthreads();
+      compute(1, w1);
+    }
+  }
+
+  // epilogue: D[n][m] -> lane holds rows n = 4 * (lane >> 4) + e (e = 0..3) of column m
+#pragma unroll
+  for (int i = 0; i < MW; ++i) {
+    const int64_t m = m0 + wm * 16 * MW + 16 * i + (lane & 15);
+    if (m >= M) continue;
+    if (GATED) {
+      const int64_t f = static_cast<int64_t>(nt) * 64 + wn * 16 + 4 * (lane >> 4);
+      gu16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = gbf(gto_bf(acc[i][0][e]));
+        const float u = gbf(gto_bf(acc[i][1][e]));
+        const uint16_t a = gto_bf(act ? g_gelu_tanh(g) : g_silu(g));
+        o[e] = gto_bf(gbf(a) * u);
+      }
+      *reinterpret_cast<gu16x4*>(Y + m * ldy + f) = o;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t n = static_cast<int64_t>(nt) * kGemmBN + wn * 32 + 16 * j + 4 * (lane >> 4);
+        if (P) {
+          *reinterpret_cast<gf32x4*>(P + (static_cast<int64_t>(sp) * M + m) * n_out + n) = acc[i][j];
+        } else {
+          gu16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = gto_bf(acc[i][j][e]);
+          *reinterpret_cast<gu16x4*>(Y + m * ldy + n) = o;
+        }
+      }
+    }
+  }
+}
+
+// Y[m][n] = bf16(sum_s P[s][m][n]) in split order; 8 outputs per thread
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splits,
+                                                            int64_t M, int64_t N,
+                                                            uint16_t* __restrict__ Y, int64_t ldy) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t nv = N / 8;
+  if (v >= M * nv) return;
+  const int64_t m = v / nv;
+  const int64_t n = (v - m * nv) * 8;
+  gf32x4 a = *reinterpret_cast<const gf32x4*>(P + m * N + n);
+  gf32x4 b = *reinterpret_cast<const gf32x4*>(P + m * N + n + 4);
+  for (int s = 1; s < splits; ++s) {
+    const float* q = P + (static_cast<int64_t>(s) * M + m) * N + n;
+    a += *reinterpret_cast<const gf32x4*>(q);
+    b += *reinterpret_cast<const gf32x4*>(q + 4);
+  }
+  gu16x8 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    o[e] = gto_bf(a[e]);
+    o[4 + e] = gto_bf(b[e]);
+  }
+  *reinterpret_cast<gu16x8*>(Y + m * ldy + n) = o;
+}
+
+template <int MW, int GATED>
+void launch_ws(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
+               int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
+               int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+  hipLaunchKernelGGL((ws_gemm_kernel<MW, GATED>), dim3(blocks), dim3(kGemmThreads), 0, st, X, ldx, W,
+                     ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act);
+}
+
+template <int GATED>
+void dispatch_ws(int mw, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
+                 const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M,
+                 int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+#define CS_WS_CASE(V) \
+  case V: launch_ws<V, GATED>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act); break;
+  switch (mw) {
+    CS_WS_CASE(1) CS_WS_CASE(2) CS_WS_CASE(3) CS_WS_CASE(4) CS_WS_CASE(5)
+    CS_WS_CASE(6) CS_WS_CASE(7) CS_WS_CASE(8) CS_WS_CASE(9)
+    default: break;
+  }
+#undef CS_WS_CASE
+}
+
+// 16-row tiles per wave for M rows: all rows in one block up to 288
+int ws_mw(int64_t M) {
+  const int64_t tiles = (M + 15) / 16;
+  const int64_t mw = (tiles + 1) / 2;
+  return static_cast<int>(mw < kGemmMaxMW ? mw : kGemmMaxMW);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int mw = ws_mw(M);
+  const int64_t mblocks = (M + 32 * mw - 1) / (32 * mw);
+  const int64_t tiles = (gated ? N / 2 / 64 : N / kGemmBN) * mblocks;
+  if (gated) return 1;
+  // fill the 256 CUs (one 512-thread workgroup each) while keeping >= 8 K steps per split
+  int64_t s = 1;
+  while (tiles * s < 256 && K % (kGemmBK * s * 2) == 0 && K / (kGemmBK * s * 2) >= 8) s *= 2;
+  return s;
+}
+
+int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy,
+                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act, float* workspace,
+                 cs_stream_t stream) {
+  if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
+  if (M == 0) return CS_OK;
+  if (!x || !w || !y) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
+  if (gated && (N % 128 || splits > 1))
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: gated needs N (= 2F) a multiple of 128 and no K split");
+  if (!gated && N % kGemmBN) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
+  if (splits <= 0) splits = static_cast<int>(cs_gemm_splits(M, N, K, gated));
+  if (K % (kGemmBK * splits))
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: K must be a multiple of 64 * splits");
+  if (ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K || ldy < (gated ? N / 2 : N))
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: leading dimensions too small or misaligned");
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15 ||
+      reinterpret_cast<uintptr_t>(y) & 7)
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: operands must be 16-byte aligned (y 8-byte)");
+  if (splits > 1 && !workspace)
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: split K needs a workspace of splits * M * N floats");
+  const int mw = ws_mw(M);
+  const int64_t mblocks = (M + 32 * mw - 1) / (32 * mw);
+  const int64_t n_tiles = gated ? N / 128 : N / kGemmBN;
+  const int64_t blocks = n_tiles * splits * mblocks;
+  if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
+  const int nk = static_cast<int>(K / (kGemmBK * splits));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint16_t* X = static_cast<const uint16_t*>(x);
+  const uint16_t* Wp = static_cast<const uint16_t*>(w);
+  uint16_t* Y = static_cast<uint16_t*>(y);
+  if (gated) {
+    dispatch_ws<1>(mw, static_cast<int>(blocks), st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2,
+                   N / 2, nk, static_cast<int>(n_tiles), 1, act);
+  } else {
+    dispatch_ws<0>(mw, static_cast<int>(blocks), st, X, ldx, Wp, ldw, Y, ldy,
+                   splits > 1 ? workspace : nullptr, M, N, 0, nk, static_cast<int>(n_tiles), splits, 0);
+    if (splits > 1) {
+      const int64_t nv = M * (N / 8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(static_cast<uint32_t>((nv + 255) / 256)), dim3(256),
+                         0, st, workspace, splits, M, N, Y, ldy);
+    }
+  }
+  return check_launch("cs_gemm_bf16");
+}
+
+}  // extern "C"

@@ -692,6 +692,51 @@ def gated_act(gate: torch.Tensor, up: torch.Tensor, act: str = "silu",
     return out
 
 
+def gemm_ok(x: torch.Tensor, w: torch.Tensor, gated: bool = False) -> bool:
+    """Whether cs_gemm_bf16 takes y = x @ w.T: bf16 2-D operands with unit column stride,
+    N a multiple of 128, K of 64, 16-byte aligned rows."""
+    if x.dim() != 2 or w.dim() != 2 or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    N, K = w.shape
+    if x.shape[1] != K or N % 128 or K % 64 or x.stride(1) != 1 or w.stride(1) != 1:
+        return False
+    if (x.stride(0) % 8 and x.shape[0] > 1) or w.stride(0) % 8:
+        return False
+    return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+
+
+def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "silu",
+         splits: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T (cs_gemm_bf16): x [M, K], w [N, K] bf16, y [M, N] bf16, fp32 accumulation.
+    gated: w is the fused gate|up weight [2F, K] and y [M, F] = act(gate) * up (the rounding
+    of cs_gated_act).  splits: K split (0 = the library's choice); the fp32 partials are a
+    per-call tensor (inside a capture it belongs to the graph's pool)."""
+    L = _lib.load()
+    if not gemm_ok(x, w, gated):
+        raise CSError("cs_gemm_bf16 needs bf16 x [M, K], w [N, K] with N % 128 == 0, K % 64 == 0")
+    M, K = x.shape
+    N = w.shape[0]
+    n_out = N // 2 if gated else N
+    if out is None:
+        out = torch.empty(M, n_out, dtype=torch.bfloat16, device=x.device)
+    if out.shape != (M, n_out) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise CSError("out must be a bf16 [M, N] tensor with unit column stride")
+    _require_cuda(x, w, out)
+    if gated:
+        splits = 1
+    elif splits <= 0:
+        splits = int(L.cs_gemm_splits(M, N, K, 0))
+    part = (torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
+            if splits > 1 else None)
+    ldx = x.stride(0) if M > 1 else K
+    ldy = out.stride(0) if M > 1 else n_out
+    rc = L.cs_gemm_bf16(x.data_ptr(), ldx, w.data_ptr(), w.stride(0), out.data_ptr(), ldy, M, N,
+                        K, splits, int(bool(gated)), {"silu": 0, "gelu_tanh": 1}[act],
+                        part.data_ptr() if part is not None else None, _stream())
+    _lib.check(rc, "cs_gemm_bf16")
+    return out
+
+
 def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
                 dst_vt: torch.Tensor, parent: torch.Tensor, hist_base: torch.Tensor) -> None:
     """dst[l][s] = src[l][parent[s]] over the filled history slots (cs_hist_gather);

@@ -1,0 +1,81 @@
+"""cs_gemm_bf16 (csrc/gemm.hip) on the MI355X: the decode-step projection GEMM against an
+fp32 product of the same bf16 operands (a floating-point kernel: torch fp32 is its
+reference, SURVEY.md §8(d) "parity gates"), the gated gate|up form against cs_gated_act of
+the rounded GEMM halves, K splits against no split, and bitwise run-to-run determinism.
+
+Tolerance: |y - ref| <= 2^-7 |ref| + 1e-3 * max|ref| — one bf16 rounding of the output
+(relative 2^-8) plus fp32 accumulation-order differences over K <= 14336."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    # M, N, K            what it covers
+    (1, 128, 64),        # one row, one K step, one tile
+    (20, 3072, 2048),    # C1 q|k|v (one 32-row block)
+    (33, 256, 192),      # ragged rows (padded rows of the last tile dropped), K = 3 steps
+    (272, 8192, 3584),   # C3 q|k|v: 17 row tiles, split K
+    (272, 3584, 14336),  # C3 down: long K, split K
+    (300, 384, 640),     # > 288 rows: two row blocks
+    (520, 1024, 1024),   # C5 row count: two row blocks
+]
+
+
+def _tol(ref):
+    return ref.abs() * 2.0 ** -7 + 1e-3 * ref.abs().max()
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_matches_fp32_product(ops, dev, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = ops.gemm(x, w)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert torch.all((y.float() - ref).abs() <= _tol(ref)), (y.float() - ref).abs().max().item()
+    # every K split gives the same result up to accumulation order, and each is reproducible
+    for sp in (1, 2, 4):
+        if K % (64 * sp):
+            continue
+        a = ops.gemm(x, w, splits=sp)
+        b = ops.gemm(x, w, splits=sp)
+        assert torch.equal(a, b), f"splits={sp} not bitwise reproducible"
+        assert torch.all((a.float() - ref).abs() <= _tol(ref)), sp
+
+
+def test_gemm_strided_operands_and_out(ops, dev):
+    """x a column slice of a wider buffer (ld > K), out a slice of a wider buffer."""
+    M, N, K = 40, 256, 128
+    big = torch.randn(M, K + 64, device=dev).to(torch.bfloat16)
+    x = big[:, :K]
+    w = (torch.randn(N, K, device=dev) * 0.1).to(torch.bfloat16)
+    ob = torch.zeros(M, N + 128, device=dev, dtype=torch.bfloat16)
+    ops.gemm(x, w, out=ob[:, :N])
+    ref = x.float() @ w.float().t()
+    assert torch.all((ob[:, :N].float() - ref).abs() <= _tol(ref))
+    assert torch.all(ob[:, N:] == 0)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+@pytest.mark.parametrize("M,F,K", [(20, 512, 256), (272, 1024, 448), (300, 256, 128)])
+def test_gated_gemm_equals_gemm_then_gated_act(ops, dev, act, M, F, K):
+    """gated = 1 is act(gate) * up of the ROUNDED GEMM halves with cs_gated_act's rounding:
+    bitwise equal to cs_gated_act applied to the unsplit cs_gemm output."""
+    g = torch.Generator(device="cpu").manual_seed(F + K)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(2 * F, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    gu = ops.gemm(x, w, splits=1)
+    want = ops.gated_act(gu[:, :F], gu[:, F:], act)
+    got = ops.gemm(x, w, gated=True, act=act)
+    assert got.shape == (M, F)
+    assert torch.equal(got, want)
+
+
+def test_gemm_rejects_unsupported_shapes(ops, dev):
+    x = torch.zeros(4, 100, device=dev, dtype=torch.bfloat16)
+    w = torch.zeros(128, 100, device=dev, dtype=torch.bfloat16)
+    assert not ops.gemm_ok(x, w)
+    with pytest.raises(ops.CSError):
+        ops.gemm(x, w)
