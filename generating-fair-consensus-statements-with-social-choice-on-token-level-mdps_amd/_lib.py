@@ -122,9 +122,9 @@ def load():
     L.cs_tree_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i64, i32, i32, i32, vp]
     L.cs_tree_gather.restype = ctypes.c_int
     L.cs_gemm_bf16.argtypes = [vp, i64, vp, i64, vp, i64, i64, i64, i64, ctypes.c_int, ctypes.c_int,
-                               ctypes.c_int, vp, vp]
+                               ctypes.c_int, ctypes.c_int, vp, vp]
     L.cs_gemm_bf16.restype = ctypes.c_int
-    L.cs_gemm_splits.argtypes = [i64, i64, i64, ctypes.c_int]
+    L.cs_gemm_splits.argtypes = [i64, i64, i64, ctypes.c_int, ctypes.c_int]
     L.cs_gemm_splits.restype = i64
     _lib = L
     return L

@@ -229,6 +229,184 @@ __global__ __launch_bounds__(kGemmThreads, 1) void ws_gemm_kernel(
   }
 }
 
+typedef __attribute__((address_space(3))) void* gl_lds_ptr;
+
+// one LDS DMA piece: 16 bytes per lane from src into the wave's 1 KB at lds_base
+__device__ __forceinline__ void dma16(const uint16_t* src, unsigned char* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (gl_lds_ptr)lds_base, 16, 0, 0);
+}
+
+// a 16-byte global load the compiler does not track (its vmcnt is counted by hand)
+__device__ __forceinline__ gbf16x8 asm_load16(const uint16_t* p) {
+  gbf16x8 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// ws2_gemm_kernel<MT, NT>: the per-CU traffic of ws_gemm_kernel halved.  The 8 waves split
+// only the columns (NT 16-column tiles each, 128 * NT per workgroup) and every wave covers
+// all MT row tiles, so each W fragment is loaded by exactly one wave; X is staged by LDS
+// DMA (global_load_lds_dwordx4: no staging registers, no ds_write; the chunk swizzle is
+// applied to the per-lane SOURCE address, the LDS image is lane-linear) in three stages;
+// W goes to registers through inline-asm loads, so the compiler's waits never drain the
+// DMA queue: one counted s_waitcnt vmcnt per step (this step's X and W landed, the next
+// two steps' loads still in flight) + a raw s_barrier.
+template <int MT, int NT, int GATED, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
+    const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
+    uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
+    int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+  constexpr int kRows = 16 * MT;
+  constexpr int kStage = kRows * 128;
+  constexpr int kPieces = kRows / 8;            // 1 KB DMA pieces (8 rows) per stage
+  constexpr int kG = (kPieces + WAVES - 1) / WAVES;   // DMA instructions per wave per stage
+  constexpr int kBN = 16 * NT * WAVES;
+  constexpr int kHalf = NT / 2;                 // gated: tiles [0, kHalf) gate, [kHalf, NT) up
+  constexpr int kWait = kG + 4 * NT;            // loads issued after X(t) when step t starts
+  static_assert(!GATED || NT % 2 == 0, "the gated form pairs gate and up column tiles");
+  __shared__ __align__(16) unsigned char lds[3 * kStage];
+
+  const int bid = blockIdx.x;
+  const int nt = bid % n_tiles;
+  const int sp = (bid / n_tiles) % splits;
+  const int mb = bid / (n_tiles * splits);
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t m0 = static_cast<int64_t>(mb) * kRows;
+  const int64_t kbase = static_cast<int64_t>(sp) * nk * kGemmBK;
+
+  const uint16_t* wp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    int64_t row;
+    if (GATED) {
+      const int jj = j % kHalf;
+      const int64_t f = static_cast<int64_t>(nt) * (kBN / 2) + wv * 16 * kHalf + 16 * jj + (lane & 15);
+      row = j < kHalf ? f : gate_off + f;
+    } else {
+      row = static_cast<int64_t>(nt) * kBN + wv * 16 * NT + 16 * j + (lane & 15);
+    }
+    wp[j] = W + row * ldw + kbase + 8 * (lane >> 4);
+  }
+  const uint16_t* xsrc[kG];
+  int xdst[kG];
+#pragma unroll
+  for (int g = 0; g < kG; ++g) {
+    int pc = wv + WAVES * g;
+    if (pc > kPieces - 1) pc = kPieces - 1;     // surplus pieces rewrite the last one
+    const int r = 8 * pc + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);  // x_swz's involution, applied at the source
+    int64_t gr = m0 + r;
+    if (gr > M - 1) gr = M - 1;
+    xsrc[g] = X + gr * ldx + kbase + 8 * c;
+    xdst[g] = pc * 1024;
+  }
+
+  gf32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue_x = [&](int kt, int buf) {
+    kt = kt < nk ? kt : nk - 1;
+#pragma unroll
+    for (int g = 0; g < kG; ++g)
+      dma16(xsrc[g] + kt * kGemmBK, lds + buf * kStage + xdst[g]);
+  };
+  auto load_w = [&](gbf16x8 (&w)[NT][2], int kt) {
+    kt = kt < nk ? kt : nk - 1;
+    const int64_t o = static_cast<int64_t>(kt) * kGemmBK;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      w[j][0] = asm_load16(wp[j] + o);
+      w[j][1] = asm_load16(wp[j] + o + 32);
+    }
+  };
+  const int xr = lane & 15;
+  constexpr int kQ = 2 * MT;
+  auto frag = [&](const unsigned char* base, int q) {
+    const int s = q / MT, i = q % MT;
+    return *reinterpret_cast<const gbf16x8*>(base + x_swz(xr + 16 * i, s * 4 + (lane >> 4)));
+  };
+  auto compute = [&](int buf, const gbf16x8 (&w)[NT][2]) {
+    const unsigned char* base = lds + buf * kStage;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const gbf16x8 xf = frag(base, q);
+      const int s = q / MT, i = q % MT;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j][s], xf, acc[i][j], 0, 0, 0);
+    }
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // Step t: X(t) in LDS buffer t % 3, W(t) in register set t % 3.  It waits for X(t) (and
+  // the older W(t)) with the loads of steps t - 2 and t - 1 after it still in flight, passes
+  // the barrier (every wave done with step t - 1, so buffer (t + 2) % 3 — read in step
+  // t - 1 — is free), issues X(t + 2) into it, computes, then loads W(t + 3) into the set
+  // it used: W (HBM) three steps ahead, X (L2) two.
+  gbf16x8 w0[NT][2], w1[NT][2], w2[NT][2];
+  load_w(w0, 0);
+  issue_x(0, 0);
+  load_w(w1, 1);
+  issue_x(1, 1);
+  load_w(w2, 2);
+#define CS_WS2_STEP(T, B, WB)        \
+  sync();                            \
+  issue_x((T) + 2, ((B) + 2) % 3);   \
+  if ((T) < nk) compute(B, WB);      \
+  load_w(WB, (T) + 3);
+  for (int t = 0; t < nk; t += 3) {
+    CS_WS2_STEP(t, 0, w0)
+    CS_WS2_STEP(t + 1, 1, w1)
+    CS_WS2_STEP(t + 2, 2, w2)
+  }
+#undef CS_WS2_STEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
+
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int64_t m = m0 + 16 * i + (lane & 15);
+    if (m >= M) continue;
+    if (GATED) {
+#pragma unroll
+      for (int jj = 0; jj < kHalf; ++jj) {
+        const int64_t f =
+            static_cast<int64_t>(nt) * (kBN / 2) + wv * 16 * kHalf + 16 * jj + 4 * (lane >> 4);
+        gu16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g = gbf(gto_bf(acc[i][jj][e]));
+          const float u = gbf(gto_bf(acc[i][kHalf + jj][e]));
+          const uint16_t a = gto_bf(act ? g_gelu_tanh(g) : g_silu(g));
+          o[e] = gto_bf(gbf(a) * u);
+        }
+        *reinterpret_cast<gu16x4*>(Y + m * ldy + f) = o;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int64_t n = static_cast<int64_t>(nt) * kBN + wv * 16 * NT + 16 * j + 4 * (lane >> 4);
+        if (P) {
+          *reinterpret_cast<gf32x4*>(P + (static_cast<int64_t>(sp) * M + m) * n_out + n) = acc[i][j];
+        } else {
+          gu16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = gto_bf(acc[i][j][e]);
+          *reinterpret_cast<gu16x4*>(Y + m * ldy + n) = o;
+        }
+      }
+    }
+  }
+}
+
 // Y[m][n] = bf16(sum_s P[s][m][n]) in split order; 8 outputs per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splits,
                                                             int64_t M, int64_t N,
@@ -283,16 +461,78 @@ int ws_mw(int64_t M) {
   return static_cast<int>(mw < kGemmMaxMW ? mw : kGemmMaxMW);
 }
 
+// ws2: row tiles per workgroup (instantiated counts) and row blocks for M rows
+constexpr int kWs2MT[] = {2, 4, 8, 12, 17, 18};
+void ws2_rows(int64_t M, int* mt, int64_t* mblocks) {
+  const int64_t tiles = (M + 15) / 16;
+  const int64_t mb = (tiles + 17) / 18;
+  const int64_t per = (tiles + mb - 1) / mb;
+  int v = 18;
+  for (int c : kWs2MT) {
+    if (c >= per) { v = c; break; }
+  }
+  *mt = v;
+  *mblocks = (tiles + v - 1) / v;
+}
+
+template <int MT, int NT, int GATED, int WAVES>
+void launch_ws2(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
+                int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
+                int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+  hipLaunchKernelGGL((ws2_gemm_kernel<MT, NT, GATED, WAVES>), dim3(blocks), dim3(64 * WAVES), 0, st,
+                     X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act);
+}
+
+template <int NT, int GATED, int WAVES>
+void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
+                  const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M,
+                  int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+#define CS_WS2_CASE(V)                                                                          \
+  case V:                                                                                       \
+    launch_ws2<V, NT, GATED, WAVES>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, \
+                             n_tiles, splits, act);                                             \
+    break;
+  switch (mt) {
+    CS_WS2_CASE(2) CS_WS2_CASE(4) CS_WS2_CASE(8) CS_WS2_CASE(12) CS_WS2_CASE(17) CS_WS2_CASE(18)
+    default: break;
+  }
+#undef CS_WS2_CASE
+}
+
+// W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16)
+int64_t variant_bn(int variant, int gated) {
+  if (variant == 1) return 128;
+  if (variant == 3 && !gated) return 128;
+  return 256;
+}
+
+int64_t gemm_tiles(int variant, int64_t M, int64_t N, int gated) {
+  if (variant == 1) {
+    const int mw = ws_mw(M);
+    return (gated ? N / 128 : N / kGemmBN) * ((M + 32 * mw - 1) / (32 * mw));
+  }
+  int mt;
+  int64_t mb;
+  ws2_rows(M, &mt, &mb);
+  return (N / variant_bn(variant, gated)) * mb;
+}
+
+int resolve_variant(int variant, int64_t N, int gated) {
+  if (variant == 0) variant = 2;
+  if (variant == 2 && N % 256) variant = gated ? 1 : 3;
+  if (variant == 3 && gated) variant = 2;
+  return variant;
+}
+
 }  // namespace
 
 extern "C" {
 
-int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated) {
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  const int mw = ws_mw(M);
-  const int64_t mblocks = (M + 32 * mw - 1) / (32 * mw);
-  const int64_t tiles = (gated ? N / 2 / 64 : N / kGemmBN) * mblocks;
+int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant) {
+  if (M <= 0 || N <= 0 || K <= 0 || N % 128) return 0;
   if (gated) return 1;
+  variant = resolve_variant(variant, N, gated);
+  const int64_t tiles = gemm_tiles(variant, M, N, gated);
   // fill the 256 CUs (one 512-thread workgroup each) while keeping >= 8 K steps per split
   int64_t s = 1;
   while (tiles * s < 256 && K % (kGemmBK * s * 2) == 0 && K / (kGemmBK * s * 2) >= 8) s *= 2;
@@ -300,15 +540,17 @@ int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated) {
 }
 
 int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy,
-                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act, float* workspace,
-                 cs_stream_t stream) {
+                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act, int variant,
+                 float* workspace, cs_stream_t stream) {
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
   if (M == 0) return CS_OK;
   if (!x || !w || !y) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
-  if (gated && (N % 128 || splits > 1))
-    return fail(CS_ERR_INVALID, "cs_gemm_bf16: gated needs N (= 2F) a multiple of 128 and no K split");
-  if (!gated && N % kGemmBN) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
-  if (splits <= 0) splits = static_cast<int>(cs_gemm_splits(M, N, K, gated));
+  if (variant < 0 || variant > 3) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..3");
+  if (N % 128) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
+  if (gated && splits > 1)
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
+  variant = resolve_variant(variant, N, gated);
+  if (splits <= 0) splits = static_cast<int>(cs_gemm_splits(M, N, K, gated, variant));
   if (K % (kGemmBK * splits))
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: K must be a multiple of 64 * splits");
   if (ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K || ldy < (gated ? N / 2 : N))
@@ -318,27 +560,42 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: operands must be 16-byte aligned (y 8-byte)");
   if (splits > 1 && !workspace)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: split K needs a workspace of splits * M * N floats");
-  const int mw = ws_mw(M);
-  const int64_t mblocks = (M + 32 * mw - 1) / (32 * mw);
-  const int64_t n_tiles = gated ? N / 128 : N / kGemmBN;
-  const int64_t blocks = n_tiles * splits * mblocks;
+  const int64_t tiles = gemm_tiles(variant, M, N, gated);
+  const int64_t blocks = tiles * splits;
   if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
   const int nk = static_cast<int>(K / (kGemmBK * splits));
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint16_t* X = static_cast<const uint16_t*>(x);
   const uint16_t* Wp = static_cast<const uint16_t*>(w);
   uint16_t* Y = static_cast<uint16_t*>(y);
-  if (gated) {
-    dispatch_ws<1>(mw, static_cast<int>(blocks), st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2,
-                   N / 2, nk, static_cast<int>(n_tiles), 1, act);
+  float* Pp = splits > 1 ? workspace : nullptr;
+  if (variant == 1) {
+    const int mw = ws_mw(M);
+    const int n_tiles = static_cast<int>(gated ? N / 128 : N / kGemmBN);
+    if (gated)
+      dispatch_ws<1>(mw, static_cast<int>(blocks), st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2,
+                     N / 2, nk, n_tiles, 1, act);
+    else
+      dispatch_ws<0>(mw, static_cast<int>(blocks), st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk,
+                     n_tiles, splits, 0);
   } else {
-    dispatch_ws<0>(mw, static_cast<int>(blocks), st, X, ldx, Wp, ldw, Y, ldy,
-                   splits > 1 ? workspace : nullptr, M, N, 0, nk, static_cast<int>(n_tiles), splits, 0);
-    if (splits > 1) {
-      const int64_t nv = M * (N / 8);
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(static_cast<uint32_t>((nv + 255) / 256)), dim3(256),
-                         0, st, workspace, splits, M, N, Y, ldy);
+    int mt;
+    int64_t mb;
+    ws2_rows(M, &mt, &mb);
+    const int n_tiles = static_cast<int>(N / variant_bn(variant, gated));
+    const int b = static_cast<int>(blocks);
+    if (gated) {
+      dispatch_ws2<2, 1, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1, act);
+    } else if (variant == 2) {
+      dispatch_ws2<2, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0);
+    } else {
+      dispatch_ws2<1, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0);
     }
+  }
+  if (splits > 1 && !gated) {
+    const int64_t nv = M * (N / 8);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(static_cast<uint32_t>((nv + 255) / 256)), dim3(256),
+                       0, st, workspace, splits, M, N, Y, ldy);
   }
   return check_launch("cs_gemm_bf16");
 }

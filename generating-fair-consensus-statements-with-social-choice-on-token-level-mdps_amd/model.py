@@ -357,6 +357,10 @@ class Model:
 
     def lm_head(self, h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         W = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
+        if h.is_cuda and h.dim() == 2 and h.dtype == W.dtype == torch.bfloat16:
+            from . import ops   # local: model.py stays importable without the library
+            if ops.gemm_choice(h.shape[0], W.shape[0], W.shape[1]) is not None:
+                return ops.linear(h, W, out=out)
         if out is not None:
             return torch.matmul(h.to(W.dtype), W.t(), out=out)
         return h.to(W.dtype) @ W.t()
@@ -404,7 +408,7 @@ class Model:
         x = ops.add_rms_norm(h, self.w["l0.attn_norm"], eps, plus_one=g2)
         for i in range(c.n_layers):
             p = f"l{i}."
-            qkv = x @ self.wf[p + "qkv"].t()
+            qkv = ops.linear(x, self.wf[p + "qkv"])
             q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
             ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
                            hist_k[i], hist_vt[i], group_prefix=group_prefix)
@@ -415,12 +419,12 @@ class Model:
                                      group_prefix=group_prefix,
                                      prefix_len_host=getattr(pfx, "lens_host", None),
                                      group_prefix_host=group_prefix_host)
-            o = o.view(n_tok, H * D) @ self.w[p + "wo"].t()
+            o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"])
             if g2:
                 o = ops.add_rms_norm(o, self.w[p + "post_attn_norm"], eps, plus_one=True)
             x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2)
-            gu = x @ self.wf[p + "gate_up"].t()
-            y = ops.gated_act(gu[:, :c.d_ff], gu[:, c.d_ff:], act) @ self.w[p + "w_down"].t()
+            y = ops.linear(ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act),
+                           self.w[p + "w_down"])
             if g2:
                 y = ops.add_rms_norm(y, self.w[p + "post_mlp_norm"], eps, plus_one=True)
             nxt = self.w[f"l{i + 1}.attn_norm"] if i + 1 < c.n_layers else self.w["norm"]

@@ -12,6 +12,8 @@ from __future__ import annotations
 import collections
 import contextlib
 import ctypes
+import json
+import os
 import threading
 from typing import Optional, Sequence
 
@@ -176,7 +178,7 @@ def welfare(U: torch.Tensor, kind, *, eps: float = 1e-9, nonfinite: str = "skip"
     L = _lib.load()
     if isinstance(kind, str):
         kind = WELFARE[kind]
-    if U.dim() != 2 or U.dtype != torch.float32 or U.stride(1) != 1:
+    if U.dim() != 2 or U.dtype != torch.float32 or (U.stride(1) != 1 and U.shape[1] > 1):
         raise CSError("U must be 2-D float32 with unit column stride")
     _require_cuda(U, out)
     A, C = U.shape
@@ -692,6 +694,46 @@ def gated_act(gate: torch.Tensor, up: torch.Tensor, act: str = "silu",
     return out
 
 
+GEMM_DISPATCH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned",
+                             "gemm_dispatch_mi355x.json")
+_gemm_table: Optional[dict] = None
+
+
+def gemm_choice(M: int, N: int, K: int, gated: bool = False) -> Optional[dict]:
+    """The cs_gemm_bf16 tile variant and K split measured faster than hipBLASLt for this
+    exact shape on MI355X (tools/tune_gemm_dispatch.py -> tuned/gemm_dispatch_mi355x.json,
+    read only), or None: the shape stays on hipBLASLt.  CS_GEMM_DISPATCH=0 turns the table
+    off, CS_GEMM_DISPATCH=<file> reads another one."""
+    global _gemm_table
+    if _gemm_table is None:
+        env = os.environ.get("CS_GEMM_DISPATCH", "")
+        path = GEMM_DISPATCH if env in ("", "1") else env
+        table = {}
+        if env != "0" and os.path.exists(path):
+            with open(path) as f:
+                table = json.load(f).get("table", {})
+        _gemm_table = table
+    return _gemm_table.get(f"{M},{N},{K},{int(bool(gated))}")
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "silu",
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T (gated: act(gate) * up of the fused gate|up weight) on whichever GEMM the
+    dispatch table measured faster for this shape: cs_gemm_bf16 or hipBLASLt (+ cs_gated_act)."""
+    if x.is_cuda and x.dim() == 2:
+        ch = gemm_choice(x.shape[0], w.shape[0], w.shape[1], gated)
+        if ch is not None and gemm_ok(x, w, gated):
+            return gemm(x, w, gated=gated, act=act, splits=int(ch["splits"]),
+                        variant=int(ch["variant"]), out=out)
+    if gated:          # the plain GEMM (on whichever library is faster) + cs_gated_act
+        F = w.shape[0] // 2
+        y = linear(x, w)
+        return gated_act(y[:, :F], y[:, F:], act, out=out)
+    if out is not None:
+        return torch.matmul(x, w.t(), out=out)
+    return x @ w.t()
+
+
 def gemm_ok(x: torch.Tensor, w: torch.Tensor, gated: bool = False) -> bool:
     """Whether cs_gemm_bf16 takes y = x @ w.T: bf16 2-D operands with unit column stride,
     N a multiple of 128, K of 64, 16-byte aligned rows."""
@@ -706,7 +748,7 @@ def gemm_ok(x: torch.Tensor, w: torch.Tensor, gated: bool = False) -> bool:
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "silu",
-         splits: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+         splits: int = 0, variant: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w.T (cs_gemm_bf16): x [M, K], w [N, K] bf16, y [M, N] bf16, fp32 accumulation.
     gated: w is the fused gate|up weight [2F, K] and y [M, F] = act(gate) * up (the rounding
     of cs_gated_act).  splits: K split (0 = the library's choice); the fp32 partials are a
@@ -725,13 +767,13 @@ def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "s
     if gated:
         splits = 1
     elif splits <= 0:
-        splits = int(L.cs_gemm_splits(M, N, K, 0))
+        splits = int(L.cs_gemm_splits(M, N, K, 0, variant))
     part = (torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
             if splits > 1 else None)
     ldx = x.stride(0) if M > 1 else K
     ldy = out.stride(0) if M > 1 else n_out
     rc = L.cs_gemm_bf16(x.data_ptr(), ldx, w.data_ptr(), w.stride(0), out.data_ptr(), ldy, M, N,
-                        K, splits, int(bool(gated)), {"silu": 0, "gelu_tanh": 1}[act],
+                        K, splits, int(bool(gated)), {"silu": 0, "gelu_tanh": 1}[act], variant,
                         part.data_ptr() if part is not None else None, _stream())
     _lib.check(rc, "cs_gemm_bf16")
     return out

@@ -401,19 +401,21 @@ int cs_gated_act(const void* gate, int64_t ld_gate, const void* up, int64_t ld_u
  * gate|up weight [2F, K] (gate rows first) and Y [M, F] = act(gate) * up with the rounding
  * of cs_gated_act (act 0 SiLU, 1 tanh-GeLU).  splits > 1 divides K over workgroups and
  * folds the fp32 partials in split order (workspace: splits * M * N floats); splits <= 0
- * takes cs_gemm_splits.  N a multiple of 128, K of 64 * splits; ldx, ldw multiples of 8,
- * ldy of 4; X, W 16-byte aligned.  Deterministic (no atomics).
+ * takes cs_gemm_splits.  variant: 0 = the library's choice, 1 = 2 x 4 wave grid (128 columns x
+ * up to 288 rows per workgroup), 2 = column-only wave split, 256 columns, LDS-DMA X,
+ * 3 = as 2 with 128 columns.  N a multiple of 128, K of 64 * splits; ldx, ldw multiples of
+ * 8, ldy of 4; X, W 16-byte aligned.  Deterministic (no atomics).
  *
  * Replaces: part of the remote forward behind every get_prompt_logprobs call
  *   (src/utils.py:249-259) — the per-layer q|k|v, output, gate|up and down projections of
  *   each new token (the gated form also replaces cs_gated_act on that path).
  */
 int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy,
-                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act,
+                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act, int variant,
                  float* workspace, cs_stream_t stream);
 
 /* cs_gemm_splits — the K split cs_gemm_bf16 takes for splits <= 0 (>= 1; 0 on a bad shape). */
-int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated);
+int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant);
 
 #ifdef __cplusplus
 }

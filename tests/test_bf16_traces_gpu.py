@@ -22,6 +22,11 @@ replayed through that path:
 TOL_BF16 is the absolute per-agent log-prob tolerance of the bf16 forward (weights and
 activations rounded to bf16, fp32 accumulation) against the reference's fp32 forward.
 The measured maxima are printed (pytest -s) and recorded in DESIGN.md.
+
+Each trace runs twice: with the projection / LM-head GEMMs as the shipped dispatch table
+routes them (hipBLASLt for these fixture shapes) and with EVERY eligible GEMM forced onto
+cs_gemm_bf16 (csrc/gemm.hip), so the hand-written GEMM is pinned to the reference's traces
+at the same tolerance, not only to an fp32 product.
 """
 import importlib
 import json
@@ -40,14 +45,41 @@ BF16_TRACE_FILES = ["method_traces_c1.json", "method_traces_wide.json"]
 _REPORT = {}
 
 
-@pytest.fixture(scope="module", params=BF16_TRACE_FILES)
+class _EveryShape(dict):
+    """A dispatch table that routes every shape cs_gemm_bf16 takes onto it."""
+
+    def get(self, key, default=None):
+        M, N, K, g = (int(v) for v in key.split(","))
+        if N % 128 or K % 64:
+            return default
+        return {"variant": 2 if N % 256 == 0 else 3, "splits": 1}
+
+
+@pytest.fixture(scope="module", params=[(f, r) for f in BF16_TRACE_FILES
+                                        for r in ("dispatch", "cs_gemm")],
+                ids=lambda p: f"{p[0]}-{p[1]}")
 def bf16_traces(request, dev):
-    t = mp.load_traces(request.param)
-    t["_file"] = request.param
+    fname, route = request.param
+    ops = importlib.import_module(mp.PKG + ".ops")
+    t = mp.load_traces(fname)
+    t["_file"] = fname if route == "dispatch" else f"{fname} (every GEMM on cs_gemm)"
     eng, tok = mp.register_fixture_engine(t, dev, dtype=torch.bfloat16)
     assert eng.model.fused_ok(), "fixture heads must be served by the stream kernels"
-    yield t, eng, tok
-    importlib.import_module(mp.PKG + ".runtime").clear_engines()
+    saved_table, saved_gemm = ops._gemm_table, ops.gemm
+    calls = [0]
+    if route == "cs_gemm":
+        def counted(*a, **k):
+            calls[0] += 1
+            return saved_gemm(*a, **k)
+        ops._gemm_table = _EveryShape()
+        ops.gemm = counted
+    try:
+        yield t, eng, tok
+    finally:
+        ops._gemm_table, ops.gemm = saved_table, saved_gemm
+        importlib.import_module(mp.PKG + ".runtime").clear_engines()
+    if route == "cs_gemm" and fname == "method_traces_c1.json":
+        assert calls[0] > 0, "no GEMM of the C1 fixture went through cs_gemm_bf16"
 
 
 def _report(name, key, value):

@@ -6,7 +6,9 @@ read the row the decode already has for the context they keep) against the full 
 (every unstable (agent, candidate) prompt re-encoded, the reference's per-call semantics,
 src/methods/beam_search.py:335-404 through src/utils.py:201-373) on the same bf16 model:
 the same candidates at every step, per-agent increments within the bf16 tolerance, and the
-same kept beams wherever no near tie decides."""
+same kept beams wherever no near tie decides.  The first two steps' proposals are forced to
+BPE pieces that merge (" sh" + "ould" -> " should", " the" + "ir" -> " their", ...), so the
+incremental rows are exercised whatever the random model would have drawn."""
 import importlib
 import os
 
@@ -46,12 +48,28 @@ def test_incremental_text_path_matches_full_text_path(dev, family):
                 "Agent 2": "Sharing genes helps research cure illnesses.",
                 "Agent 3": "Families should decide together about genetic tests."}
     issue = "Should a person's genetic code be considered private information?"
+    # pieces of the fixture BPE whose concatenation is ONE token of its vocabulary
+    firsts = [tok.encode(s)[0] for s in (" sh", " the", " benef")]
+    seconds = [tok.encode(s)[0] for s in ("ould", "ir", "it", "its")]
+    assert tok.encode(" should") == [tok.encode(" should")[0]]
     try:
         logs, gens = [], []
         for incremental in (True, False):
             g = methods.get_method_generator("beam_search", {
                 "beam_width": 3, "max_tokens": 6, "max_sampling_attempts": 5, "seed": 3,
                 "text_incremental": incremental}, "test/text-path")
+            drawn = g._propose
+            calls = [0]
+
+            def forced(st, ref_idx, bias, seed, tok_, drawn=drawn, calls=calls):
+                k = calls[0]
+                calls[0] += 1
+                if k == 0:
+                    return [list(firsts)] + [[] for _ in range(st.n_beams - 1)]
+                if k == 1:
+                    return [list(seconds) for _ in range(st.n_beams)]
+                return drawn(st, ref_idx, bias, seed, tok_)
+            g._propose = forced
             g.generate_statement(issue, opinions)
             assert g.decode_path == "fused"
             logs.append(g.step_log)

@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
 R = importlib.import_module(PKG + ".runtime")
 ops = importlib.import_module(PKG + ".ops")
@@ -57,6 +57,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="c1,c3,c5")
     ap.add_argument("--splits", default="0")
+    ap.add_argument("--variants", default="0")
     ap.add_argument("--msweep", default="", help="torch only: comma list of M for the C3 shapes")
     args = ap.parse_args()
     print("tuning:", R.use_gemm_tuning(), file=sys.stderr)
@@ -89,17 +90,18 @@ def main():
             g = ref[:, :F].to(torch.bfloat16)
             u = ref[:, F:].to(torch.bfloat16)
             ref = ops.gated_act(g, u, "silu").float()
-        for sp in [int(s) for s in args.splits.split(",")]:
+        for var, sp in [(int(v), int(s)) for v in args.variants.split(",")
+                        for s in args.splits.split(",")]:
             if gated and sp > 1:
                 continue
-            y = ops.gemm(x, ws[0], gated=bool(gated), splits=sp)
+            y = ops.gemm(x, ws[0], gated=bool(gated), splits=sp, variant=var)
             torch.cuda.synchronize()
             err = (y.float() - ref).abs().max().item()
             scale = ref.abs().max().item()
-            t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), splits=sp)
+            t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), splits=sp, variant=var)
                                for i in range(calls)]) / calls * 1e3
-            eff = int(ops._lib.load().cs_gemm_splits(M, N, K, gated)) if sp <= 0 else sp
-            rec = {"shape": name, "M": M, "N": N, "K": K, "impl": "cs_gemm", "splits": eff,
+            eff = int(ops._lib.load().cs_gemm_splits(M, N, K, gated, var)) if sp <= 0 else sp
+            rec = {"shape": name, "M": M, "N": N, "K": K, "impl": f"cs_gemm_v{var}", "splits": eff,
                    "us": round(t, 2), "weight_GBps": round(N * K * 2 / t / 1e3, 1),
                    "TFLOPs": round(2 * M * N * K / t / 1e6, 1), "max_err": err, "ref_max": scale}
             print(json.dumps(rec), flush=True)

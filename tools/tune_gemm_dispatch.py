@@ -1,0 +1,130 @@
+"""Choose, per decode-step projection GEMM shape, between hipBLASLt (torch, with the
+committed TunableOp selection) and cs_gemm_bf16 (csrc/gemm.hip, each tile variant and K
+split), measured on this MI355X with the weights streamed from HBM (distinct matrices
+rotated past the Infinity Cache, 20 calls per captured graph), and write the selection the
+model reads (ops.gemm_choice; read-only at run time).
+
+Shapes: the q|k|v, output, gate|up (plain and with the gated activation fused), down and
+LM-head GEMMs of the C1 / C3 / C5 beam-search decode steps, at every agent shard of 1, 2,
+4 and 8 ranks (M = (agents / ranks + 1) * beams: the agents' streams plus the reference
+policy's).
+
+    python tools/tune_gemm_dispatch.py [--out gpurun_out/gemm_dispatch.json] [--install]
+"""
+import argparse
+import importlib
+import json
+import os
+import shutil
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+R = importlib.import_module(PKG + ".runtime")
+ops = importlib.import_module(PKG + ".ops")
+model = importlib.import_module(PKG + ".model")
+
+CONFIGS = {"c1": ("llama-3.2-1b", 4, 4), "c3": ("gemma-2-9b", 16, 16), "c5": ("llama-3.3-70b", 64, 8)}
+
+
+def shapes_of(preset: str):
+    c = model.PRESETS[preset]
+    d, H, Hkv, D, F = c.d_model, c.n_heads, c.n_kv_heads, c.head_dim, c.d_ff
+    act = "gelu_tanh" if c.family == "gemma2" else "silu"
+    return [("qkv", (H + 2 * Hkv) * D, d, 0, act), ("o", d, H * D, 0, act),
+            ("gate_up", 2 * F, d, 0, act), ("gate_up_act", 2 * F, d, 1, act),
+            ("down", d, F, 0, act), ("lm_head", c.vocab, d, 0, act)]
+
+
+def timed(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = None
+    for _ in range(3):
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / reps
+        best = t if best is None else min(best, t)
+    return best
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "gemm_dispatch.json"))
+    ap.add_argument("--configs", default="c1,c3,c5")
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--install", action="store_true")
+    args = ap.parse_args()
+    print("tuning:", R.use_gemm_tuning(), file=sys.stderr)
+    dev = torch.device("cuda:0")
+    L = ops._lib.load()
+    table, record = {}, []
+    calls = 20
+    for cname in args.configs.split(","):
+        preset, A, B = CONFIGS[cname]
+        Ms = sorted({(A // w + (1 if A % w else 0) + 1) * B for w in map(int, args.worlds.split(","))})
+        for name, N, K, gated, act in shapes_of(preset):
+            nw = max(2, min(20, (700 << 20) // (N * K * 2) + 1))
+            ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05 for _ in range(nw)]
+            for M in Ms:
+                x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+                if gated:
+                    Fh = N // 2
+
+                    def tfn():
+                        for i in range(calls):
+                            gu = x @ ws[i % nw].t()
+                            ops.gated_act(gu[:, :Fh], gu[:, Fh:], act)
+                else:
+                    def tfn():
+                        for i in range(calls):
+                            x @ ws[i % nw].t()
+                t_torch = timed(tfn) / calls * 1e3
+                best = ("torch", 0, 0, t_torch)
+                cands = []
+                for var in (2, 3):
+                    for sp in ((1,) if gated else (1, 2, 4, 8, 16)):
+                        if K % (64 * sp) or K // (64 * sp) < 2 or (var == 2 and N % 256):
+                            continue
+                        t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), act=act,
+                                                    splits=sp, variant=var)
+                                           for i in range(calls)]) / calls * 1e3
+                        cands.append({"variant": var, "splits": sp, "us": round(t, 2)})
+                        if t < best[3]:
+                            best = ("cs_gemm", var, sp, t)
+                rec = {"config": cname, "gemm": name, "M": M, "N": N, "K": K, "gated": gated,
+                       "torch_us": round(t_torch, 2), "cs_gemm": cands, "choice": best[0],
+                       "best_us": round(best[3], 2)}
+                record.append(rec)
+                print(json.dumps(rec), flush=True)
+                if best[0] == "cs_gemm":
+                    table[f"{M},{N},{K},{gated}"] = {"variant": best[1], "splits": best[2],
+                                                     "us": round(best[3], 2),
+                                                     "torch_us": round(t_torch, 2)}
+            del ws
+    out = {"device": torch.cuda.get_device_name(0), "torch": torch.__version__,
+           "hip": torch.version.hip, "library": ops._lib.version(),
+           "note": "shapes absent here run on hipBLASLt (torch)", "table": table,
+           "measured": record}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    if args.install:
+        shutil.copy(args.out, os.path.join(REPO, PKG, "tuned", "gemm_dispatch_mi355x.json"))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
