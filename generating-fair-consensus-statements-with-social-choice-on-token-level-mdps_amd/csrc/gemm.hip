@@ -255,7 +255,7 @@ template <int MT, int NT, int GATED, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
     const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
     uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
-    int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+    int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
   constexpr int kRows = 16 * MT;
   constexpr int kStage = kRows * 128;
   constexpr int kPieces = kRows / 8;            // 1 KB DMA pieces (8 rows) per stage
@@ -266,10 +266,19 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   static_assert(!GATED || NT % 2 == 0, "the gated form pairs gate and up column tiles");
   __shared__ __align__(16) unsigned char lds[3 * kStage];
 
+  // row blocks of one (column tile, split) cell are 8 block ids apart — dispatched to the
+  // same XCD (ids are dealt round-robin over the 8 XCDs) at about the same time, so the
+  // second block's W reads hit that XCD's L2; the grid is padded to whole groups of 8 cells
   const int bid = blockIdx.x;
-  const int nt = bid % n_tiles;
-  const int sp = (bid / n_tiles) % splits;
-  const int mb = bid / (n_tiles * splits);
+  int cell = bid, mb = 0;
+  if (m_blocks > 1) {
+    const int g = bid / (8 * m_blocks), r = bid % (8 * m_blocks);
+    mb = r / 8;
+    cell = g * 8 + (r % 8);
+  }
+  if (cell >= n_tiles * splits) return;
+  const int nt = cell % n_tiles;
+  const int sp = cell / n_tiles;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t m0 = static_cast<int64_t>(mb) * kRows;
@@ -331,13 +340,37 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   };
   auto compute = [&](int buf, const gbf16x8 (&w)[NT][2]) {
     const unsigned char* base = lds + buf * kStage;
+    if constexpr (MT > 9) {        // 2 waves per SIMD, no registers left for a ring
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const gbf16x8 xf = frag(base, q);
-      const int s = q / MT, i = q % MT;
+      for (int q = 0; q < kQ; ++q) {
+        const gbf16x8 xf = frag(base, q);
+        const int s = q / MT, i = q % MT;
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j][s], xf, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j][s], xf, acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // B-fragments through a ring of kRing registers, kRing - 1 reads ahead of their
+      // MFMAs; the schedule is pinned (ring fill, then one ds_read per NT MFMAs) so the LDS
+      // round trip hides behind the MFMAs of earlier fragments
+      constexpr int kRing = 4;
+      gbf16x8 f[kRing];
+#pragma unroll
+      for (int q = 0; q < kRing - 1; ++q) f[q] = frag(base, q);
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        if (q + kRing - 1 < kQ) f[(q + kRing - 1) % kRing] = frag(base, q + kRing - 1);
+        const int s = q / MT, i = q % MT;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j][s], f[q % kRing], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, kRing - 1, 0);
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        if (q + kRing - 1 < kQ) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
+      }
     }
   };
   auto sync = [&]() {
@@ -462,10 +495,10 @@ int ws_mw(int64_t M) {
 }
 
 // ws2: row tiles per workgroup (instantiated counts) and row blocks for M rows
-constexpr int kWs2MT[] = {2, 4, 8, 12, 17, 18};
-void ws2_rows(int64_t M, int* mt, int64_t* mblocks) {
+constexpr int kWs2MT[] = {2, 4, 8, 9, 12, 17, 18};
+void ws2_rows(int64_t M, int* mt, int64_t* mblocks, int max_tiles = 18) {
   const int64_t tiles = (M + 15) / 16;
-  const int64_t mb = (tiles + 17) / 18;
+  const int64_t mb = (tiles + max_tiles - 1) / max_tiles;
   const int64_t per = (tiles + mb - 1) / mb;
   int v = 18;
   for (int c : kWs2MT) {
@@ -478,33 +511,39 @@ void ws2_rows(int64_t M, int* mt, int64_t* mblocks) {
 template <int MT, int NT, int GATED, int WAVES>
 void launch_ws2(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
                 int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
-                int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+                int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
   hipLaunchKernelGGL((ws2_gemm_kernel<MT, NT, GATED, WAVES>), dim3(blocks), dim3(64 * WAVES), 0, st,
-                     X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act);
+                     X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act,
+                     m_blocks);
 }
 
 template <int NT, int GATED, int WAVES>
 void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
                   const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M,
-                  int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act) {
+                  int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act,
+                  int m_blocks) {
 #define CS_WS2_CASE(V)                                                                          \
   case V:                                                                                       \
     launch_ws2<V, NT, GATED, WAVES>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, \
-                             n_tiles, splits, act);                                             \
+                                    n_tiles, splits, act, m_blocks);                            \
     break;
   switch (mt) {
-    CS_WS2_CASE(2) CS_WS2_CASE(4) CS_WS2_CASE(8) CS_WS2_CASE(12) CS_WS2_CASE(17) CS_WS2_CASE(18)
+    CS_WS2_CASE(2) CS_WS2_CASE(4) CS_WS2_CASE(8) CS_WS2_CASE(9) CS_WS2_CASE(12) CS_WS2_CASE(17)
+    CS_WS2_CASE(18)
     default: break;
   }
 #undef CS_WS2_CASE
 }
 
-// W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16)
+// W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16;
+// 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
 int64_t variant_bn(int variant, int gated) {
   if (variant == 1) return 128;
   if (variant == 3 && !gated) return 128;
   return 256;
 }
+
+int variant_max_tiles(int variant) { return variant == 4 ? 9 : 18; }
 
 int64_t gemm_tiles(int variant, int64_t M, int64_t N, int gated) {
   if (variant == 1) {
@@ -513,13 +552,18 @@ int64_t gemm_tiles(int variant, int64_t M, int64_t N, int gated) {
   }
   int mt;
   int64_t mb;
-  ws2_rows(M, &mt, &mb);
+  ws2_rows(M, &mt, &mb, variant_max_tiles(variant));
   return (N / variant_bn(variant, gated)) * mb;
+}
+
+// grid of a ws2 launch: (column tile, split) cells padded to groups of 8 when row blocks pair
+int64_t ws2_grid(int64_t cells, int64_t mblocks) {
+  return mblocks > 1 ? (cells + 7) / 8 * 8 * mblocks : cells;
 }
 
 int resolve_variant(int variant, int64_t N, int gated) {
   if (variant == 0) variant = 2;
-  if (variant == 2 && N % 256) variant = gated ? 1 : 3;
+  if ((variant == 2 || variant == 4) && N % 256) variant = gated ? 1 : 3;
   if (variant == 3 && gated) variant = 2;
   return variant;
 }
@@ -545,7 +589,7 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
   if (M == 0) return CS_OK;
   if (!x || !w || !y) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
-  if (variant < 0 || variant > 3) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..3");
+  if (variant < 0 || variant > 4) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..4");
   if (N % 128) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
   if (gated && splits > 1)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
@@ -581,15 +625,19 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   } else {
     int mt;
     int64_t mb;
-    ws2_rows(M, &mt, &mb);
+    ws2_rows(M, &mt, &mb, variant_max_tiles(variant));
     const int n_tiles = static_cast<int>(N / variant_bn(variant, gated));
-    const int b = static_cast<int>(blocks);
+    const int64_t grid = ws2_grid(static_cast<int64_t>(n_tiles) * splits, mb);
+    if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
+    const int b = static_cast<int>(grid);
+    const int mbi = static_cast<int>(mb);
     if (gated) {
-      dispatch_ws2<2, 1, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1, act);
-    } else if (variant == 2) {
-      dispatch_ws2<2, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0);
+      dispatch_ws2<2, 1, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1,
+                            act, mbi);
+    } else if (variant == 3) {
+      dispatch_ws2<1, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
     } else {
-      dispatch_ws2<1, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0);
+      dispatch_ws2<2, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
     }
   }
   if (splits > 1 && !gated) {

@@ -94,9 +94,9 @@ def main() -> int:
                 t_torch = timed(tfn) / calls * 1e3
                 best = ("torch", 0, 0, t_torch)
                 cands = []
-                for var in (2, 3):
+                for var in (2, 3, 4):
                     for sp in ((1,) if gated else (1, 2, 4, 8, 16)):
-                        if K % (64 * sp) or K // (64 * sp) < 2 or (var == 2 and N % 256):
+                        if K % (64 * sp) or K // (64 * sp) < 2 or (var in (2, 4) and N % 256):
                             continue
                         t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), act=act,
                                                     splits=sp, variant=var)
