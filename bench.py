@@ -172,6 +172,8 @@ def parse():
     ap.add_argument("--method", default="c1,c3,c4,c5",
                     help="method-level decode configs: beam_search c1/c3/c5, finite_lookahead c4 "
                          "('' disables)")
+    ap.add_argument("--method-bon", type=int, default=1,
+                    help="1: time BASELINE C2 through BestOfNGenerator.score_candidates too")
     ap.add_argument("--method-text-steps", type=int, default=4,
                     help="steps of a short statement timed with the re-tokenized text semantics")
     ap.add_argument("--method-statements", type=int, default=1,
@@ -426,6 +428,63 @@ def c2_e2e_leg(args, world, rank, dev, prefix_len=200, seed=0):
     del eng, model
     _free()
     return out
+
+
+def method_leg_bon(args, world, rank, dev):
+    """BASELINE C2 through the product's Best-of-N API: ``BestOfNGenerator.score_candidates``
+    (candidate texts re-encoded, the 8 agents' prompts prefilled, every (agent, candidate)
+    scored on the stream kernels, the per-pair check of the reference's find() semantics,
+    best_of_n.py:240-327) + ``combine_welfare`` + top-1 (best_of_n.py:329-418, 198) on the
+    64 candidate TEXTS of ~150 tokens -- the host work of a BoN selection pass included.
+    Candidate generation is not part of a pass."""
+    R = importlib.import_module(PKG_DIR + ".runtime")
+    methods = importlib.import_module(PKG_DIR + ".methods")
+    ops = importlib.import_module(PKG_DIR + ".ops")
+    par = importlib.import_module(PKG_DIR + ".parallel")
+    A, N, T, V, wkind, desc = CONFIGS["c2"]
+    t0 = time.perf_counter()
+    eng, tok = R.random_engine("llama-3.1-8b", dev, reuse_caches=0, tokenizer_dir=BPE_FIXTURE)
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    model_id = "random:llama-3.1-8b"
+    R.register_engine(model_id, eng, tok)
+    opinions = synthetic_opinions(A * world)
+    shard = par.AgentShard(A * world, rank, world)
+    # candidate texts: random pieces of the BPE fixture's own vocabulary, cut to T tokens
+    g = torch.Generator().manual_seed(11)
+    n_real = getattr(tok, "n_table", None) or 4000
+    cands = []
+    for _ in range(N):
+        ids = torch.randint(300, min(n_real, 4000), (T,), generator=g).tolist()
+        cands.append(tok.decode(tok.encode(tok.decode(ids))[:T]))
+    toks = [len(tok.encode(c)) for c in cands]
+    gen = methods.get_method_generator("best_of_n", {"n": N, "seed": 1}, model_id)
+
+    def one_pass():
+        U = gen.score_candidates(SCENARIO_ISSUE, opinions, cands, shard)
+        W = par.combine_welfare(U, "min", shard, nonfinite="replace", nan_val=gen.DEFAULT_REWARD,
+                                posinf_val=gen.REWARD_CLIP_MAX, neginf_val=gen.REWARD_CLIP_MIN)
+        return int(ops.topk(W, 1)[0].item())
+
+    for _ in range(max(1, args.warmup // 2)):
+        one_pass()
+    _barrier_sync(world)
+    steps = max(2, args.steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    _barrier_sync(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    dt = el / steps
+    R.clear_engines()
+    del eng, gen
+    _free()
+    return {"workload": desc + "; product API (BestOfNGenerator.score_candidates + "
+                               "combine_welfare + top-1) on candidate texts, forward included",
+            "scorings_per_s": world * A * N / dt, "s_per_pass": dt, "passes": steps,
+            "candidate_tokens_mean": sum(toks) / len(toks), "model_init_s": init_s,
+            "note": "vs end_to_end: + text encoding, the agents' prompt rendering and the "
+                    "per-(agent, candidate) find() check of the reference's span semantics"}
 
 
 def method_leg_fl(name, args, world, rank, dev):
@@ -1057,6 +1116,11 @@ def main():
     e2e = (guarded("end_to_end", c2_e2e_leg, args, world, rank, dev)
            if args.e2e and args.config == "c2" else None)
     method = {}
+    if args.e2e and args.config == "c2" and args.method_bon:
+        _progress("method_bon.c2")
+        r = guarded("method_bon.c2", method_leg_bon, args, world, rank, dev)
+        if r is not None:
+            method["c2_best_of_n"] = r
     for name in [m for m in args.method.split(",") if m]:
         _progress("method_decode." + name)
         r = guarded("method_decode." + name, method_leg, name, args, world, rank, dev)
