@@ -27,37 +27,8 @@ namespace {
 // Nobody waits on anybody, so the launch cannot stall; the last arrivers reset the
 // counters to zero, which keeps the workspace reusable (and graph-replayable) without
 // a memset.
-// Cross-workgroup hand-off without fences (MI355X_MICROARCH.md, hand-off table row 1):
-// every handed-off byte is stored and loaded with sc1 (agent-scope relaxed atomics lower
-// to global_store/global_load ... sc1: write-through past the L2, L1 bypassed), every
-// storing wave waits vmcnt(0), the workgroup barriers, and ONE lane then adds to the
-// arrival counter; the workgroup whose add returns the last count consumes.
-// Memory-model note: these are RELAXED agent-scope atomics, not release / acquire.  What
-// orders the hand-off is the gfx950 ISA behaviour of the sc1 forms (a store completes,
-// s_waitcnt vmcnt(0), only once it is past the per-XCD L2; an sc1 load bypasses the L1 and
-// reads past the L2), which the HIP memory model does not promise: an agent-scope release
-// here would write back the whole L2 (buffer_wbl2) per arrival, tens of microseconds per
-// step.  The assumption is pinned by tests/test_kernels_gpu.py (the fused launches against
-// the unfused kernels word for word: the fuzz, and the shared-workspace stress of
-// alternating shapes on a busy device and of hipGraph replays), and a failed launch
-// re-zeroes the counters (ops.Workspace.reset).
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_sc1(unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ uint32_t arrive(uint32_t* cnt) {
-  return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
+// The hand-off primitives (st_sc1 / ld_sc1 / wait_stores / arrive) live in
+// cs_kernels.cuh; tests/test_abi.py pins their sc1 lowering on this toolchain.
 // Hand-off regions are padded so that every 128-byte line is read by ONE consumer
 // workgroup, after all of it is published: a line is never in an L2 (per XCD) before its
 // consumer's first read of it in the launch.

@@ -192,3 +192,41 @@ def test_prefix_attention_plan_rejects_bad_arguments(pkg):
     assert _plan(L, [100], None, 4, 1, 30, 8, 128, 32)[0] == -1            # H % Hkv
     assert _plan(L, [100], None, 4, 1, 32, 8, 96, 32)[0] == -1             # head_dim
     assert _plan(L, [100], None, 4, 1, 32, 8, 128, 40)[0] == -1            # ld_hist % 32
+
+
+def test_handoff_primitives_lower_to_sc1(pkg, tmp_path):
+    """The beam kernels' cross-workgroup hand-offs (cs_kernels.cuh st_sc1 / ld_sc1 / arrive)
+    are relaxed agent-scope atomics whose ORDERING rests on their gfx950 lowering: the
+    store and the load must be sc1 (write-through past / read past the per-XCD L2) and
+    the arrival counter a device atomic.  Compile a probe with the library's own flags
+    and check the disassembly, so a toolchain that lowers them otherwise fails here."""
+    import shutil
+    import subprocess
+    from importlib import import_module
+    build = import_module(pkg.__name__ + ".build")
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = tmp_path / "probe.hip"
+    src.write_text('#include "cs_kernels.cuh"\n'
+                   '__global__ void probe(uint32_t* data, uint32_t* cnt, uint32_t* out) {\n'
+                   '  st_sc1(data + threadIdx.x, threadIdx.x);\n'
+                   '  wait_stores();\n'
+                   '  __syncthreads();\n'
+                   '  if (threadIdx.x == 0 && arrive(cnt) == gridDim.x - 1)\n'
+                   '    st_sc1(out + blockIdx.x, ld_sc1(data + 7));\n'
+                   '}\n')
+    asm = tmp_path / "probe.s"
+    flags = [f for f in build._flags() if f != "-fPIC"]
+    subprocess.run([hipcc] + flags + ["--cuda-device-only", "-S", str(src), "-o", str(asm)],
+                   check=True, capture_output=True)
+    text = asm.read_text()
+    body = text[text.index("probe"):]
+    stores = [l for l in body.splitlines() if l.strip().startswith("global_store_dword")]
+    loads = [l for l in body.splitlines() if l.strip().startswith("global_load_dword")]
+    atomics = [l for l in body.splitlines() if l.strip().startswith("global_atomic_add")]
+    assert stores and all("sc1" in l for l in stores), stores
+    assert loads and all("sc1" in l for l in loads), loads
+    assert atomics, "the arrival counter must be one device atomic"
+    assert "s_waitcnt vmcnt(0)" in body
+    shutil.rmtree(tmp_path, ignore_errors=True)
