@@ -112,8 +112,8 @@ def load():
     L.cs_rope_place.argtypes = [vp, i64, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp,
                                 i64, vp]
     L.cs_rope_place.restype = ctypes.c_int
-    L.cs_add_rms_norm.argtypes = [vp, i64, vp, i64, vp, i64, vp, i64, i64, f32, ctypes.c_int, vp,
-                                  i64, vp]
+    L.cs_add_rms_norm.argtypes = [vp, i64, vp, i64, vp, vp, i64, vp, i64, i64, f32, ctypes.c_int,
+                                  vp, i64, vp]
     L.cs_add_rms_norm.restype = ctypes.c_int
     L.cs_gated_act.argtypes = [vp, i64, vp, i64, i64, i64, ctypes.c_int, vp, i64, vp]
     L.cs_gated_act.restype = ctypes.c_int

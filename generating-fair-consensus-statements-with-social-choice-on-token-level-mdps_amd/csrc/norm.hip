@@ -29,16 +29,65 @@ __device__ __forceinline__ uint16_t to_bf(float f) {
 
 constexpr int kNormThreads = 256;
 
+// the row's sum over the workgroup: wave64 butterfly, then the 4 wave sums in wave order
+// (the same order everywhere, so a norm is bitwise the same in every kernel that uses it)
+__device__ __forceinline__ float row_sum(float ss, float* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  float tot = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kNormThreads / 64; ++i) tot += red[i];
+  return tot;
+}
+
 // one workgroup per row; VPT 16-byte vectors per thread (d <= 256 * 8 * VPT).  s_out may
 // alias a (the residual stream updated in place): every element is loaded before the
-// barrier and stored after it by the same thread.
+// barrier and stored after it by the same thread.  wb != nullptr: the branch b is first
+// RMS-normalised itself with weight wb (Gemma-2's post-attention / post-MLP norm), with
+// the arithmetic and rounding of a separate add_rms launch over b alone.
 template <int VPT>
 __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
     const uint16_t* a, int64_t lda, const uint16_t* __restrict__ b, int64_t ldb,
-    uint16_t* s_out, int64_t lds, const uint16_t* __restrict__ w, int64_t d,
-    float eps, int plus_one, uint16_t* __restrict__ y, int64_t ldy) {
+    const uint16_t* __restrict__ wb, uint16_t* s_out, int64_t lds,
+    const uint16_t* __restrict__ w, int64_t d, float eps, int plus_one,
+    uint16_t* __restrict__ y, int64_t ldy) {
   const int64_t r = blockIdx.x;
   const int nv = static_cast<int>(d >> 3);
+  __shared__ float red[2][kNormThreads / 64];
+  u16x8 bv[VPT];
+  if (b) {
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int v = threadIdx.x + k * kNormThreads;
+      if (v < nv) bv[k] = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
+    }
+    if (wb) {
+      float sb = 0.0f;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int v = threadIdx.x + k * kNormThreads;
+        if (v < nv) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sb = fmaf(bf(bv[k][e]), bf(bv[k][e]), sb);
+        }
+      }
+      const float inv_b = 1.0f / sqrtf(row_sum(sb, red[0]) / static_cast<float>(d) + eps);
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int v = threadIdx.x + k * kNormThreads;
+        if (v < nv) {
+          const u16x8 wv = *reinterpret_cast<const u16x8*>(wb + 8 * v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float g = plus_one ? 1.0f + bf(wv[e]) : bf(wv[e]);
+            bv[k][e] = to_bf((bf(bv[k][e]) * inv_b) * g);
+          }
+        }
+      }
+    }
+  }
   u16x8 sv[VPT];
   float ss = 0.0f;
 #pragma unroll
@@ -47,24 +96,15 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
     if (v < nv) {
       u16x8 x = *reinterpret_cast<const u16x8*>(a + r * lda + 8 * v);
       if (b) {
-        const u16x8 o = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = to_bf(bf(x[e]) + bf(o[e]));
+        for (int e = 0; e < 8; ++e) x[e] = to_bf(bf(x[e]) + bf(bv[k][e]));
       }
       sv[k] = x;
 #pragma unroll
       for (int e = 0; e < 8; ++e) ss = fmaf(bf(x[e]), bf(x[e]), ss);
     }
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
-  __shared__ float red[kNormThreads / 64];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-  __syncthreads();
-  float tot = 0.0f;
-#pragma unroll
-  for (int i = 0; i < kNormThreads / 64; ++i) tot += red[i];
-  const float inv = 1.0f / sqrtf(tot / static_cast<float>(d) + eps);
+  const float inv = 1.0f / sqrtf(row_sum(ss, red[1]) / static_cast<float>(d) + eps);
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int v = threadIdx.x + k * kNormThreads;
@@ -112,12 +152,13 @@ __global__ __launch_bounds__(kNormThreads) void gated_act_kernel(
 
 extern "C" {
 
-int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, void* s_out,
-                    int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
+int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, const void* b_weight,
+                    void* s_out, int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
                     int plus_one, void* y, int64_t ldy, cs_stream_t stream) {
   if (rows < 0 || d <= 0) return fail(CS_ERR_INVALID, "cs_add_rms_norm: bad shape");
   if (rows == 0) return CS_OK;
   if (!a || !weight || !y) return fail(CS_ERR_INVALID, "cs_add_rms_norm: NULL pointer");
+  if (b_weight && !b) return fail(CS_ERR_INVALID, "cs_add_rms_norm: b_weight without b");
   if (d % 8 != 0 || d > 16 * 8 * kNormThreads)
     return fail(CS_ERR_INVALID, "cs_add_rms_norm: d must be a multiple of 8 and <= 32768");
   if (lda < d || ldy < d || (b && ldb < d) || (s_out && lds < d) || lda % 8 || ldy % 8 ||
@@ -125,6 +166,7 @@ int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, void
     return fail(CS_ERR_INVALID, "cs_add_rms_norm: leading dimensions must be >= d and multiples of 8");
   const uint16_t* A = static_cast<const uint16_t*>(a);
   const uint16_t* B = static_cast<const uint16_t*>(b);
+  const uint16_t* WB = static_cast<const uint16_t*>(b_weight);
   uint16_t* S = static_cast<uint16_t*>(s_out);
   const uint16_t* W = static_cast<const uint16_t*>(weight);
   uint16_t* Y = static_cast<uint16_t*>(y);
@@ -132,17 +174,17 @@ int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, void
   const int nv = static_cast<int>(d / 8);
   const dim3 grid(static_cast<uint32_t>(rows));
   if (nv <= kNormThreads) {
-    hipLaunchKernelGGL(add_rms_kernel<1>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
-                       d, eps, plus_one, Y, ldy);
+    hipLaunchKernelGGL(add_rms_kernel<1>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
+                       W, d, eps, plus_one, Y, ldy);
   } else if (nv <= 2 * kNormThreads) {
-    hipLaunchKernelGGL(add_rms_kernel<2>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
-                       d, eps, plus_one, Y, ldy);
+    hipLaunchKernelGGL(add_rms_kernel<2>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
+                       W, d, eps, plus_one, Y, ldy);
   } else if (nv <= 4 * kNormThreads) {
-    hipLaunchKernelGGL(add_rms_kernel<4>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
-                       d, eps, plus_one, Y, ldy);
+    hipLaunchKernelGGL(add_rms_kernel<4>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
+                       W, d, eps, plus_one, Y, ldy);
   } else {
-    hipLaunchKernelGGL(add_rms_kernel<16>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, S, lds, W,
-                       d, eps, plus_one, Y, ldy);
+    hipLaunchKernelGGL(add_rms_kernel<16>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
+                       W, d, eps, plus_one, Y, ldy);
   }
   return check_launch("cs_add_rms_norm");
 }

@@ -73,7 +73,11 @@ class StatementEvaluator:
         for a, op in enumerate(agent_opinions.values()):
             system = EVAL_SYSTEM.format(issue=issue, opinion=op)
             for si, st in enumerate(statements):
-                if not utils.span_found_at_user(tok, system, st):
+                where = utils.span_check(tok, system, st)
+                if where == utils.SPAN_NONE:      # the reference's call returns ([], [])
+                    avg_lp[a, si] = float("nan")
+                    avg_p[a, si] = float("nan")
+                elif where == utils.SPAN_ELSEWHERE:
                     m_lp, m_p, _ = utils.text_compat_mean(self.evaluation_model, system, st)
                     avg_lp[a, si] = m_lp
                     avg_p[a, si] = m_p

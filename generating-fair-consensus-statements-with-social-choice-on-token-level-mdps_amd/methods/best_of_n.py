@@ -120,7 +120,10 @@ class BestOfNGenerator(BaseGenerator):
         for a, op in enumerate(mine):
             system = BON["agent_system"] + "\n\n" + BON["agent_user"].format(issue=issue, opinion=op)
             for c, cand in enumerate(cands):
-                if not utils.span_found_at_user(tok, system, cand):
+                where = utils.span_check(tok, system, cand)
+                if where == utils.SPAN_NONE:          # the reference's call returns ([], [])
+                    U[a, c] = self.DEFAULT_REWARD
+                elif where == utils.SPAN_ELSEWHERE:
                     m_lp, _, n_ok = utils.text_compat_mean(self.model_identifier, system, cand)
                     U[a, c] = m_lp if n_ok else self.DEFAULT_REWARD
         U = U.contiguous()

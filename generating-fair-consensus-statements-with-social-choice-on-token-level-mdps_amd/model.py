@@ -420,15 +420,15 @@ class Model:
                                      prefix_len_host=getattr(pfx, "lens_host", None),
                                      group_prefix_host=group_prefix_host)
             o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"])
-            if g2:
-                o = ops.add_rms_norm(o, self.w[p + "post_attn_norm"], eps, plus_one=True)
-            x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2)
+            # Gemma-2's post-attention / post-MLP norms of the branch ride in the residual
+            # add's launch (b_weight): one cs_add_rms_norm per residual add
+            x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2,
+                                 b_weight=self.w[p + "post_attn_norm"] if g2 else None)
             y = ops.linear(ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act),
                            self.w[p + "w_down"])
-            if g2:
-                y = ops.add_rms_norm(y, self.w[p + "post_mlp_norm"], eps, plus_one=True)
             nxt = self.w[f"l{i + 1}.attn_norm"] if i + 1 < c.n_layers else self.w["norm"]
-            x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2)
+            x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2,
+                                 b_weight=self.w[p + "post_mlp_norm"] if g2 else None)
         return x
 
 

@@ -651,10 +651,13 @@ def _rows2d(t: torch.Tensor, name: str):
 
 
 def add_rms_norm(a: torch.Tensor, weight: torch.Tensor, eps: float, *, b: Optional[torch.Tensor] = None,
-                 plus_one: bool = False, s_out: Optional[torch.Tensor] = None,
+                 b_weight: Optional[torch.Tensor] = None, plus_one: bool = False,
+                 s_out: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = RMSNorm(a + b) (cs_add_rms_norm); the bf16 sum a + b is also written to s_out.
-    a, b, s_out, out [rows, d] bf16; weight [d] bf16 (Gemma-2: plus_one, 1 + weight)."""
+    a, b, s_out, out [rows, d] bf16; weight [d] bf16 (Gemma-2: plus_one, 1 + weight).
+    b_weight: b is RMS-normalised first with that weight (Gemma-2's post norms), bitwise as
+    add_rms_norm(b, b_weight) followed by this call."""
     L = _lib.load()
     lda = _rows2d(a, "a")
     rows, d = a.shape
@@ -664,11 +667,15 @@ def add_rms_norm(a: torch.Tensor, weight: torch.Tensor, eps: float, *, b: Option
         raise CSError("a, b and s_out must share one shape")
     if weight.dtype != torch.bfloat16 or weight.numel() != d or not weight.is_contiguous():
         raise CSError("weight must be a contiguous bfloat16 [d] tensor")
+    if b_weight is not None and (b is None or b_weight.dtype != torch.bfloat16 or
+                                 b_weight.numel() != d or not b_weight.is_contiguous()):
+        raise CSError("b_weight must be a contiguous bfloat16 [d] tensor and needs b")
     if out is None:
         out = torch.empty_like(a, memory_format=torch.contiguous_format)
     ldy = _rows2d(out, "out")
     _require_cuda(a, b, s_out, weight, out)
     rc = L.cs_add_rms_norm(a.data_ptr(), lda, b.data_ptr() if b is not None else None, ldb,
+                           b_weight.data_ptr() if b_weight is not None else None,
                            s_out.data_ptr() if s_out is not None else None, lds, weight.data_ptr(),
                            rows, d, float(eps), int(bool(plus_one)), out.data_ptr(), ldy, _stream())
     _lib.check(rc, "cs_add_rms_norm")

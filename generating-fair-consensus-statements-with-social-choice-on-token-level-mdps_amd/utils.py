@@ -131,15 +131,37 @@ def last_user_span_index(tokens: Sequence[str], user_prompt: str) -> int:
     return bisect.bisect_left(ends, lo + len(user_prompt))
 
 
+SPAN_AT_USER, SPAN_NONE, SPAN_ELSEWHERE = 1, 0, -1
+
+
+def span_check(tok, system_prompt, user_prompt) -> int:
+    """Where the reference's first-occurrence ``find`` of the user prompt lands in the
+    rendered prompt's token strings (src/utils.py:321-327): SPAN_AT_USER (the user turn
+    itself: the batched engine path holds the reference's value), SPAN_NONE (nowhere: the
+    reference's call returns ([], []) and its caller takes its fallback reward -- e.g. a
+    candidate with leading whitespace the chat template trims), SPAN_ELSEWHERE (e.g. a
+    one-word statement that also occurs in the system text: the text-compat path).
+    An ASCII prompt's token strings join to the rendered text itself, so SPAN_NONE is
+    decided by one string search there, without encoding."""
+    api_user = user_prompt + MARKER if user_prompt.endswith(("\n", " ")) else user_prompt
+    chat_text = getattr(tok, "chat_text", None)
+    if chat_text is not None:
+        text = chat_text(system_prompt or None, api_user, True)
+        if text.isascii() and text.find(user_prompt) == -1:
+            return SPAN_NONE
+    ids, (start, _) = tok.render_chat(system_prompt or None, api_user)
+    text = "".join(tok.tokens(ids))
+    lo = text.find(user_prompt)
+    if lo == -1:
+        return SPAN_NONE
+    return SPAN_AT_USER if lo == len("".join(tok.tokens(ids[:start]))) else SPAN_ELSEWHERE
+
+
 def span_found_at_user(tok, system_prompt, user_prompt) -> bool:
     """True when the reference's first-occurrence ``find`` of the user prompt lands on the
     user turn itself (src/utils.py:321-327).  False means the reference scores a span
-    elsewhere in the prompt (e.g. a one-word statement that also occurs in the system
-    text); callers then take the text-compat path to stay result-identical."""
-    api_user = user_prompt + MARKER if user_prompt.endswith(("\n", " ")) else user_prompt
-    ids, (start, _) = tok.render_chat(system_prompt or None, api_user)
-    text = "".join(tok.tokens(ids))
-    return text.find(user_prompt) == len("".join(tok.tokens(ids[:start])))
+    elsewhere in the prompt, or none; callers then take the text-compat path."""
+    return span_check(tok, system_prompt, user_prompt) == SPAN_AT_USER
 
 
 def text_compat_mean(model, system_prompt, user_prompt):
@@ -173,8 +195,8 @@ def user_span_sums(model, systems: Sequence[Optional[str]], users: Sequence[str]
 def _user_span_sums(engine, tok, systems, users, device_out):
     n = len(users)
     out = torch.full((n,), float("nan"), dtype=torch.float64)
-    fast = [i for i in range(n) if users[i] and span_found_at_user(tok, systems[i], users[i])]
-    fast_set = set(fast)
+    where = [span_check(tok, systems[i], users[i]) if users[i] else SPAN_NONE for i in range(n)]
+    fast = [i for i in range(n) if where[i] == SPAN_AT_USER]
     if fast:
         keys, owner, uniq = {}, [], []
         for i in fast:
@@ -194,7 +216,8 @@ def _user_span_sums(engine, tok, systems, users, device_out):
         if device_out and len(fast) == n:
             return sums
         out[torch.as_tensor(fast)] = sums.cpu()
-    slow = [i for i in range(n) if i not in fast_set and users[i]]
+    # SPAN_NONE pairs stay NaN: the reference's call returns ([], [])
+    slow = [i for i in range(n) if where[i] == SPAN_ELSEWHERE]
     if slow:
         vals = text_compat_span_sums(engine, tok, [systems[i] for i in slow],
                                      [users[i] for i in slow])

@@ -370,17 +370,20 @@ int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
 
 /*
  * cs_add_rms_norm — residual add + RMSNorm of bf16 rows in one pass:
- *     s = a + b (rounded to bf16; b NULL = none), written to s_out when non-NULL (may alias a)
+ *     b' = b, or with b_weight: b' = b * rsqrt(mean(b^2) + eps) * g_b (rounded to bf16; the
+ *          branch's own norm, Gemma-2's post-attention / post-MLP norm, bitwise as a
+ *          separate cs_add_rms_norm over b alone)
+ *     s = a + b' (rounded to bf16; b NULL = none), written to s_out when non-NULL (may alias a)
  *     y = s * rsqrt(mean(s^2) + eps) * g,  g = weight (plus_one = 0, Llama-3) or
- *         1 + weight (plus_one = 1, Gemma-2); fp32 statistics, one rounding.
+ *         1 + weight (plus_one = 1, Gemma-2; also g_b); fp32 statistics, one rounding.
  * d a multiple of 8 (<= 32768), leading dimensions multiples of 8.
  *
  * Replaces: part of the remote forward behind every get_prompt_logprobs call
  *   (src/utils.py:249-259) — the per-layer residual + normalisation of each new token.
  */
-int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, void* s_out,
-                    int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
-                    int plus_one, void* y, int64_t ldy, cs_stream_t stream);
+int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, const void* b_weight,
+                    void* s_out, int64_t lds, const void* weight, int64_t rows, int64_t d,
+                    float eps, int plus_one, void* y, int64_t ldy, cs_stream_t stream);
 
 /*
  * cs_gated_act — the gated MLP activation of bf16 rows: out = act(gate) * up with act =

@@ -368,6 +368,25 @@ def test_add_rms_norm_matches_torch(ops, dev, plus_one, d, with_b):
     assert float(diff.max()) <= float(y_ref.float().abs().max()) * 2 ** -7
 
 
+@pytest.mark.parametrize("plus_one,d", [(True, 3584), (True, 256), (False, 2048), (True, 8192)])
+def test_add_rms_norm_branch_prenorm_is_the_two_launches(ops, dev, plus_one, d):
+    """b_weight (Gemma-2's post-attention / post-MLP norm of the branch) inside the residual
+    add's launch is bitwise the separate launch over the branch followed by the add + norm."""
+    g = torch.Generator(device="cpu").manual_seed(d + 1)
+    rows = 41
+    a = (torch.randn(rows, d, generator=g) * 2).to(torch.bfloat16).to(dev)
+    b = (torch.randn(rows, d, generator=g) * 3).to(torch.bfloat16).to(dev)
+    wb = (torch.randn(d, generator=g) * 0.1).to(torch.bfloat16).to(dev)
+    w = (torch.randn(d, generator=g) * 0.1).to(torch.bfloat16).to(dev)
+    a_two, a_one = a.clone(), a.clone()
+    bn = ops.add_rms_norm(b, wb, 1e-6, plus_one=plus_one)
+    y_two = ops.add_rms_norm(a_two, w, 1e-6, b=bn, s_out=a_two, plus_one=plus_one)
+    y_one = ops.add_rms_norm(a_one, w, 1e-6, b=b, b_weight=wb, s_out=a_one, plus_one=plus_one)
+    torch.cuda.synchronize()
+    assert torch.equal(a_one, a_two)
+    assert torch.equal(y_one, y_two)
+
+
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
 def test_gated_act_matches_torch(ops, dev, act):
     import torch.nn.functional as F
