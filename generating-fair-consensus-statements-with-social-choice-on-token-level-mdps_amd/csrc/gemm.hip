@@ -373,8 +373,17 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
       }
     }
   };
-  auto sync = [&]() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
+  // the step's wait names the W set it releases as read-write operands: the MFMAs consume
+  // the wait's outputs, so the compiler cannot copy or move an asm-loaded register before
+  // its data has landed (cdna_hip_programming.md §5.7 item 1, form (ii))
+  auto sync = [&](gbf16x8 (&w)[NT][2]) {
+    if constexpr (NT == 1) {
+      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(w[0][0]), "+v"(w[0][1]) : "n"(kWait) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%4)"
+                   : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1])
+                   : "n"(kWait) : "memory");
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -392,7 +401,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   issue_x(1, 1);
   load_w(w2, 2);
 #define CS_WS2_STEP(T, B, WB)        \
-  sync();                            \
+  sync(WB);                          \
   issue_x((T) + 2, ((B) + 2) % 3);   \
   if ((T) < nk) compute(B, WB);      \
   load_w(WB, (T) + 3);

@@ -47,7 +47,11 @@ FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
             # scenario's 4 opinions cycled and tagged per participant, as bench.py's
             # synthetic_opinions), beam width 8 (the top of the main-body sweep
             # configs/main_body/scenario_1.yaml beam_width [2, 4, 6, 8]), BoN N = 8, FL bf 3
-            "wide": ("tiny-gemma-wide-fixture", "method_traces_wide.json")}
+            "wide": ("tiny-gemma-wide-fixture", "method_traces_wide.json"),
+            # C1 at its full horizon: the same Llama-3.2-1B-shaped fixture, beam 4 x 8
+            # attempts over 50 tokens (configs/appendix/llama/scenario_1/beam_search.yaml:33-38
+            # max_tokens 50): beams whose histories span two 32-slot tiles
+            "c1long": ("llama-3.2-1b-shaped-fixture", "method_traces_c1_long.json")}
 BPE_DIR = os.path.join(HERE, "bpe_fixture")
 # untied LM head: with the random tied embedding a shallow model's residual stream makes
 # the last token's own logit ~45 sigma above the rest (every draw repeats it); an
@@ -62,7 +66,7 @@ def fixture_model(family: str = "llama3"):
     """The seeded fixture model (CPU fp32) and tokenizer shared by both sides."""
     Mm = importlib.import_module(PKG + ".model")
     T = importlib.import_module(PKG + ".tokenizer")
-    if family == "c1":
+    if family in ("c1", "c1long"):
         cfg = Mm.preset("llama-3.2-1b", **C1_OVERRIDES)
         tok = T.CharTokenizer("llama3", vocab_size=cfg.vocab)
     elif family == "bpe":
@@ -86,6 +90,12 @@ C1_RUNS = [
                    "log_level": "WARNING"}),
     ("finite_lookahead", {"branching_factor": 3, "max_depth": 2, "max_tokens": 3, "seed": 11,
                           "api_delay": 0, "log_level": "WARNING"}),
+]
+
+
+C1_LONG_RUNS = [
+    ("beam_search", {"beam_width": 4, "max_tokens": 50, "max_sampling_attempts": 8, "seed": 1,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
 ]
 
 
@@ -170,17 +180,18 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
-           "family": ("llama3" if args.family in ("c1", "bpe")
+           "family": ("llama3" if args.family in ("c1", "c1long", "bpe")
                       else "gemma2" if args.family == "wide" else args.family),
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
-    if args.family == "c1":
+    if args.family in ("c1", "c1long"):
         out["preset_overrides"] = dict(C1_OVERRIDES)
         out["tokenizer_vocab"] = cfg.vocab
     if args.family == "bpe":
         out["tokenizer"] = "bpe_fixture"
     if args.family == "wide":
         out["preset_overrides"] = dict(WIDE_OVERRIDES)
-    runs = (C1_RUNS if args.family == "c1" else BPE_RUNS if args.family == "bpe"
+    runs = (C1_RUNS if args.family == "c1" else C1_LONG_RUNS if args.family == "c1long"
+            else BPE_RUNS if args.family == "bpe"
             else WIDE_RUNS if args.family == "wide" else None) or [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,
                        "log_level": "WARNING"}),
