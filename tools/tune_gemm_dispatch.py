@@ -66,6 +66,7 @@ def main() -> int:
     ap.add_argument("--configs", default="c1,c3,c5")
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--install", action="store_true")
+    ap.add_argument("--variants", default="2,3,4")
     args = ap.parse_args()
     print("tuning:", R.use_gemm_tuning(), file=sys.stderr)
     dev = torch.device("cuda:0")
@@ -94,9 +95,9 @@ def main() -> int:
                 t_torch = timed(tfn) / calls * 1e3
                 best = ("torch", 0, 0, t_torch)
                 cands = []
-                for var in (2, 3, 4):
+                for var in map(int, args.variants.split(",")):
                     for sp in ((1,) if gated else (1, 2, 4, 8, 16)):
-                        if K % (64 * sp) or K // (64 * sp) < 2 or (var in (2, 4) and N % 256):
+                        if K % (64 * sp) or K // (64 * sp) < 2 or (var in (2, 4, 5) and N % 256):
                             continue
                         t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), act=act,
                                                     splits=sp, variant=var)
