@@ -636,6 +636,7 @@ def method_leg(name, args, world, rank, dev):
         out["retokenize_text"] = {
             "ms_per_step": ms, "steps": gen.steps_run, "decode_path": gen.decode_path,
             "rescored_candidates": gen.text_compat_candidates, "candidates": n_cand,
+            "from_decode_rows": gen.text_rows_candidates,
             "prefix_reuse": dict(eng.reuse_stats),
             "note": "the reference's re-tokenized last log-prob (product default): candidates "
                     "whose BPE re-tokenization differs from the id append are re-scored on the "

@@ -391,6 +391,14 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // the loads of the last steps are never consumed: their registers stay allocated (named
+  // as read-write operands) until the final vmcnt(0), or the compiler hands them to the
+  // epilogue while the data is still in flight (a landing load overwrote an address)
+  auto hold = [&](gbf16x8 (&w)[NT][2]) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(w[j][0]), "+v"(w[j][1]));
+  };
+
   // Step t: X(t) in LDS buffer t % 3, W(t) in register set t % 3.  It waits for X(t) (and
   // the older W(t)) with the loads of steps t - 2 and t - 1 after it still in flight, passes
   // the barrier (every wave done with step t - 1, so buffer (t + 2) % 3 — read in step
@@ -414,6 +422,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
       CS_WS2_STEP(t + 2, 2, w2)
     }
 #undef CS_WS2_STEP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
+    hold(w0);
+    hold(w1);
+    hold(w2);
   } else {
     // W two steps ahead (two register sets): the registers it frees feed the B-fragment
     // ring of compute(); LDS buffer t % 3 and W set t % 2 -> six steps per iteration
@@ -436,8 +448,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
       CS_WS2_STEP(t + 5, 2, w1)
     }
 #undef CS_WS2_STEP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hold(w0);
+    hold(w1);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
 
 #pragma unroll
   for (int i = 0; i < MT; ++i) {

@@ -14,7 +14,8 @@ reference's ``extract_user_prompt_logprobs`` relies on (``"".join(tokens)``).
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, List, Sequence
+import operator
+from typing import Dict, Iterable, List, Optional, Sequence
 
 LLAMA3_SPECIALS = ["<|begin_of_text|>", "<|end_of_text|>", "<|start_header_id|>",
                    "<|end_header_id|>", "<|eot_id|>"]
@@ -229,6 +230,7 @@ class BPETokenizer:
         self.n_table = self.tk.get_vocab_size(with_added_tokens=True)
         self.full_vocab = max(int(vocab_size), self.n_table)
         self._strs: Dict[int, str] = {}
+        self._table: Optional[List[str]] = None
         self._jinja = None
 
     @property
@@ -256,6 +258,12 @@ class BPETokenizer:
         return s
 
     def tokens(self, ids: Sequence[int]) -> List[str]:
+        table = self._table
+        if table is None:     # every table id's string, decoded once (C-speed lookups after)
+            table = self._table = [self.token_str(i) for i in range(self.n_table)]
+        ids = list(ids)
+        if len(ids) > 1 and 0 <= min(ids) and max(ids) < self.n_table:
+            return list(operator.itemgetter(*ids)(table))
         return [self.token_str(i) for i in ids]
 
     def decode(self, ids: Iterable[int]) -> str:

@@ -275,24 +275,39 @@ def text_compat_last(engine, tok, systems: Sequence[Optional[str]],
     its except branch does (:397-404)."""
     n = len(users)
     res = [float(fallback)] * n
-    idss, last = [], []
+    idss, last = [[] for _ in range(n)], [-1] * n
     apis = [u + MARKER if u.endswith(("\n", " ")) else u for u in users]
-    many = getattr(tok, "render_chat_ids_many", None)
-    rendered = None
-    if many is not None:
-        try:    # one batched (multi-threaded) encode of every rendered prompt
-            rendered = many([s or None for s in systems], apis)
-        except Exception:   # noqa: BLE001 -- per-call path below reports the failure
-            rendered = None
-    for j, (s, u) in enumerate(zip(systems, users)):
+    # an ASCII prompt's token strings join to the rendered text itself: a user prompt that
+    # text does not contain is found nowhere (the reference's call gives ([], []) and the
+    # fallback), decided without encoding -- the common case of re-scored beam candidates
+    # whose statement begins with whitespace the chat template trims
+    live = list(range(n))
+    chat_text = getattr(tok, "chat_text", None)
+    texts = None
+    if chat_text is not None:
         try:
-            ids = rendered[j] if rendered is not None else tok.render_chat(s or None, apis[j])[0]
-            k = last_user_span_index(tok.tokens(ids), u)
+            texts = [chat_text(s or None, a, True) for s, a in zip(systems, apis)]
+            live = [j for j in range(n)
+                    if not (texts[j].isascii() and texts[j].find(users[j]) == -1)]
+        except Exception:   # noqa: BLE001 -- per-call path below reports the failure
+            texts, live = None, list(range(n))
+    rendered = None
+    many = getattr(tok, "encode_many", None) if texts is not None else None
+    if live and many is not None:
+        try:    # one batched (multi-threaded) encode of the prompts left
+            rendered = dict(zip(live, many([texts[j] for j in live])))
+        except Exception:   # noqa: BLE001
+            rendered = None
+    for j in live:
+        try:
+            ids = (rendered[j] if rendered is not None
+                   else tok.render_chat(systems[j] or None, apis[j])[0])
+            k = last_user_span_index(tok.tokens(ids), users[j])
         except Exception as e:       # get_prompt_logprobs would return ([], [])
             logger.error("get_prompt_logprobs failed: %s", e)
             ids, k = [], -1
-        idss.append(list(ids))
-        last.append(k)
+        idss[j] = list(ids)
+        last[j] = k
     todo = [j for j in range(n) if last[j] > 0]      # position 0 has no log-prob (None)
     if not todo:
         return res
