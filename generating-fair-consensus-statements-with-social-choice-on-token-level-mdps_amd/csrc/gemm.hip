@@ -251,7 +251,7 @@ __device__ __forceinline__ gbf16x8 asm_load16(const uint16_t* p) {
 // W goes to registers through inline-asm loads, so the compiler's waits never drain the
 // DMA queue: one counted s_waitcnt vmcnt per step (this step's X and W landed, the next
 // two steps' loads still in flight) + a raw s_barrier.
-template <int MT, int NT, int GATED, int WAVES, int WD = 3>
+template <int MT, int NT, int GATED, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
     const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
     uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
@@ -262,9 +262,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   constexpr int kG = (kPieces + WAVES - 1) / WAVES;   // DMA instructions per wave per stage
   constexpr int kBN = 16 * NT * WAVES;
   constexpr int kHalf = NT / 2;                 // gated: tiles [0, kHalf) gate, [kHalf, NT) up
-  // loads issued after the older of X(t), W(t) when step t starts: WD = 3 -> W(t + 1),
-  // X(t + 1), W(t + 2) after X(t); WD = 2 -> X(t + 1), W(t + 1) after W(t)
-  constexpr int kWait = WD == 3 ? kG + 4 * NT : kG + 2 * NT;
+  // loads issued after the older of X(t), W(t) when step t starts: W(t + 1), X(t + 1),
+  // W(t + 2) after X(t)
+  constexpr int kWait = kG + 4 * NT;
   static_assert(!GATED || NT % 2 == 0, "the gated form pairs gate and up column tiles");
   __shared__ __align__(16) unsigned char lds[3 * kStage];
 
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   };
   auto compute = [&](int buf, const gbf16x8 (&w)[NT][2]) {
     const unsigned char* base = lds + buf * kStage;
-    if constexpr (MT > 9 && WD == 3) {   // 2 waves per SIMD, no registers left for a ring
+    if constexpr (MT > 9) {   // 2 waves per SIMD, no registers left for a ring
 #pragma unroll
       for (int q = 0; q < kQ; ++q) {
         const gbf16x8 xf = frag(base, q);
@@ -404,54 +404,27 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   // the barrier (every wave done with step t - 1, so buffer (t + 2) % 3 — read in step
   // t - 1 — is free), issues X(t + 2) into it, computes, then loads W(t + 3) into the set
   // it used: W (HBM) three steps ahead, X (L2) two.
-  if constexpr (WD == 3) {
-    gbf16x8 w0[NT][2], w1[NT][2], w2[NT][2];
-    load_w(w0, 0);
-    issue_x(0, 0);
-    load_w(w1, 1);
-    issue_x(1, 1);
-    load_w(w2, 2);
+  gbf16x8 w0[NT][2], w1[NT][2], w2[NT][2];
+  load_w(w0, 0);
+  issue_x(0, 0);
+  load_w(w1, 1);
+  issue_x(1, 1);
+  load_w(w2, 2);
 #define CS_WS2_STEP(T, B, WB)        \
   sync(WB);                          \
   issue_x((T) + 2, ((B) + 2) % 3);   \
   if ((T) < nk) compute(B, WB);      \
   load_w(WB, (T) + 3);
-    for (int t = 0; t < nk; t += 3) {
-      CS_WS2_STEP(t, 0, w0)
-      CS_WS2_STEP(t + 1, 1, w1)
-      CS_WS2_STEP(t + 2, 2, w2)
-    }
-#undef CS_WS2_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
-    hold(w0);
-    hold(w1);
-    hold(w2);
-  } else {
-    // W two steps ahead (two register sets): the registers it frees feed the B-fragment
-    // ring of compute(); LDS buffer t % 3 and W set t % 2 -> six steps per iteration
-    gbf16x8 w0[NT][2], w1[NT][2];
-    issue_x(0, 0);
-    load_w(w0, 0);
-    issue_x(1, 1);
-    load_w(w1, 1);
-#define CS_WS2_STEP(T, B, WB)        \
-  sync(WB);                          \
-  issue_x((T) + 2, ((B) + 2) % 3);   \
-  if ((T) < nk) compute(B, WB);      \
-  load_w(WB, (T) + 2);
-    for (int t = 0; t < nk; t += 6) {
-      CS_WS2_STEP(t, 0, w0)
-      CS_WS2_STEP(t + 1, 1, w1)
-      CS_WS2_STEP(t + 2, 2, w0)
-      CS_WS2_STEP(t + 3, 0, w1)
-      CS_WS2_STEP(t + 4, 1, w0)
-      CS_WS2_STEP(t + 5, 2, w1)
-    }
-#undef CS_WS2_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    hold(w0);
-    hold(w1);
+  for (int t = 0; t < nk; t += 3) {
+    CS_WS2_STEP(t, 0, w0)
+    CS_WS2_STEP(t + 1, 1, w1)
+    CS_WS2_STEP(t + 2, 2, w2)
   }
+#undef CS_WS2_STEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
+  hold(w0);
+  hold(w1);
+  hold(w2);
 
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -557,23 +530,23 @@ void ws2_rows(int64_t M, int* mt, int64_t* mblocks, int max_tiles = 18) {
   *mblocks = (tiles + v - 1) / v;
 }
 
-template <int MT, int NT, int GATED, int WAVES, int WD>
+template <int MT, int NT, int GATED, int WAVES>
 void launch_ws2(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
                 int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
                 int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
-  hipLaunchKernelGGL((ws2_gemm_kernel<MT, NT, GATED, WAVES, WD>), dim3(blocks), dim3(64 * WAVES), 0, st,
+  hipLaunchKernelGGL((ws2_gemm_kernel<MT, NT, GATED, WAVES>), dim3(blocks), dim3(64 * WAVES), 0, st,
                      X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act,
                      m_blocks);
 }
 
-template <int NT, int GATED, int WAVES, int WD = 3>
+template <int NT, int GATED, int WAVES>
 void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
                   const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M,
                   int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act,
                   int m_blocks) {
 #define CS_WS2_CASE(V)                                                                          \
   case V:                                                                                       \
-    launch_ws2<V, NT, GATED, WAVES, WD>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, \
+    launch_ws2<V, NT, GATED, WAVES>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, \
                                     n_tiles, splits, act, m_blocks);                            \
     break;
   switch (mt) {
@@ -585,8 +558,7 @@ void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t
 }
 
 // W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16;
-// 4: as 2 with at most 9 row tiles (144 rows) per workgroup; 5: as 2 with W two K steps
-// ahead and a B-fragment register ring)
+// 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
 int64_t variant_bn(int variant, int gated) {
   if (variant == 1) return 128;
   if (variant == 3 && !gated) return 128;
@@ -613,7 +585,7 @@ int64_t ws2_grid(int64_t cells, int64_t mblocks) {
 
 int resolve_variant(int variant, int64_t N, int gated) {
   if (variant == 0) variant = 2;
-  if ((variant == 2 || variant == 4 || variant == 5) && N % 256) variant = gated ? 1 : 3;
+  if ((variant == 2 || variant == 4) && N % 256) variant = gated ? 1 : 3;
   if (variant == 3 && gated) variant = 2;
   return variant;
 }
@@ -639,7 +611,7 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
   if (M == 0) return CS_OK;
   if (!x || !w || !y) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
-  if (variant < 0 || variant > 5) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..5");
+  if (variant < 0 || variant > 4) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..4");
   if (N % 128) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
   if (gated && splits > 1)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
@@ -681,15 +653,9 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
     const int b = static_cast<int>(grid);
     const int mbi = static_cast<int>(mb);
-    if (gated && variant == 5) {
-      dispatch_ws2<2, 1, 8, 2>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
-                               n_tiles, 1, act, mbi);
-    } else if (gated) {
+    if (gated) {
       dispatch_ws2<2, 1, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1,
                             act, mbi);
-    } else if (variant == 5) {
-      dispatch_ws2<2, 0, 8, 2>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0,
-                               mbi);
     } else if (variant == 3) {
       dispatch_ws2<1, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
     } else {

@@ -97,7 +97,7 @@ def main() -> int:
                 cands = []
                 for var in map(int, args.variants.split(",")):
                     for sp in ((1,) if gated else (1, 2, 4, 8, 16)):
-                        if K % (64 * sp) or K // (64 * sp) < 2 or (var in (2, 4, 5) and N % 256):
+                        if K % (64 * sp) or K // (64 * sp) < 2 or (var in (2, 4) and N % 256):
                             continue
                         t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), act=act,
                                                     splits=sp, variant=var)
