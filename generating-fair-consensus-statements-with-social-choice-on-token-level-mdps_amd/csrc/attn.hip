@@ -878,16 +878,22 @@ struct RopeParams {
   int32_t skip_v;           // V placed by v_tile_place_kernel instead
 };
 
-// one workgroup per token: the token's D/2 angles' sincos once into LDS, then every
-// (head, 4-pair quad) of the token (q, k rotated; v placed) by its own thread with 8-byte
-// loads / stores — all of a token's heads in flight at once (a per-thread loop over the
-// heads serialised one memory round trip per head: ~30 us per decode step and layer)
-__global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
+// n_split workgroups per token (kRopeItems (head, P-pair group) items each): the token's D/2
+// angles' sincos into LDS, then every item of the workgroup (q, k rotated; v placed) by its
+// own thread with 2P-byte loads / stores.  A decode step's few hundred tokens give over a
+// thousand workgroups (one workgroup per token left most CUs with one: 18 us per C3 layer);
+// a per-thread loop over the heads serialised one memory round trip per head.
+constexpr int kRopeItems = 256;
+
+template <int P>
+__global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r, int32_t n_split) {
+  typedef __bf16 vec_t __attribute__((ext_vector_type(P)));
   __shared__ float cs[128], sn[128];                // D / 2 <= 128
   const int half = r.D >> 1;
-  const int nq = half >> 2;                         // 4-pair quads per head
+  const int nq = half / P;                          // P-pair groups per head
   const int nh = r.H + 2 * r.Hkv;
-  const int64_t tok = blockIdx.x;
+  const int64_t tok = blockIdx.x / n_split;
+  const int split = static_cast<int>(blockIdx.x % n_split);
   const int64_t s = tok / r.T;
   const int t = static_cast<int>(tok % r.T);
   const int gi = static_cast<int>(s / r.n_str);
@@ -900,36 +906,36 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r) {
   __bf16* __restrict__ qo = r.q_out;
   __bf16* __restrict__ kh = r.kh;
   __bf16* __restrict__ vth = r.vth;
-#pragma unroll 4
-  for (int item = threadIdx.x; item < nh * nq; item += 256) {
+  const int lim = min(nh * nq, (split + 1) * kRopeItems);
+  for (int item = split * kRopeItems + threadIdx.x; item < lim; item += 256) {
     const int hh = item / nq;
-    const int i0 = 4 * (item - hh * nq);
+    const int i0 = P * (item - hh * nq);
     const __bf16* src = row + static_cast<int64_t>(hh) * r.D + i0;
-    const bf16x4 a = *reinterpret_cast<const bf16x4*>(src);
-    const bf16x4 b = *reinterpret_cast<const bf16x4*>(src + half);
+    const vec_t a = *reinterpret_cast<const vec_t*>(src);
+    const vec_t b = *reinterpret_cast<const vec_t*>(src + half);
     if (hh >= r.H + r.Hkv) {                         // v: transposed placement, no rotation
       if (r.skip_v) continue;
       const int g = hh - r.H - r.Hkv;
       __bf16* dst = vth + ((s * r.Hkv + g) * r.ldh + (slot & ~31)) * r.D +
                     static_cast<int64_t>(i0) * 32 + (slot & 31);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < P; ++e) {
         dst[e * 32] = a[e];
         dst[(half + e) * 32] = b[e];
       }
       continue;
     }
-    bf16x4 y1, y2;
+    vec_t y1, y2;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < P; ++e) {
       const float x1 = static_cast<float>(a[e]), x2 = static_cast<float>(b[e]);
       y1[e] = static_cast<__bf16>(fmaf(x1, cs[i0 + e], -x2 * sn[i0 + e]));
       y2[e] = static_cast<__bf16>(fmaf(x2, cs[i0 + e], x1 * sn[i0 + e]));
     }
     __bf16* dst = hh < r.H ? qo + (tok * r.H + hh) * r.D
                            : kh + ((s * r.Hkv + (hh - r.H)) * r.ldh + slot) * r.D;
-    *reinterpret_cast<bf16x4*>(dst + i0) = y1;
-    *reinterpret_cast<bf16x4*>(dst + half + i0) = y2;
+    *reinterpret_cast<vec_t*>(dst + i0) = y1;
+    *reinterpret_cast<vec_t*>(dst + half + i0) = y2;
   }
 }
 
@@ -1362,8 +1368,18 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
                 reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && n_vwg <= 0x7fffffffLL &&
                 !(e && atoi(e) == 0)) ? 1 : 0;
   }
-  hipLaunchKernelGGL(rope_place_kernel, dim3(static_cast<uint32_t>(r.n_tok)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), r);
+  // 8-pair (16-byte) items when every head's halves are 16-byte aligned, else 4-pair
+  const bool p8 = ld_qkv % 8 == 0 && reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && D % 16 == 0;
+  const int64_t n_items = static_cast<int64_t>(H + 2 * Hkv) * (D / 2) / (p8 ? 8 : 4);
+  const int64_t n_split = (n_items + kRopeItems - 1) / kRopeItems;
+  if (r.n_tok * n_split > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many tokens");
+  const dim3 grid(static_cast<uint32_t>(r.n_tok * n_split));
+  if (p8)
+    hipLaunchKernelGGL(rope_place_kernel<8>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), r,
+                       static_cast<int32_t>(n_split));
+  else
+    hipLaunchKernelGGL(rope_place_kernel<4>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), r,
+                       static_cast<int32_t>(n_split));
   if (r.skip_v)
     hipLaunchKernelGGL(v_tile_place_kernel, dim3(static_cast<uint32_t>(n_vwg)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), r, static_cast<int32_t>(n_tiles));

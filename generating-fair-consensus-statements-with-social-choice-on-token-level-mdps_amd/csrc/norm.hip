@@ -56,52 +56,60 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
   const int64_t r = blockIdx.x;
   const int nv = static_cast<int>(d >> 3);
   __shared__ float red[2][kNormThreads / 64];
-  u16x8 bv[VPT];
-  if (b) {
+  // every load of the row is issued before the first reduction: one memory round trip per
+  // row instead of four (b, then wb after b's norm, then a, then w after the second norm);
+  // the weights are prefetched only while the registers allow (VPT <= 4)
+  constexpr bool kPre = VPT <= 4;
+  u16x8 bv[VPT], av[VPT], wv[kPre ? VPT : 1], wbv[kPre ? VPT : 1];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = threadIdx.x + k * kNormThreads;
+    if (v < nv) {
+      av[k] = *reinterpret_cast<const u16x8*>(a + r * lda + 8 * v);
+      if (b) bv[k] = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
+      if constexpr (kPre) {
+        wv[k] = *reinterpret_cast<const u16x8*>(w + 8 * v);
+        if (wb) wbv[k] = *reinterpret_cast<const u16x8*>(wb + 8 * v);
+      }
+    }
+  }
+  if (b && wb) {
+    float sb = 0.0f;
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       const int v = threadIdx.x + k * kNormThreads;
-      if (v < nv) bv[k] = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
-    }
-    if (wb) {
-      float sb = 0.0f;
+      if (v < nv) {
 #pragma unroll
-      for (int k = 0; k < VPT; ++k) {
-        const int v = threadIdx.x + k * kNormThreads;
-        if (v < nv) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) sb = fmaf(bf(bv[k][e]), bf(bv[k][e]), sb);
-        }
+        for (int e = 0; e < 8; ++e) sb = fmaf(bf(bv[k][e]), bf(bv[k][e]), sb);
       }
-      const float inv_b = 1.0f / sqrtf(row_sum(sb, red[0]) / static_cast<float>(d) + eps);
+    }
+    const float inv_b = 1.0f / sqrtf(row_sum(sb, red[0]) / static_cast<float>(d) + eps);
 #pragma unroll
-      for (int k = 0; k < VPT; ++k) {
-        const int v = threadIdx.x + k * kNormThreads;
-        if (v < nv) {
-          const u16x8 wv = *reinterpret_cast<const u16x8*>(wb + 8 * v);
+    for (int k = 0; k < VPT; ++k) {
+      const int v = threadIdx.x + k * kNormThreads;
+      if (v < nv) {
+        u16x8 g8;
+        if constexpr (kPre) g8 = wbv[k];
+        else g8 = *reinterpret_cast<const u16x8*>(wb + 8 * v);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float g = plus_one ? 1.0f + bf(wv[e]) : bf(wv[e]);
-            bv[k][e] = to_bf((bf(bv[k][e]) * inv_b) * g);
-          }
+        for (int e = 0; e < 8; ++e) {
+          const float g = plus_one ? 1.0f + bf(g8[e]) : bf(g8[e]);
+          bv[k][e] = to_bf((bf(bv[k][e]) * inv_b) * g);
         }
       }
     }
   }
-  u16x8 sv[VPT];
   float ss = 0.0f;
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int v = threadIdx.x + k * kNormThreads;
     if (v < nv) {
-      u16x8 x = *reinterpret_cast<const u16x8*>(a + r * lda + 8 * v);
       if (b) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = to_bf(bf(x[e]) + bf(bv[k][e]));
+        for (int e = 0; e < 8; ++e) av[k][e] = to_bf(bf(av[k][e]) + bf(bv[k][e]));
       }
-      sv[k] = x;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ss = fmaf(bf(x[e]), bf(x[e]), ss);
+      for (int e = 0; e < 8; ++e) ss = fmaf(bf(av[k][e]), bf(av[k][e]), ss);
     }
   }
   const float inv = 1.0f / sqrtf(row_sum(ss, red[1]) / static_cast<float>(d) + eps);
@@ -109,14 +117,16 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
   for (int k = 0; k < VPT; ++k) {
     const int v = threadIdx.x + k * kNormThreads;
     if (v < nv) {
-      if (s_out) *reinterpret_cast<u16x8*>(s_out + r * lds + 8 * v) = sv[k];
-      const u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * v);
+      if (s_out) *reinterpret_cast<u16x8*>(s_out + r * lds + 8 * v) = av[k];
+      u16x8 g8;
+      if constexpr (kPre) g8 = wv[k];
+      else g8 = *reinterpret_cast<const u16x8*>(w + 8 * v);
       u16x8 out;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float g = plus_one ? 1.0f + bf(wv[e]) : bf(wv[e]);
+        const float g = plus_one ? 1.0f + bf(g8[e]) : bf(g8[e]);
         // Llama (F.rms_norm): x * inv * w, one rounding; Gemma: (x * inv) * (1 + w)
-        out[e] = to_bf((bf(sv[k][e]) * inv) * g);
+        out[e] = to_bf((bf(av[k][e]) * inv) * g);
       }
       *reinterpret_cast<u16x8*>(y + r * ldy + 8 * v) = out;
     }

@@ -44,7 +44,12 @@ def draw_seed(seed: int, t: int) -> int:
 class Backend:
     """CPU fp32 transformers model + the product's char tokenizer."""
 
-    def __init__(self, hf_model, tokenizer, softcap: float = 0.0):
+    def __init__(self, hf_model, tokenizer, softcap: float = 0.0,
+                 tail_positions: Optional[int] = None):
+        """tail_positions: echo log-probs of the prompt's last tail_positions tokens only
+        (NaN before them) -- the LM head over a few rows instead of the whole prompt, for
+        traces whose recorded calls keep only the span's tail (beam search sums [-1:])."""
+        self.tail = tail_positions
         self.m = hf_model.eval()
         self.tok = tokenizer
         self.softcap = softcap
@@ -52,15 +57,22 @@ class Backend:
         self.calls: List[Dict] = []
 
     @torch.no_grad()
-    def logits(self, ids: List[int]) -> np.ndarray:
-        out = self.m(torch.tensor([ids])).logits[0].double().numpy()   # (softcap applied by HF)
-        return out
+    def logits(self, ids: List[int], last_only: bool = False) -> np.ndarray:
+        """fp32 logits as float64 (softcap applied by HF); last_only: the last position's
+        row alone (the LM head over one position instead of the whole prompt)."""
+        kw = {"logits_to_keep": 1} if last_only else {}
+        return self.m(torch.tensor([ids]), **kw).logits[0].double().numpy()
 
+    @torch.no_grad()
     def prompt_logprobs(self, ids: List[int]) -> List[Optional[float]]:
-        lg = self.logits(ids)
-        mx = lg.max(axis=1, keepdims=True)
-        ls = lg - mx - np.log(np.exp(lg - mx).sum(axis=1, keepdims=True))
-        return [None] + [float(ls[i, ids[i + 1]]) for i in range(len(ids) - 1)]
+        """log_softmax(logits)[i, ids[i + 1]] in float64 for every prompt position."""
+        P = len(ids)
+        K = P if self.tail is None else min(P, int(self.tail) + 1)
+        kw = {} if K == P else {"logits_to_keep": K}
+        lg = self.m(torch.tensor([ids]), **kw).logits[0].double()      # positions P-K .. P-1
+        nxt = torch.tensor(ids[P - K + 1:], dtype=torch.long)
+        ls = lg[:-1].gather(1, nxt[:, None])[:, 0] - torch.logsumexp(lg[:-1], dim=1)
+        return [None] + [float("nan")] * (P - K) + [float(v) for v in ls.tolist()]
 
     def sample(self, ids: List[int], max_tokens: int, temperature: float, seed: Optional[int],
                bias: Dict[int, float]):
@@ -70,7 +82,7 @@ class Backend:
         cur = list(ids)
         drawn, lps = [], []
         for t in range(max_tokens):
-            x = self.logits(cur)[-1].copy()
+            x = self.logits(cur, last_only=True)[-1].copy()
             for i, v in bias.items():
                 x[i] += v
             i, lp = oracle.gumbel_sample(x, draw_seed(seed, t), temperature)

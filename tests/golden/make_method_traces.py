@@ -148,7 +148,9 @@ def main() -> None:
     global MODEL_ID
     MODEL_ID, out_name = FAMILIES[args.family]
     cfg, model, tok = fixture_model(args.family)
-    backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok)
+    # c1long: beam search only, whose calls are recorded by their last 6 span log-probs
+    backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok,
+                                    tail_positions=32 if args.family == "c1long" else None)
     install(args.reference, backend)
     scen = yaml.safe_load(open(os.path.join(args.reference, "configs", "appendix", "llama",
                                             "scenario_1", "beam_search.yaml")))["scenario"]
@@ -246,6 +248,15 @@ def main() -> None:
                             "pre_brushup": getattr(gen, "pre_brushup_statement", None),
                             "calls": list(calls), **extra})
         print(f"{method}: {stmt!r} ({len(calls)} scoring calls)")
+
+    if args.family == "c1long":      # tail-only echo log-probs: every recorded tail finite
+        import math
+        assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
+                   if v is not None), "a recorded tail reaches past the computed positions"
+        with open(os.path.join(HERE, out_name), "w") as f:
+            json.dump(out, f, indent=1)
+        print("wrote", out_name)
+        return
 
     # post-hoc evaluation (src/evaluation.py:128-634) on fixed statements
     from src.evaluation import StatementEvaluator  # noqa: E402

@@ -139,11 +139,14 @@ def test_prefix_attention_matches_fp32_reference(ops, dev, case):
     assert torch.equal(out, run())          # deterministic: bit-identical relaunch
 
 
-@pytest.mark.parametrize("D,H,Hkv,T", [(64, 8, 2, 3), (128, 32, 8, 1), (256, 16, 8, 2),
-                                        # T >= 32: V placed by 32-slot tiles (partial tiles
-                                        # at both ends: slots 5 .. 5 + T)
-                                        (128, 32, 8, 40), (64, 8, 2, 64), (256, 16, 8, 33)])
-def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
+@pytest.mark.parametrize("D,H,Hkv,T,col0", [(64, 8, 2, 3, 0), (128, 32, 8, 1, 0), (256, 16, 8, 2, 0),
+                                             # T >= 32: V placed by 32-slot tiles (partial
+                                             # tiles at both ends: slots 5 .. 5 + T)
+                                             (128, 32, 8, 40, 0), (64, 8, 2, 64, 0),
+                                             (256, 16, 8, 33, 0),
+                                             # rows 8-byte but not 16-byte aligned: 4-pair items
+                                             (128, 64, 8, 1, 4), (256, 16, 8, 2, 4)])
+def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T, col0):
     M = importlib.import_module(PKG + ".model")
     cfg = M.preset("tiny-llama", head_dim=D, n_heads=H, n_kv_heads=Hkv)
     inv = M.rope_inv_freq(cfg, dev)
@@ -153,7 +156,8 @@ def test_rope_place_matches_torch(ops, dev, D, H, Hkv, T):
     plens = [17, 250, 1000]
     hb = 5
     ldh = _ceil32(hb + T)
-    qkv = torch.randn(S * T, (H + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    width = (H + 2 * Hkv) * D
+    qkv = torch.randn(S * T, width + 8, generator=g).to(torch.bfloat16).to(dev)[:, col0:col0 + width]
     plen = torch.tensor(plens, dtype=torch.int32, device=dev)
     hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
     q_out = torch.empty(S * T, H, D, dtype=torch.bfloat16, device=dev)
@@ -349,7 +353,8 @@ def test_prefill_streams_matches_padded_prefill(dev, family):
 
 
 @pytest.mark.parametrize("plus_one,d,with_b", [(False, 2048, True), (True, 3584, True),
-                                               (False, 8192, False), (True, 256, False)])
+                                               (False, 8192, False), (True, 256, False),
+                                               (False, 16384, True)])
 def test_add_rms_norm_matches_torch(ops, dev, plus_one, d, with_b):
     g = torch.Generator(device="cpu").manual_seed(d)
     rows = 37
