@@ -27,7 +27,7 @@ EXPORTED = (
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
-    "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits",
+    "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits", "cs_add_rms_norm_splitk",
 )
 
 
@@ -115,6 +115,9 @@ def load():
     L.cs_add_rms_norm.argtypes = [vp, i64, vp, i64, vp, vp, i64, vp, i64, i64, f32, ctypes.c_int,
                                   vp, i64, vp]
     L.cs_add_rms_norm.restype = ctypes.c_int
+    L.cs_add_rms_norm_splitk.argtypes = [vp, i64, vp, i32, vp, vp, i64, vp, i64, i64, f32,
+                                         ctypes.c_int, vp, i64, vp]
+    L.cs_add_rms_norm_splitk.restype = ctypes.c_int
     L.cs_gated_act.argtypes = [vp, i64, vp, i64, i64, i64, ctypes.c_int, vp, i64, vp]
     L.cs_gated_act.restype = ctypes.c_int
     L.cs_hist_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, vp]

@@ -610,16 +610,18 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
                  float* workspace, cs_stream_t stream) {
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
   if (M == 0) return CS_OK;
-  if (!x || !w || !y) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
+  if (!x || !w) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
   if (variant < 0 || variant > 4) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..4");
   if (N % 128) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
   if (gated && splits > 1)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
   variant = resolve_variant(variant, N, gated);
   if (splits <= 0) splits = static_cast<int>(cs_gemm_splits(M, N, K, gated, variant));
+  if (!y && (splits <= 1 || gated))
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: y may be NULL only with a K split (partials kept)");
   if (K % (kGemmBK * splits))
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: K must be a multiple of 64 * splits");
-  if (ldx % 8 || ldw % 8 || ldy % 4 || ldx < K || ldw < K || ldy < (gated ? N / 2 : N))
+  if (ldx % 8 || ldw % 8 || (y && (ldy % 4 || ldy < (gated ? N / 2 : N))) || ldx < K || ldw < K)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: leading dimensions too small or misaligned");
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15 ||
       reinterpret_cast<uintptr_t>(y) & 7)
@@ -662,7 +664,7 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
       dispatch_ws2<2, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
     }
   }
-  if (splits > 1 && !gated) {
+  if (splits > 1 && !gated && Y) {     // y == NULL: the caller folds the partials itself
     const int64_t nv = M * (N / 8);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(static_cast<uint32_t>((nv + 255) / 256)), dim3(256),
                        0, st, workspace, splits, M, N, Y, ldy);

@@ -17,6 +17,7 @@
 namespace {
 
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
 
@@ -28,6 +29,7 @@ __device__ __forceinline__ uint16_t to_bf(float f) {
 }
 
 constexpr int kNormThreads = 256;
+constexpr int kMaxSplits = 16;      // K-split partials folded by cs_add_rms_norm_splitk
 
 // the row's sum over the workgroup: wave64 butterfly, then the 4 wave sums in wave order
 // (the same order everywhere, so a norm is bitwise the same in every kernel that uses it)
@@ -47,12 +49,12 @@ __device__ __forceinline__ float row_sum(float ss, float* red) {
 // barrier and stored after it by the same thread.  wb != nullptr: the branch b is first
 // RMS-normalised itself with weight wb (Gemma-2's post-attention / post-MLP norm), with
 // the arithmetic and rounding of a separate add_rms launch over b alone.
-template <int VPT>
+template <int VPT, bool FOLD>
 __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
     const uint16_t* a, int64_t lda, const uint16_t* __restrict__ b, int64_t ldb,
     const uint16_t* __restrict__ wb, uint16_t* s_out, int64_t lds,
     const uint16_t* __restrict__ w, int64_t d, float eps, int plus_one,
-    uint16_t* __restrict__ y, int64_t ldy) {
+    uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ bp, int splits) {
   const int64_t r = blockIdx.x;
   const int nv = static_cast<int>(d >> 3);
   __shared__ float red[2][kNormThreads / 64];
@@ -66,14 +68,43 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
     const int v = threadIdx.x + k * kNormThreads;
     if (v < nv) {
       av[k] = *reinterpret_cast<const u16x8*>(a + r * lda + 8 * v);
-      if (b) bv[k] = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
+      if constexpr (FOLD) {
+        // b = bf16 of the split-K partials [splits][rows][d] folded in split order: the
+        // arithmetic of cs_gemm_bf16's own fold (splitk_reduce_kernel), so the fused launch
+        // is bitwise the GEMM's bf16 output followed by this norm
+        // (all kMaxSplits loads issued unconditionally from clamped splits, so they are in
+        // flight together; a select, not an added zero, skips the ones past `splits`)
+        const float* q = bp + r * d + 8 * v;
+        const int64_t sstride = static_cast<int64_t>(gridDim.x) * d;
+        f32x4 p0[kMaxSplits], p1[kMaxSplits];
+#pragma unroll
+        for (int sp = 0; sp < kMaxSplits; ++sp) {
+          const float* qs = q + (sp < splits ? sp : splits - 1) * sstride;
+          p0[sp] = *reinterpret_cast<const f32x4*>(qs);
+          p1[sp] = *reinterpret_cast<const f32x4*>(qs + 4);
+        }
+        f32x4 x0 = p0[0], x1 = p1[0];
+#pragma unroll
+        for (int sp = 1; sp < kMaxSplits; ++sp) {
+          x0 = sp < splits ? x0 + p0[sp] : x0;
+          x1 = sp < splits ? x1 + p1[sp] : x1;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bv[k][e] = to_bf(x0[e]);
+          bv[k][4 + e] = to_bf(x1[e]);
+        }
+      } else if (b) {
+        bv[k] = *reinterpret_cast<const u16x8*>(b + r * ldb + 8 * v);
+      }
       if constexpr (kPre) {
         wv[k] = *reinterpret_cast<const u16x8*>(w + 8 * v);
         if (wb) wbv[k] = *reinterpret_cast<const u16x8*>(wb + 8 * v);
       }
     }
   }
-  if (b && wb) {
+  const bool has_b = FOLD || b;
+  if (has_b && wb) {
     float sb = 0.0f;
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
@@ -104,7 +135,7 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
   for (int k = 0; k < VPT; ++k) {
     const int v = threadIdx.x + k * kNormThreads;
     if (v < nv) {
-      if (b) {
+      if (has_b) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) av[k][e] = to_bf(bf(av[k][e]) + bf(bv[k][e]));
       }
@@ -158,22 +189,23 @@ __global__ __launch_bounds__(kNormThreads) void gated_act_kernel(
   *reinterpret_cast<u16x8*>(out + r * ldo + j) = o;
 }
 
-}  // namespace
-
-extern "C" {
-
-int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, const void* b_weight,
-                    void* s_out, int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
-                    int plus_one, void* y, int64_t ldy, cs_stream_t stream) {
-  if (rows < 0 || d <= 0) return fail(CS_ERR_INVALID, "cs_add_rms_norm: bad shape");
+int add_rms_launch(const char* name, const void* a, int64_t lda, const void* b, int64_t ldb,
+                   const float* bp, int splits, const void* b_weight, void* s_out, int64_t lds,
+                   const void* weight, int64_t rows, int64_t d, float eps, int plus_one, void* y,
+                   int64_t ldy, cs_stream_t stream) {
+  if (rows < 0 || d <= 0) return fail(CS_ERR_INVALID, std::string(name) + ": bad shape");
   if (rows == 0) return CS_OK;
-  if (!a || !weight || !y) return fail(CS_ERR_INVALID, "cs_add_rms_norm: NULL pointer");
-  if (b_weight && !b) return fail(CS_ERR_INVALID, "cs_add_rms_norm: b_weight without b");
+  if (!a || !weight || !y) return fail(CS_ERR_INVALID, std::string(name) + ": NULL pointer");
+  const bool has_b = b || bp;
+  if (b_weight && !has_b) return fail(CS_ERR_INVALID, std::string(name) + ": b_weight without b");
   if (d % 8 != 0 || d > 16 * 8 * kNormThreads)
-    return fail(CS_ERR_INVALID, "cs_add_rms_norm: d must be a multiple of 8 and <= 32768");
+    return fail(CS_ERR_INVALID, std::string(name) + ": d must be a multiple of 8 and <= 32768");
+  if (rows > 0x7fffffffLL) return fail(CS_ERR_INVALID, std::string(name) + ": too many rows");
+  if (bp && d > 4 * 8 * kNormThreads)
+    return fail(CS_ERR_INVALID, std::string(name) + ": d must be <= 8192 with split partials");
   if (lda < d || ldy < d || (b && ldb < d) || (s_out && lds < d) || lda % 8 || ldy % 8 ||
       (b && ldb % 8) || (s_out && lds % 8))
-    return fail(CS_ERR_INVALID, "cs_add_rms_norm: leading dimensions must be >= d and multiples of 8");
+    return fail(CS_ERR_INVALID, std::string(name) + ": leading dimensions must be >= d and multiples of 8");
   const uint16_t* A = static_cast<const uint16_t*>(a);
   const uint16_t* B = static_cast<const uint16_t*>(b);
   const uint16_t* WB = static_cast<const uint16_t*>(b_weight);
@@ -183,20 +215,48 @@ int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, cons
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int nv = static_cast<int>(d / 8);
   const dim3 grid(static_cast<uint32_t>(rows));
+#define CS_ADD_RMS(V)                                                                             \
+  if (bp)                                                                                         \
+    hipLaunchKernelGGL((add_rms_kernel<V, true>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, \
+                       S, lds, W, d, eps, plus_one, Y, ldy, bp, splits);                          \
+  else                                                                                            \
+    hipLaunchKernelGGL((add_rms_kernel<V, false>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb,   \
+                       WB, S, lds, W, d, eps, plus_one, Y, ldy, bp, splits)
   if (nv <= kNormThreads) {
-    hipLaunchKernelGGL(add_rms_kernel<1>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
-                       W, d, eps, plus_one, Y, ldy);
+    CS_ADD_RMS(1);
   } else if (nv <= 2 * kNormThreads) {
-    hipLaunchKernelGGL(add_rms_kernel<2>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
-                       W, d, eps, plus_one, Y, ldy);
+    CS_ADD_RMS(2);
   } else if (nv <= 4 * kNormThreads) {
-    hipLaunchKernelGGL(add_rms_kernel<4>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
-                       W, d, eps, plus_one, Y, ldy);
-  } else {
-    hipLaunchKernelGGL(add_rms_kernel<16>, grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, S, lds,
-                       W, d, eps, plus_one, Y, ldy);
+    CS_ADD_RMS(4);
+  } else {       // (d > 8192: the fold is refused above)
+    hipLaunchKernelGGL((add_rms_kernel<16, false>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb,
+                       WB, S, lds, W, d, eps, plus_one, Y, ldy, nullptr, 0);
   }
-  return check_launch("cs_add_rms_norm");
+#undef CS_ADD_RMS
+  return check_launch(name);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, const void* b_weight,
+                    void* s_out, int64_t lds, const void* weight, int64_t rows, int64_t d, float eps,
+                    int plus_one, void* y, int64_t ldy, cs_stream_t stream) {
+  return add_rms_launch("cs_add_rms_norm", a, lda, b, ldb, nullptr, 0, b_weight, s_out, lds, weight,
+                        rows, d, eps, plus_one, y, ldy, stream);
+}
+
+int cs_add_rms_norm_splitk(const void* a, int64_t lda, const float* partials, int32_t splits,
+                           const void* b_weight, void* s_out, int64_t lds, const void* weight,
+                           int64_t rows, int64_t d, float eps, int plus_one, void* y, int64_t ldy,
+                           cs_stream_t stream) {
+  if (!partials || splits < 1 || splits > kMaxSplits)
+    return fail(CS_ERR_INVALID, "cs_add_rms_norm_splitk: partials and 1 <= splits <= 16 required");
+  if (reinterpret_cast<uintptr_t>(partials) & 15)
+    return fail(CS_ERR_INVALID, "cs_add_rms_norm_splitk: partials must be 16-byte aligned");
+  return add_rms_launch("cs_add_rms_norm_splitk", a, lda, nullptr, 0, partials, splits, b_weight,
+                        s_out, lds, weight, rows, d, eps, plus_one, y, ldy, stream);
 }
 
 int cs_gated_act(const void* gate, int64_t ld_gate, const void* up, int64_t ld_up, int64_t rows,

@@ -424,8 +424,9 @@ class Model:
             # add's launch (b_weight): one cs_add_rms_norm per residual add
             x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2,
                                  b_weight=self.w[p + "post_attn_norm"] if g2 else None)
+            # a K-split down projection hands its partials to the residual add's launch
             y = ops.linear(ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act),
-                           self.w[p + "w_down"])
+                           self.w[p + "w_down"], fold=False)
             nxt = self.w[f"l{i + 1}.attn_norm"] if i + 1 < c.n_layers else self.w["norm"]
             x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2,
                                  b_weight=self.w[p + "post_mlp_norm"] if g2 else None)

@@ -15,7 +15,7 @@ import ctypes
 import json
 import os
 import threading
-from typing import Optional, Sequence
+from typing import NamedTuple, Optional, Sequence
 
 import numpy as np
 import torch
@@ -650,17 +650,27 @@ def _rows2d(t: torch.Tensor, name: str):
     return t.stride(0) if t.shape[0] > 1 else t.shape[1]
 
 
-def add_rms_norm(a: torch.Tensor, weight: torch.Tensor, eps: float, *, b: Optional[torch.Tensor] = None,
+class SplitPartials(NamedTuple):
+    """A K-split GEMM's unfolded fp32 partials [splits, M, N] (cs_gemm_bf16 with y = NULL),
+    folded by the add_rms_norm that consumes them (cs_add_rms_norm_splitk)."""
+    part: torch.Tensor
+
+
+def add_rms_norm(a: torch.Tensor, weight: torch.Tensor, eps: float, *,
+                 b: "Optional[torch.Tensor | SplitPartials]" = None,
                  b_weight: Optional[torch.Tensor] = None, plus_one: bool = False,
                  s_out: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = RMSNorm(a + b) (cs_add_rms_norm); the bf16 sum a + b is also written to s_out.
     a, b, s_out, out [rows, d] bf16; weight [d] bf16 (Gemma-2: plus_one, 1 + weight).
     b_weight: b is RMS-normalised first with that weight (Gemma-2's post norms), bitwise as
-    add_rms_norm(b, b_weight) followed by this call."""
+    add_rms_norm(b, b_weight) followed by this call.  b may be a SplitPartials (linear(...,
+    fold=False)): folded inside this launch, bitwise as the GEMM's own fold then this call."""
     L = _lib.load()
     lda = _rows2d(a, "a")
     rows, d = a.shape
+    if isinstance(b, SplitPartials):
+        return _add_rms_norm_splitk(L, a, lda, weight, eps, b.part, b_weight, plus_one, s_out, out)
     ldb = _rows2d(b, "b") if b is not None else 0
     lds = _rows2d(s_out, "s_out") if s_out is not None else 0
     if (b is not None and b.shape != a.shape) or (s_out is not None and s_out.shape != a.shape):
@@ -679,6 +689,32 @@ def add_rms_norm(a: torch.Tensor, weight: torch.Tensor, eps: float, *, b: Option
                            s_out.data_ptr() if s_out is not None else None, lds, weight.data_ptr(),
                            rows, d, float(eps), int(bool(plus_one)), out.data_ptr(), ldy, _stream())
     _lib.check(rc, "cs_add_rms_norm")
+    return out
+
+
+def _add_rms_norm_splitk(L, a, lda, weight, eps, part, b_weight, plus_one, s_out, out):
+    rows, d = a.shape
+    if part.dim() != 3 or part.dtype != torch.float32 or not part.is_contiguous() or \
+            tuple(part.shape[1:]) != (rows, d):
+        raise CSError("split partials must be a contiguous float32 [splits, rows, d] tensor")
+    lds = _rows2d(s_out, "s_out") if s_out is not None else 0
+    if s_out is not None and s_out.shape != a.shape:
+        raise CSError("a and s_out must share one shape")
+    if weight.dtype != torch.bfloat16 or weight.numel() != d or not weight.is_contiguous():
+        raise CSError("weight must be a contiguous bfloat16 [d] tensor")
+    if b_weight is not None and (b_weight.dtype != torch.bfloat16 or b_weight.numel() != d or
+                                 not b_weight.is_contiguous()):
+        raise CSError("b_weight must be a contiguous bfloat16 [d] tensor")
+    if out is None:
+        out = torch.empty_like(a, memory_format=torch.contiguous_format)
+    ldy = _rows2d(out, "out")
+    _require_cuda(a, part, s_out, weight, out)
+    rc = L.cs_add_rms_norm_splitk(a.data_ptr(), lda, part.data_ptr(), int(part.shape[0]),
+                                  b_weight.data_ptr() if b_weight is not None else None,
+                                  s_out.data_ptr() if s_out is not None else None, lds,
+                                  weight.data_ptr(), rows, d, float(eps), int(bool(plus_one)),
+                                  out.data_ptr(), ldy, _stream())
+    _lib.check(rc, "cs_add_rms_norm_splitk")
     return out
 
 
@@ -724,12 +760,16 @@ def gemm_choice(M: int, N: int, K: int, gated: bool = False) -> Optional[dict]:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "silu",
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, fold: bool = True):
     """y = x @ w.T (gated: act(gate) * up of the fused gate|up weight) on whichever GEMM the
-    dispatch table measured faster for this shape: cs_gemm_bf16 or hipBLASLt (+ cs_gated_act)."""
+    dispatch table measured faster for this shape: cs_gemm_bf16 or hipBLASLt (+ cs_gated_act).
+    fold=False: a K-split cs_gemm_bf16 returns its unfolded SplitPartials (for an
+    add_rms_norm to fold); every other path returns the bf16 tensor as usual."""
     if x.is_cuda and x.dim() == 2:
         ch = gemm_choice(x.shape[0], w.shape[0], w.shape[1], gated)
         if ch is not None and gemm_ok(x, w, gated):
+            if not fold and not gated and out is None and int(ch["splits"]) > 1:
+                return gemm_partials(x, w, splits=int(ch["splits"]), variant=int(ch["variant"]))
             return gemm(x, w, gated=gated, act=act, splits=int(ch["splits"]),
                         variant=int(ch["variant"]), out=out)
     if gated:          # the plain GEMM (on whichever library is faster) + cs_gated_act
@@ -784,6 +824,22 @@ def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "s
                         part.data_ptr() if part is not None else None, _stream())
     _lib.check(rc, "cs_gemm_bf16")
     return out
+
+
+def gemm_partials(x: torch.Tensor, w: torch.Tensor, *, splits: int, variant: int = 0) -> SplitPartials:
+    """The fp32 partials [splits, M, N] of cs_gemm_bf16 with a K split, unfolded (y = NULL)."""
+    L = _lib.load()
+    if not gemm_ok(x, w) or splits < 2:
+        raise CSError("gemm_partials needs cs_gemm_bf16 operands and splits >= 2")
+    M, K = x.shape
+    N = w.shape[0]
+    _require_cuda(x, w)
+    part = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    ldx = x.stride(0) if M > 1 else K
+    rc = L.cs_gemm_bf16(x.data_ptr(), ldx, w.data_ptr(), w.stride(0), None, 0, M, N, K, splits, 0,
+                        0, variant, part.data_ptr(), _stream())
+    _lib.check(rc, "cs_gemm_bf16")
+    return SplitPartials(part)
 
 
 def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,

@@ -386,6 +386,18 @@ int cs_add_rms_norm(const void* a, int64_t lda, const void* b, int64_t ldb, cons
                     float eps, int plus_one, void* y, int64_t ldy, cs_stream_t stream);
 
 /*
+ * cs_add_rms_norm_splitk — cs_add_rms_norm whose branch b is the K-split partials of a
+ * cs_gemm_bf16 called with y = NULL: partials [splits][rows][d] fp32 (contiguous, 16-byte
+ * aligned, 1 <= splits <= 16, d <= 8192) are folded in split order and rounded to bf16 exactly as cs_gemm_bf16's own fold,
+ * so the result is bitwise cs_gemm_bf16(y) followed by cs_add_rms_norm(b = y) — one launch
+ * and one bf16 round trip fewer (a decode step's down projection + the residual add).
+ */
+int cs_add_rms_norm_splitk(const void* a, int64_t lda, const float* partials, int32_t splits,
+                           const void* b_weight, void* s_out, int64_t lds, const void* weight,
+                           int64_t rows, int64_t d, float eps, int plus_one, void* y, int64_t ldy,
+                           cs_stream_t stream);
+
+/*
  * cs_gated_act — the gated MLP activation of bf16 rows: out = act(gate) * up with act =
  * SiLU (act = 0, Llama-3) or tanh-GeLU (act = 1, Gemma-2), the activation rounded to bf16
  * before the product.  F and leading dimensions multiples of 8.
@@ -404,7 +416,8 @@ int cs_gated_act(const void* gate, int64_t ld_gate, const void* up, int64_t ld_u
  * gate|up weight [2F, K] (gate rows first) and Y [M, F] = act(gate) * up with the rounding
  * of cs_gated_act (act 0 SiLU, 1 tanh-GeLU).  splits > 1 divides K over workgroups and
  * folds the fp32 partials in split order (workspace: splits * M * N floats); splits <= 0
- * takes cs_gemm_splits.  variant: 0 = the library's choice, 1 = 2 x 4 wave grid (128 columns x
+ * takes cs_gemm_splits; y = NULL with splits > 1 leaves the partials [splits][M][N] in the
+ * workspace unfolded (cs_add_rms_norm_splitk folds them).  variant: 0 = the library's choice, 1 = 2 x 4 wave grid (128 columns x
  * up to 288 rows per workgroup), 2 = column-only wave split, 256 columns, LDS-DMA X,
  * 3 = as 2 with 128 columns, 4 = as 2 with at most 144 rows per workgroup (row blocks of a
  * column tile paired on one XCD).  N a multiple of 128, K of 64 * splits; ldx, ldw multiples of

@@ -155,7 +155,7 @@ def check_evaluations(traces):
     ev = ev_mod.StatementEvaluator(traces["model_id"], include_comparative_ranking=False,
                                    verbose=False)
     failures = []
-    for rec in traces["evaluations"]:
+    for rec in traces.get("evaluations", []):     # (absent from the beam-only c1long trace)
         got = ev.evaluate_statement(rec["statement"], traces["issue"], dict(traces["agent_opinions"]))
         for k, ref in rec["result"].items():
             g = got.get(k, "MISSING")
@@ -176,7 +176,7 @@ def check_evaluations(traces):
 def check_prompt_logprobs(traces):
     utils = importlib.import_module(PKG + ".utils")
     failures = []
-    for rec in traces["prompt_logprobs"]:
+    for rec in traces.get("prompt_logprobs", []):
         toks, lps = utils.get_prompt_logprobs(traces["model_id"], rec["system"], rec["user"])
         if toks != rec["tokens"]:
             failures.append(f"prompt_logprobs {rec['user']!r}: tokens {toks} vs {rec['tokens']}")

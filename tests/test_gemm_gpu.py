@@ -83,3 +83,27 @@ def test_gemm_rejects_unsupported_shapes(ops, dev):
     assert not ops.gemm_ok(x, w)
     with pytest.raises(ops.CSError):
         ops.gemm(x, w)
+
+
+@pytest.mark.parametrize("M,d,K,splits,variant", [(272, 3584, 2048, 8, 3), (37, 2048, 1024, 2, 2),
+                                                  (72, 8192, 1024, 4, 4)])
+@pytest.mark.parametrize("plus_one,post_norm", [(False, False), (True, True)])
+def test_split_partials_folded_by_add_rms_norm_is_bitwise(ops, dev, M, d, K, splits, variant,
+                                                          plus_one, post_norm):
+    """cs_gemm_bf16(y = NULL) + cs_add_rms_norm_splitk == cs_gemm_bf16's own fold followed by
+    cs_add_rms_norm (the down projection + residual add of a decode step), bit for bit."""
+    g = torch.Generator(device="cpu").manual_seed(M + d + splits)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(d, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    a = (torch.randn(M, d, generator=g) * 2).to(dev, torch.bfloat16)
+    wt = (torch.randn(d, generator=g) * 0.1).to(dev, torch.bfloat16)
+    wb = (torch.randn(d, generator=g) * 0.1).to(dev, torch.bfloat16) if post_norm else None
+    y = ops.gemm(x, w, splits=splits, variant=variant)
+    a_ref, a_got = a.clone(), a.clone()
+    ref = ops.add_rms_norm(a_ref, wt, 1e-6, b=y, b_weight=wb, s_out=a_ref, plus_one=plus_one)
+    part = ops.gemm_partials(x, w, splits=splits, variant=variant)
+    assert tuple(part.part.shape) == (splits, M, d)
+    got = ops.add_rms_norm(a_got, wt, 1e-6, b=part, b_weight=wb, s_out=a_got, plus_one=plus_one)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(a_got, a_ref)
