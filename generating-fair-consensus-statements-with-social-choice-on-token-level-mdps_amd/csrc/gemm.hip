@@ -518,211 +518,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   }
 }
 
-// acc += A * B (v_mfma_f32_16x16x32_bf16) as inline asm, the accumulator in an AGPR
-// (IN_AGPR) or a VGPR: a fixed instruction the compiler does not move past the other asm
-template <bool IN_AGPR>
-__device__ __forceinline__ void asm_mfma(gf32x4& acc, const gbf16x8& a, const gbf16x8& b) {
-  if constexpr (IN_AGPR)
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-
-// ws4_gemm_kernel<MT, GATED>: one wave per SIMD (4 waves, 256 output features per
-// workgroup, 64 per wave) so every X fragment read from LDS feeds 4 MFMAs instead of 2 (the
-// LDS array carried ws2's 8 waves' fragment reads plus the X DMA at ~60 % of its cycles).
-// The 16 * MT * 4 accumulators per lane (272 at MT = 17) live in AGPRs (the first 16 row
-// tiles; the 17th in VGPRs), which is why the MFMAs are inline asm ("+a"): with one wave per
-// SIMD nothing hides a stall, so the whole K step is a fixed program order — fragment read
-// kR ahead, counted lgkmcnt, 4 MFMAs — that the compiler may not reschedule.  X staging,
-// the W register ring (three 64-deep steps ahead) and the split-K / gated epilogues are
-// ws2's.
-template <int MT, int GATED>
-__global__ __launch_bounds__(256, 1) void ws4_gemm_kernel(
-    const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
-    uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
-    int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
-  constexpr int NT = 4;
-  constexpr int WAVES = 4;
-  constexpr int kRows = 16 * MT;
-  constexpr int kStage = kRows * 128;
-  constexpr int kPieces = kRows / 8;
-  constexpr int kG = (kPieces + WAVES - 1) / WAVES;
-  constexpr int kBN = 16 * NT * WAVES;
-  constexpr int kHalf = NT / 2;
-  constexpr int kWait = kG + 4 * NT;
-  constexpr int kQ = 2 * MT;
-  constexpr int kR = 6;                          // fragment reads in flight
-  constexpr int kAT = MT < 16 ? MT : 16;          // row tiles whose accumulators are AGPRs
-  static_assert(kWait < 64, "vmcnt counts to 63");
-  __shared__ __align__(16) unsigned char lds[3 * kStage];
-
-  const int bid = blockIdx.x;
-  int cell = bid, mb = 0;
-  if (m_blocks > 1) {
-    const int g = bid / (8 * m_blocks), r = bid % (8 * m_blocks);
-    mb = r / 8;
-    cell = g * 8 + (r % 8);
-  }
-  if (cell >= n_tiles * splits) return;
-  const int nt = cell % n_tiles;
-  const int sp = cell / n_tiles;
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int64_t m0 = static_cast<int64_t>(mb) * kRows;
-  const int64_t kbase = static_cast<int64_t>(sp) * nk * kGemmBK;
-
-  const uint16_t* wp[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    int64_t row;
-    if (GATED) {
-      const int jj = j % kHalf;
-      const int64_t f = static_cast<int64_t>(nt) * (kBN / 2) + wv * 16 * kHalf + 16 * jj + (lane & 15);
-      row = j < kHalf ? f : gate_off + f;
-    } else {
-      row = static_cast<int64_t>(nt) * kBN + wv * 16 * NT + 16 * j + (lane & 15);
-    }
-    wp[j] = W + row * ldw + kbase + 8 * (lane >> 4);
-  }
-  const uint16_t* xsrc[kG];
-  int xdst[kG];
-#pragma unroll
-  for (int g = 0; g < kG; ++g) {
-    int pc = wv + WAVES * g;
-    if (pc > kPieces - 1) pc = kPieces - 1;
-    const int r = 8 * pc + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    int64_t gr = m0 + r;
-    if (gr > M - 1) gr = M - 1;
-    xsrc[g] = X + gr * ldx + kbase + 8 * c;
-    xdst[g] = pc * 1024;
-  }
-
-  gf32x4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue_x = [&](int kt, int buf) {
-    kt = kt < nk ? kt : nk - 1;
-#pragma unroll
-    for (int g = 0; g < kG; ++g)
-      dma16(xsrc[g] + kt * kGemmBK, lds + buf * kStage + xdst[g]);
-  };
-  auto load_w = [&](gbf16x8 (&w)[NT][2], int kt) {
-    kt = kt < nk ? kt : nk - 1;
-    const int64_t o = static_cast<int64_t>(kt) * kGemmBK;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      w[j][0] = asm_load16(wp[j] + o);
-      w[j][1] = asm_load16(wp[j] + o + 32);
-    }
-  };
-  const int xr = lane & 15;
-  const uint32_t lds_u32 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((gl_lds_ptr)lds));
-  const uint32_t fa0 = lds_u32 + x_swz(xr, lane >> 4);
-  const uint32_t fa1 = lds_u32 + x_swz(xr, 4 + (lane >> 4));
-  auto rd = [](gbf16x8 (&fr)[kR], uint32_t a0, uint32_t a1, auto qc) {
-    constexpr int q = decltype(qc)::value;
-    if constexpr (q < kQ) {
-      constexpr int off = (q % MT) * 2048;
-      gbf16x8 v;
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(q < MT ? a0 : a1), "n"(off));
-      fr[q % kR] = v;
-    }
-  };
-  auto compute = [&](int buf, gbf16x8 (&w)[NT][2]) {
-    const uint32_t a0 = fa0 + buf * kStage, a1 = fa1 + buf * kStage;
-    gbf16x8 f[kR];
-    cs_static_for<kR - 1>([&](auto qc) { rd(f, a0, a1, qc); });
-    cs_static_for<kQ>([&](auto qc) {
-      constexpr int q = decltype(qc)::value;
-      rd(f, a0, a1, std::integral_constant<int, q + kR - 1>{});
-      constexpr int issued_after = (q + kR - 1 < kQ ? q + kR - 1 : kQ - 1) - q;
-      gbf16x8 v = f[q % kR];
-      asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(issued_after));
-      constexpr int sub = q / MT, i = q % MT;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) asm_mfma<(i < kAT)>(acc[i][j], w[j][sub], v);
-    });
-  };
-  auto sync = [&](gbf16x8 (&w)[NT][2]) {
-    asm volatile("s_waitcnt vmcnt(%8)"
-                 : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1]),
-                   "+v"(w[2][0]), "+v"(w[2][1]), "+v"(w[3][0]), "+v"(w[3][1])
-                 : "n"(kWait) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto hold = [&](gbf16x8 (&w)[NT][2]) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(w[j][0]), "+v"(w[j][1]));
-  };
-
-  gbf16x8 w0[NT][2], w1[NT][2], w2[NT][2];
-  load_w(w0, 0);
-  issue_x(0, 0);
-  load_w(w1, 1);
-  issue_x(1, 1);
-  load_w(w2, 2);
-#define CS_WS4_STEP(T, B, WB)        \
-  sync(WB);                          \
-  issue_x((T) + 2, ((B) + 2) % 3);   \
-  if ((T) < nk) compute(B, WB);      \
-  load_w(WB, (T) + 3);
-  for (int t = 0; t < nk; t += 3) {
-    CS_WS4_STEP(t, 0, w0)
-    CS_WS4_STEP(t + 1, 1, w1)
-    CS_WS4_STEP(t + 2, 2, w2)
-  }
-#undef CS_WS4_STEP
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  hold(w0);
-  hold(w1);
-  hold(w2);
-  // the asm MFMAs' results are read by the epilogue's VALU: the compiler cannot see their
-  // latency, so wait it out here (an MFMA's write-back completes within 64 cycles)
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int64_t m = m0 + 16 * i + (lane & 15);
-    if (m >= M) continue;
-    if (GATED) {
-#pragma unroll
-      for (int jj = 0; jj < kHalf; ++jj) {
-        const int64_t f =
-            static_cast<int64_t>(nt) * (kBN / 2) + wv * 16 * kHalf + 16 * jj + 4 * (lane >> 4);
-        gu16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float g = gbf(gto_bf(acc[i][jj][e]));
-          const float u = gbf(gto_bf(acc[i][kHalf + jj][e]));
-          const uint16_t a = gto_bf(act ? g_gelu_tanh(g) : g_silu(g));
-          o[e] = gto_bf(gbf(a) * u);
-        }
-        *reinterpret_cast<gu16x4*>(Y + m * ldy + f) = o;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int64_t n = static_cast<int64_t>(nt) * kBN + wv * 16 * NT + 16 * j + 4 * (lane >> 4);
-        if (P) {
-          *reinterpret_cast<gf32x4*>(P + (static_cast<int64_t>(sp) * M + m) * n_out + n) = acc[i][j];
-        } else {
-          gu16x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = gto_bf(acc[i][j][e]);
-          *reinterpret_cast<gu16x4*>(Y + m * ldy + n) = o;
-        }
-      }
-    }
-  }
-}
-
 // Y[m][n] = bf16(sum_s P[s][m][n]) in split order; 8 outputs per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splits,
                                                             int64_t M, int64_t N,
@@ -818,41 +613,15 @@ void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t
 #undef CS_WS2_CASE
 }
 
-template <int MT, int GATED>
-void launch_ws4(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
-                int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
-                int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
-  hipLaunchKernelGGL((ws4_gemm_kernel<MT, GATED>), dim3(blocks), dim3(256), 0, st, X, ldx, W, ldw, Y,
-                     ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act, m_blocks);
-}
-
-template <int GATED>
-void dispatch_ws4(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
-                  const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M,
-                  int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act,
-                  int m_blocks) {
-#define CS_WS4_CASE(V)                                                                            \
-  case V:                                                                                         \
-    launch_ws4<V, GATED>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles,   \
-                         splits, act, m_blocks);                                                  \
-    break;
-  switch (mt) {
-    CS_WS4_CASE(2) CS_WS4_CASE(4) CS_WS4_CASE(8) CS_WS4_CASE(9) CS_WS4_CASE(12) CS_WS4_CASE(17)
-    default: break;
-  }
-#undef CS_WS4_CASE
-}
-
 // W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16;
-// 4: as 2 with at most 9 row tiles (144 rows) per workgroup; 5: ws4 4 waves x 64, at most
-// 17 row tiles)
+// 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
 int64_t variant_bn(int variant, int gated) {
   if (variant == 1) return 128;
   if (variant == 3 && !gated) return 128;
   return 256;
 }
 
-int variant_max_tiles(int variant) { return variant == 4 ? 9 : variant == 5 ? 17 : 18; }
+int variant_max_tiles(int variant) { return variant == 4 ? 9 : 18; }
 
 int64_t gemm_tiles(int variant, int64_t M, int64_t N, int gated) {
   if (variant == 1) {
@@ -872,7 +641,7 @@ int64_t ws2_grid(int64_t cells, int64_t mblocks) {
 
 int resolve_variant(int variant, int64_t N, int gated) {
   if (variant == 0) variant = 2;
-  if ((variant == 2 || variant == 4 || variant == 5) && N % 256) variant = gated ? 1 : 3;
+  if ((variant == 2 || variant == 4) && N % 256) variant = gated ? 1 : 3;
   if (variant == 3 && gated) variant = 2;
   return variant;
 }
@@ -898,7 +667,7 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
   if (M == 0) return CS_OK;
   if (!x || !w) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
-  if (variant < 0 || variant > 5) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..5");
+  if (variant < 0 || variant > 4) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..4");
   if (N % 128) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
   if (gated && splits > 1)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
@@ -942,13 +711,7 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
     const int b = static_cast<int>(grid);
     const int mbi = static_cast<int>(mb);
-    if (variant == 5) {
-      if (gated)
-        dispatch_ws4<1>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1, act,
-                        mbi);
-      else
-        dispatch_ws4<0>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
-    } else if (gated) {
+    if (gated) {
       dispatch_ws2<2, 1, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1,
                             act, mbi);
     } else if (variant == 3) {

@@ -26,14 +26,14 @@ def _tol(ref):
     return ref.abs() * 2.0 ** -7 + 1e-3 * ref.abs().max()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_matches_fp32_product(ops, dev, M, N, K, variant):
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
     x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
     ref = x.float() @ w.float().t()
-    if variant in (2, 4, 5) and N % 256:
+    if variant in (2, 4) and N % 256:
         pytest.skip("256-column tiles")
     y = ops.gemm(x, w, variant=variant)
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
@@ -46,8 +46,6 @@ def test_gemm_matches_fp32_product(ops, dev, M, N, K, variant):
         b = ops.gemm(x, w, splits=sp, variant=variant)
         assert torch.equal(a, b), f"splits={sp} not bitwise reproducible"
         assert torch.all((a.float() - ref).abs() <= _tol(ref)), sp
-        if variant == 5:   # ws4 accumulates in ws2's order: bitwise variant 2's result
-            assert torch.equal(a, ops.gemm(x, w, splits=sp, variant=2)), sp
 
 
 def test_gemm_strided_operands_and_out(ops, dev):
@@ -63,7 +61,7 @@ def test_gemm_strided_operands_and_out(ops, dev):
     assert torch.all(ob[:, N:] == 0)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 4])
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
 @pytest.mark.parametrize("M,F,K", [(20, 512, 256), (272, 1024, 448), (300, 256, 128)])
 def test_gated_gemm_equals_gemm_then_gated_act(ops, dev, act, M, F, K, variant):
@@ -88,7 +86,7 @@ def test_gemm_rejects_unsupported_shapes(ops, dev):
 
 
 @pytest.mark.parametrize("M,d,K,splits,variant", [(272, 3584, 2048, 8, 3), (37, 2048, 1024, 2, 2),
-                                                  (72, 8192, 1024, 4, 4), (520, 8192, 1024, 4, 5)])
+                                                  (72, 8192, 1024, 4, 4), (520, 8192, 1024, 4, 2)])
 @pytest.mark.parametrize("plus_one,post_norm", [(False, False), (True, True)])
 def test_split_partials_folded_by_add_rms_norm_is_bitwise(ops, dev, M, d, K, splits, variant,
                                                           plus_one, post_norm):
