@@ -989,13 +989,6 @@ __global__ __launch_bounds__(256) void v_tile_place_kernel(RopeParams r, int32_t
 // stream), 16-byte vectors; the unfilled capacity is never moved.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// 16-byte unit j of a head's filled V^T region -> its offset in the head's [tiles][D][4] units
-__device__ __forceinline__ int vt_unit(int j, int full_units, int ur) {
-  if (j < full_units) return j;
-  const int r = j - full_units;
-  return full_units + (r / ur) * 4 + (r % ur);
-}
-
 __global__ __launch_bounds__(256) void hist_gather_kernel(
     const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
     __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
@@ -1016,34 +1009,40 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
   const int v_full = (hb / 32) * D * 4, v_ur = ((hb & 31) + 7) / 8;
   const int vv = v_full + D * v_ur;
   const int pv = static_cast<int>(per / 8);
+  const float inv_kv = 1.0f / kv, inv_vv = 1.0f / vv, inv_ur = 1.0f / (v_ur > 0 ? v_ur : 1);
   const u32x4_t* sk = reinterpret_cast<const u32x4_t*>(src_k + so);
   const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(src_v + so);
   u32x4_t* dk = reinterpret_cast<u32x4_t*>(dst_k + dn);
   u32x4_t* dv = reinterpret_cast<u32x4_t*>(dst_v + dn);
   const int nk = Hkv * kv, n = nk + Hkv * vv;
+  // unit i -> its offset (same in source and destination: both [Hkv][ldh*D/8] per stream)
+  auto unit = [&](int i) -> int {
+    if (i < nk) {
+      const int g = fast_div(i, kv, inv_kv);
+      return g * pv + (i - g * kv);
+    }
+    const int iv = i - nk, g = fast_div(iv, vv, inv_vv), j = iv - g * vv;
+    if (j < v_full) return g * pv + j;
+    const int r = j - v_full, q = fast_div(r, v_ur, inv_ur);
+    return g * pv + v_full + q * 4 + (r - q * v_ur);
+  };
   constexpr int U = 8;
   for (int i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
     u32x4_t x[U];
+    int o[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u * 256;
-      if (i < nk) {
-        const int g = i / kv, j = i - g * kv;
-        x[u] = sk[g * pv + j];
-      } else if (i < n) {
-        const int iv = i - nk, g = iv / vv, j = iv - g * vv;
-        x[u] = sv[g * pv + vt_unit(j, v_full, v_ur)];
+      if (i < n) {
+        o[u] = unit(i);
+        x[u] = (i < nk ? sk : sv)[o[u]];
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u * 256;
-      if (i < nk) {
-        const int g = i / kv, j = i - g * kv;
-        dk[g * pv + j] = x[u];
-      } else if (i < n) {
-        const int iv = i - nk, g = iv / vv, j = iv - g * vv;
-        dv[g * pv + vt_unit(j, v_full, v_ur)] = x[u];
+      if (i < n) {
+        (i < nk ? dk : dv)[o[u]] = x[u];
       }
     }
   }

@@ -230,3 +230,63 @@ def test_handoff_primitives_lower_to_sc1(pkg, tmp_path):
     assert atomics, "the arrival counter must be one device atomic"
     assert "s_waitcnt vmcnt(0)" in body
     shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+def _hipcc_or_skip():
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    return hipcc
+
+
+def test_fast_div_is_floor_division(pkg, tmp_path):
+    """cs_kernels.cuh fast_div (cs_hist_gather's index math: float reciprocal + one
+    correction) equals integer floor division for every numerator below 2^20 and every
+    divisor the copy uses (units per head: hb * D / 8 and its V^T counterpart, 1..4
+    16-byte units per row), compiled as host code with the library's flags."""
+    import subprocess
+    from importlib import import_module
+    build = import_module(pkg.__name__ + ".build")
+    hipcc = _hipcc_or_skip()
+    src = tmp_path / "fast_div.hip"
+    src.write_text('#include "cs_kernels.cuh"\n'
+                   'int main() {\n'
+                   '  long bad = 0;\n'
+                   '  for (int d = 1; d <= 20000; d += (d < 64 ? 1 : 7)) {\n'
+                   '    const float inv = 1.0f / d;\n'
+                   '    for (int i = 0; i < (1 << 20); i += (d < 64 ? 1 : 3)) bad += fast_div(i, d, inv) != i / d;\n'
+                   '  }\n'
+                   '  printf("%ld\\n", bad);\n'
+                   '  return bad != 0;\n'
+                   '}\n')
+    exe = tmp_path / "fast_div"
+    flags = [f for f in build._flags() if f != "-fPIC"]
+    subprocess.run([hipcc] + flags + ["-O2", str(src), "-o", str(exe)], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout
+
+
+def test_gemm_fragment_reads_are_hand_counted(pkg, tmp_path):
+    """cs_gemm_bf16's 2-waves-per-SIMD kernels at 17 row tiles (C3's 272 rows, C5's 2 x 272)
+    keep their LDS fragment reads in flight with counted waits (inline-asm ds_read_b128 +
+    s_waitcnt lgkmcnt(5), csrc/gemm.hip) and do not spill: the compiler's own schedule drains
+    every read with lgkmcnt(0) before its use (decode-step GEMMs)."""
+    import re
+    import subprocess
+    from importlib import import_module
+    build = import_module(pkg.__name__ + ".build")
+    hipcc = _hipcc_or_skip()
+    asm = tmp_path / "gemm.s"
+    flags = [f for f in build._flags() if f != "-fPIC"]
+    gemm = [s for s in build.SOURCES if s.endswith("gemm.hip")][0]
+    subprocess.run([hipcc] + flags + ["--cuda-device-only", "-S", gemm, "-o", str(asm)],
+                   check=True, capture_output=True)
+    text = asm.read_text()
+    names = re.findall(r"^(_Z\w*ws2_gemm_kernelILi17E\w+):", text, re.M)
+    assert names, "no 17-row-tile instantiation"
+    for n in names:
+        i = text.index(n + ":")
+        body = text[i:text.index(".Lfunc_end", i)]
+        meta = text[text.index(".Lfunc_end", i):]
+        assert "lgkmcnt(5)" in body, n
+        assert re.search(r"ScratchSize: (\d+)", meta).group(1) == "0", n
