@@ -14,6 +14,7 @@ run_bench() { timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench
 run_prof() {
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -f csv -- \
      python3 "$R/bench.py" --cpu-seconds 0 > "$OUT/prof.log" 2>&1) && \
+  python3 "$R/scripts/trace_by_grid.py" "$OUT/prof/run_kernel_trace.csv" > "$OUT/prof/run_kernel_by_grid.csv" && \
   rm -f "$OUT/prof/run_kernel_trace.csv"   # the per-dispatch trace exceeds gpurun's copy-back cap
 }
 run_pmc() {
