@@ -1003,13 +1003,14 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
   const int64_t per = static_cast<int64_t>(ldh) * D;                 // elements per (l, s, g)
   const int64_t so = (l * S_src + p) * Hkv * per, dn = (l * S + s) * Hkv * per;
   const int kv = hb * D / 8;                                          // K: hb * D contiguous
-  // V^T [ldh/32][D][32]: the full 32-slot tiles below hb whole, then in the last tile only
-  // the 16-byte units (8 slots) of each row that hold slots < hb (the rest of a row is
-  // weighted 0 by the attention and keeps the destination's earlier finite contents)
-  const int v_full = (hb / 32) * D * 4, v_ur = ((hb & 31) + 7) / 8;
-  const int vv = v_full + D * v_ur;
+  // V^T [ldh/32][D][32]: every 32-slot tile that holds a filled slot, whole — one
+  // contiguous span per head.  The last tile's slots >= hb come along (the parent's finite
+  // contents instead of the destination's; the attention weights them 0): copying only
+  // the 16-byte units below hb left 16-48 B holes in every 64-B row and ran at 2.4-4.5 TB/s
+  // against 6.3 with whole rows (profiles/r03i_hist_gather_tile_ab.jsonl)
+  const int vv = ((hb + 31) / 32) * D * 4;
   const int pv = static_cast<int>(per / 8);
-  const float inv_kv = 1.0f / kv, inv_vv = 1.0f / vv, inv_ur = 1.0f / (v_ur > 0 ? v_ur : 1);
+  const float inv_kv = 1.0f / kv, inv_vv = 1.0f / vv;
   const u32x4_t* sk = reinterpret_cast<const u32x4_t*>(src_k + so);
   const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(src_v + so);
   u32x4_t* dk = reinterpret_cast<u32x4_t*>(dst_k + dn);
@@ -1021,10 +1022,8 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
       const int g = fast_div(i, kv, inv_kv);
       return g * pv + (i - g * kv);
     }
-    const int iv = i - nk, g = fast_div(iv, vv, inv_vv), j = iv - g * vv;
-    if (j < v_full) return g * pv + j;
-    const int r = j - v_full, q = fast_div(r, v_ur, inv_ur);
-    return g * pv + v_full + q * 4 + (r - q * v_ur);
+    const int iv = i - nk, g = fast_div(iv, vv, inv_vv);
+    return g * pv + (iv - g * vv);
   };
   constexpr int U = 8;
   for (int i0 = threadIdx.x; i0 < n; i0 += 256 * U) {

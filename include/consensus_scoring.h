@@ -341,7 +341,8 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
  * j < *hist_base of stream parent[s] are copied,
  *     dst_k [l][s][g][j][:] = src_k [l][parent[s]][g][j][:]     ([L][S][Hkv][ld_hist][D])
  *     dst_vt[l][s][g][..]   = src_vt[l][parent[s]][g][..]      ([L][S][Hkv][ld_hist/32][D][32],
- *                                  the slots j < ceil8(hist_base); later slots keep dst's data)
+ *                                  every 32-slot tile holding a slot j < hist_base, whole;
+ *                                  later tiles keep dst's data)
  * src and dst distinct (a ping-pong pair).  hist_base in device memory (graph replays).
  *
  * Replaces: the reference's beams are strings re-encoded in full by every call

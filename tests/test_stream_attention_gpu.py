@@ -411,7 +411,7 @@ def test_gated_act_matches_torch(ops, dev, act):
                                              (2, 6, 4, 64, 128, 41), (1, 3, 2, 64, 64, 64)])
 def test_hist_gather_copies_filled_slots_of_the_parents(ops, dev, L, S, Hkv, ldh, D, hb):
     """cs_hist_gather: dst[l][s] = src[l][parent[s]] for the filled slots (K rows j < hb,
-    V^T slots j < ceil8(hb)); the rest of dst is left as it was."""
+    the V^T 32-slot tiles holding a slot j < hb, whole); the rest of dst is left as it was."""
     g = torch.Generator(device="cpu").manual_seed(L * 100 + S + hb)
     bf = torch.bfloat16
     sk = torch.randn(L, S, Hkv, ldh, D, generator=g).to(bf).to(dev)
@@ -503,14 +503,14 @@ def test_tree_gather_copies_parent_streams_between_levels(ops, dev, L, Ss, Sd, H
 
 
 def _check_gathered(sk, sv, dk, dv, parent, hb, ldh):
-    """K rows j < hb and V^T slots j < ceil8(hb) are the parent's; K rows from hb and V^T
-    slots from ceil8(hb) on are untouched (7.0)."""
+    """K rows j < hb and the V^T tiles holding a slot j < hb (whole 32-slot tiles) are the
+    parent's; K rows from hb and the later V^T tiles are untouched (7.0)."""
     ek = torch.full_like(dk, 7.0)
     if hb > 0:
         ek[:, :, :, :hb] = sk[:, parent][:, :, :, :hb]
     assert torch.equal(dk, ek)
     slot = torch.arange(ldh, device=dv.device).view(ldh // 32, 1, 32)     # [tile, 1, lane]
-    copied = slot < ((hb + 7) // 8) * 8
+    copied = slot < ((hb + 31) // 32) * 32
     want = torch.where(copied, sv[:, parent], torch.full_like(dv, 7.0))
     assert torch.equal(dv, want)
 
