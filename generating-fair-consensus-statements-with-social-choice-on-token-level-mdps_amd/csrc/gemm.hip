@@ -684,6 +684,9 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: operands must be 16-byte aligned (y 8-byte)");
   if (splits > 1 && !workspace)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: split K needs a workspace of splits * M * N floats");
+  // the split-K fold writes 16-byte vectors of 8 features at y + m * ldy + n
+  if (splits > 1 && y && (ldy % 8 || reinterpret_cast<uintptr_t>(y) & 15))
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16: a K split needs y 16-byte aligned and ldy % 8 == 0");
   const int64_t tiles = gemm_tiles(variant, M, N, gated);
   const int64_t blocks = tiles * splits;
   if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");

@@ -382,9 +382,11 @@ class BeamSearchGenerator(BaseGenerator):
             rest = self._text_rows(engine, U, rewards, cb, encs, nt, tail_ids, apis, texts,
                                    beam_ids, bad, inc)
         if rest:
-            users = [self._agent_users[a] + beams[cb[i]][0] + tstr[i] for a in range(A_loc)
-                     for i in rest]
-            lps = utils.text_compat_last(engine, tok, [BEAM["agent_system"]] * len(users), users)
+            # agent a's user text of candidate i is agent_user[a] + beam text + token: each
+            # (agent, beam) prompt re-tokenized once, each candidate's tail once
+            lps = utils.text_compat_last_stems(engine, tok, BEAM["agent_system"], self._agent_users,
+                                               [s for s, _ in beams], [cb[i] for i in rest],
+                                               [tstr[i] for i in rest])
             bi = torch.as_tensor(rest, dtype=torch.long, device=dev)
             par = torch.as_tensor([cb[i] for i in rest], dtype=torch.long, device=dev)
             lp = torch.as_tensor(lps, dtype=torch.float32, device=dev).view(A_loc, len(rest))
@@ -520,7 +522,9 @@ class BeamSearchGenerator(BaseGenerator):
             lg_buf = torch.empty(P * B, V, dtype=m.dtype, device=dev)
             ws_p = ops.Workspace()
             Wx = torch.empty(C, dtype=torch.float32, device=dev)
-            graphs = {}
+            # the score / select graphs live on the DecodeState, so ds.release() frees them
+            # with the step graphs (not whenever the cyclic collector reaches this frame)
+            graphs = st._graphs
 
             def propose():                     # in the step graph: LM head + proposer
                 m.lm_head(st.hidden, out=lg_buf)
@@ -556,6 +560,7 @@ class BeamSearchGenerator(BaseGenerator):
                     spec_inputs()
 
             def replay(name, fn):
+                name = ("sharded", name)
                 g = graphs.get(name)
                 if g is None and st.use_graphs and st.steps >= 2:
                     g = torch.cuda.CUDAGraph()

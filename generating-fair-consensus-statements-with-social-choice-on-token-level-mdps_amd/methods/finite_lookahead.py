@@ -116,6 +116,10 @@ class FiniteLookaheadGenerator(BaseGenerator):
         # bench hook: a list to collect (start, end, rows) HIP events of every step's
         # cs_logsoftmax_gather launch over the agent rows (stream path)
         self._lsg_events: Optional[list] = None
+        # parity-test hook (None in the product): an object whose draws(frontier, seeds, kid)
+        # returns the tree's draws and choose(chains, U, W, b) the committed path, so a
+        # replay can teacher-force the stream path onto a reference trace
+        self._teacher = None
         # stream path, tokenizers that are not merge-free: "text" (default) = the reference's
         # re-tokenized prompt + statement every step; "ids" = the committed token id appended
         self.retokenize = config.get("retokenize", "text")
@@ -285,7 +289,8 @@ class FiniteLookaheadGenerator(BaseGenerator):
             b = int(best.item())
             nxt = paths[b][0][0]
             self.trace.append({"paths": [p[0] for p in paths], "best": b,
-                               "rewards": parallel.gather_agents(U, shard)[:, b].double().cpu().tolist()})
+                               "rewards": parallel.gather_agents(U, shard)[:, b].double().cpu().tolist(),
+                               "welfare": W.double().cpu().tolist()})
             if nxt.strip() in ["DONE"]:
                 break
             if nxt in FL["stop_tokens"]:
@@ -327,10 +332,13 @@ class FiniteLookaheadGenerator(BaseGenerator):
             W = self.welfare(U, shard)
             best, _ = ops.topk(W, 1)
             b = int(best.item())
+            if self._teacher is not None:
+                b = self._teacher.choose(chains, U, W, b)
             first = chains[b][0]
             nxt = first.strs[0]
             self.trace.append({"paths": [ch[-1].strs for ch in chains], "best": b,
-                               "rewards": parallel.gather_agents(U, shard)[:, b].double().cpu().tolist()})
+                               "rewards": parallel.gather_agents(U, shard)[:, b].double().cpu().tolist(),
+                               "welfare": W.double().cpu().tolist()})
             if nxt.strip() in ["DONE"]:
                 break
             if nxt in FL["stop_tokens"]:
@@ -413,6 +421,8 @@ class FiniteLookaheadGenerator(BaseGenerator):
             sd = torch.tensor(seeds, dtype=torch.int64, device=dev)
             kid, _ = ops.vocab_sample(ref_lg, sd, temperature=1.0, softcap=engine.softcap)
             kid = parallel.broadcast_from_rank0(kid.contiguous(), shard)   # one tree on every rank
+            if self._teacher is not None:
+                kid = self._teacher.draws(frontier, bf, depth, kid)
             if A_loc:
                 if defer:
                     tg_all.append(kid.repeat(A_loc, 1))

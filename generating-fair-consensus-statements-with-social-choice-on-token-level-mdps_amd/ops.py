@@ -819,6 +819,11 @@ def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "s
             if splits > 1 else None)
     ldx = x.stride(0) if M > 1 else K
     ldy = out.stride(0) if M > 1 else n_out
+    if splits > 1 and (ldy % 8 or out.data_ptr() % 16):
+        # the split-K fold stores 16-byte vectors: fold into an aligned tensor, then copy
+        tmp = gemm(x, w, splits=splits, variant=variant)
+        out.copy_(tmp)
+        return out
     rc = L.cs_gemm_bf16(x.data_ptr(), ldx, w.data_ptr(), w.stride(0), out.data_ptr(), ldy, M, N,
                         K, splits, int(bool(gated)), {"silu": 0, "gelu_tanh": 1}[act], variant,
                         part.data_ptr() if part is not None else None, _stream())

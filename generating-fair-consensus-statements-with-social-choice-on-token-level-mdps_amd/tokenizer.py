@@ -339,6 +339,76 @@ class BPETokenizer:
     def encode_many(self, texts) -> List[List[int]]:
         return [e.ids for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
 
+    # ASCII probes for ascii_joins_text: spaces (leading, doubled, trailing), newlines,
+    # tabs, digits, punctuation, a marker-free trailing newline
+    _ASCII_PROBES = (("You are a fair judge.  Answer briefly.", " The  statement: 'fair', 42.\n"),
+                     ("Issue:\tprivacy\n\nOpinions follow.", "A\tB  c -- d ... e?!\n\nend "),
+                     (None, "  leading and trailing  "))
+
+    def ascii_joins_text(self) -> bool:
+        """Whether an ASCII chat prompt's token strings join to the rendered text itself --
+        true of byte-level BPEs (Llama-3), not of every tokenizer (a normalizer or a
+        Metaspace / Strip decoder changes the strings).  The callers' shortcut that decides
+        "the user text is found nowhere" by one search of the rendered text relies on it;
+        checked once per tokenizer on probe prompts."""
+        ok = getattr(self, "_ascii_join", None)
+        if ok is None:
+            ok = True
+            for system, user in self._ASCII_PROBES:
+                text = self.chat_text(system, user, True)
+                if "".join(self.tokens(self.encode(text))) != text:
+                    ok = False
+                    break
+            self._ascii_join = ok
+        return ok
+
+    # --- incremental re-tokenization ---------------------------------------------------
+    def incremental_ok(self) -> bool:
+        """Whether prompts may be re-tokenized incrementally (chat_frame / cut_point): no
+        normalizer (the pre-tokenizer's char offsets are the text's) and a pre-tokenizer
+        whose pieces BPE merges never cross (byte-level BPEs such as Llama-3's)."""
+        ok = getattr(self, "_inc_ok", None)
+        if ok is None:
+            ok = self.tk.normalizer is None and self.tk.pre_tokenizer is not None
+            # added tokens are split out of the text before pre-tokenization: content that
+            # holds one's first character is re-tokenized whole (added_token_chars)
+            self.added_token_chars = frozenset(
+                t.content[0] for t in self.tk.get_added_tokens_decoder().values() if t.content)
+            self._inc_ok = ok
+        return ok
+
+    def chat_frame(self, system: "str | None", user_prefix: str):
+        """(pre, post, seg): the rendered chat prompt around user content ``user_prefix + X``
+        -- chat_text(system, user_prefix + X) == pre + X + post for any X that does not end in
+        whitespace (the template trims only the content's ends) -- and seg, the offset in
+        ``pre`` after its last special token (the start of the text segment the pre-tokenizer
+        sees).  None when the template does not render content that way or ``post`` does not
+        open with a special token (which guarantees a token boundary after X)."""
+        text = self.chat_text(system, user_prefix + _SENTINEL, True)
+        i = text.find(_SENTINEL)
+        if i < 0:
+            return None
+        pre, post = text[:i], text[i + len(_SENTINEL):]
+        probe = " a, b:\n c.d"
+        if self.chat_text(system, user_prefix + probe, True) != pre + probe + post:
+            return None
+        specials = list(self.special_ids)
+        if not any(post.startswith(sp) for sp in specials):
+            return None
+        seg = max((pre.rfind(sp) + len(sp) for sp in specials if sp in pre), default=0)
+        return pre, post, seg
+
+    def cut_point(self, text: str, seg: int) -> int:
+        """A token boundary of ``text + X`` for every X: the start of the second-to-last
+        pre-token of text[seg:] (seg: a special-token boundary).  Pre-token matches before
+        it end at least one whole pre-token before the end of ``text``, so appended text
+        changes none of them (the split pattern looks ahead at most one character and never
+        behind), and BPE merges stay inside pre-tokens."""
+        pieces = self.tk.pre_tokenizer.pre_tokenize_str(text[seg:])
+        if len(pieces) < 2:
+            return seg
+        return seg + pieces[-2][1][0]
+
     def chat_prefix(self, system: "str | None", user_prefix: str) -> List[int]:
         """Ids of the chat prompt up to the end of ``user_prefix`` (the part of the user
         turn shared by every candidate), with nothing of the template after it: the

@@ -134,6 +134,18 @@ def last_user_span_index(tokens: Sequence[str], user_prompt: str) -> int:
 SPAN_AT_USER, SPAN_NONE, SPAN_ELSEWHERE = 1, 0, -1
 
 
+def _ascii_text_of(tok):
+    """tok.chat_text when the tokenizer's ASCII token strings join to the rendered text
+    (BPETokenizer.ascii_joins_text, checked once per tokenizer), else None: only then may
+    "the rendered ASCII text does not contain the user text" stand for the reference's
+    failed ``find`` in the joined token strings."""
+    chat_text = getattr(tok, "chat_text", None)
+    check = getattr(tok, "ascii_joins_text", None)
+    if chat_text is None or check is None or not check():
+        return None
+    return chat_text
+
+
 def span_check(tok, system_prompt, user_prompt) -> int:
     """Where the reference's first-occurrence ``find`` of the user prompt lands in the
     rendered prompt's token strings (src/utils.py:321-327): SPAN_AT_USER (the user turn
@@ -144,7 +156,7 @@ def span_check(tok, system_prompt, user_prompt) -> int:
     An ASCII prompt's token strings join to the rendered text itself, so SPAN_NONE is
     decided by one string search there, without encoding."""
     api_user = user_prompt + MARKER if user_prompt.endswith(("\n", " ")) else user_prompt
-    chat_text = getattr(tok, "chat_text", None)
+    chat_text = _ascii_text_of(tok)
     if chat_text is not None:
         text = chat_text(system_prompt or None, api_user, True)
         if text.isascii() and text.find(user_prompt) == -1:
@@ -282,7 +294,7 @@ def text_compat_last(engine, tok, systems: Sequence[Optional[str]],
     # fallback), decided without encoding -- the common case of re-scored beam candidates
     # whose statement begins with whitespace the chat template trims
     live = list(range(n))
-    chat_text = getattr(tok, "chat_text", None)
+    chat_text = _ascii_text_of(tok)
     texts = None
     if chat_text is not None:
         try:
@@ -308,9 +320,16 @@ def text_compat_last(engine, tok, systems: Sequence[Optional[str]],
             ids, k = [], -1
         idss[j] = list(ids)
         last[j] = k
-    todo = [j for j in range(n) if last[j] > 0]      # position 0 has no log-prob (None)
+    _last_logprobs(engine, idss, last, res)
+    return res
+
+
+def _last_logprobs(engine, idss, last, res) -> None:
+    """res[j] = log p(idss[j][last[j]] | idss[j][:last[j]]) for every j with last[j] > 0
+    (position 0 has no log-prob: None in the reference's list), in one batched prefill."""
+    todo = [j for j in range(len(idss)) if last[j] > 0]
     if not todo:
-        return res
+        return
     dev = engine.device
     cache = engine.prefill([idss[j][:last[j]] for j in todo])
     rows = cache.last_hidden
@@ -318,6 +337,186 @@ def text_compat_last(engine, tok, systems: Sequence[Optional[str]],
     lp = engine.rows_logprobs(rows, tgt[:, None]).view(-1).double().cpu().tolist()
     for j, v in zip(todo, lp):
         res[j] = float(v)
+
+
+_PERIODS: Dict[str, int] = {}
+
+
+def _min_period(u: str) -> int:
+    """The smallest period of ``u`` (prefix function); two occurrences of u in a text that
+    overlap start at least this far apart."""
+    p = _PERIODS.get(u)
+    if p is None:
+        pi = [0] * len(u)
+        k = 0
+        for i in range(1, len(u)):
+            while k and u[i] != u[k]:
+                k = pi[k - 1]
+            if u[i] == u[k]:
+                k += 1
+            pi[i] = k
+        p = len(u) - (pi[-1] if u else 0)
+        if len(_PERIODS) > 256:
+            _PERIODS.clear()
+        _PERIODS[u] = p
+    return p
+
+
+@torch.no_grad()
+def text_compat_last_stems(engine, tok, system: Optional[str], agent_users: Sequence[str],
+                           stems: Sequence[str], stem_of: Sequence[int], pieces: Sequence[str],
+                           fallback: float = -10.0) -> List[float]:
+    """text_compat_last for the users ``agent_users[a] + stems[stem_of[i]] + pieces[i]``
+    (a-major: entry a * n + i) under one system prompt -- a beam step's re-tokenized texts,
+    where every (agent, beam) shares its prompt up to the beam's statement and candidates
+    differ in one token (src/methods/beam_search.py:358-395 via src/utils.py:201-373).
+
+    Re-tokenized incrementally: each agent's chat prompt is rendered once around its user
+    text (BPETokenizer.chat_frame) and encoded once up to a pre-token boundary a few
+    pre-tokens before its end (cut_point: BPE merges never cross a pre-token, and appended
+    text changes no pre-token before the last one); the short text from there to a boundary
+    before the beam statement's end is encoded once per distinct string, each distinct
+    candidate tail (statement end + token + marker) once, the template's closing part once.
+    The reference's first-occurrence ``find`` of the user text in the joined token strings
+    is decided from the head's joined strings (the agent text's first occurrence there, and
+    its smallest period bounding any later occurrence) plus a short prefix test of the
+    tail's -- exactly the full-prompt search, without building ~A * B * K prompts.  Falls
+    back to text_compat_last for tokenizers or templates without these properties, and
+    checks one prompt per call against a full encode."""
+    A, n = len(agent_users), len(pieces)
+
+    def full_path():
+        users = [agent_users[a] + stems[stem_of[i]] + pieces[i] for a in range(A) for i in range(n)]
+        return text_compat_last(engine, tok, [system] * len(users), users, fallback)
+
+    ok = getattr(tok, "incremental_ok", None)
+    if ok is None or not ok() or getattr(tok, "_inc_disabled", False) or not n or not A:
+        return full_path()
+    cache = tok.__dict__.setdefault("_inc_cache", {})
+    if len(cache) > 4096:
+        cache.clear()
+    enc_later: Dict[str, Optional[List[int]]] = {}     # strings to encode in one batch
+
+    def frame_of(u):
+        key = ("frame", system, u)
+        fr = cache.get(key)
+        if fr is None:
+            fr = tok.chat_frame(system or None, u)
+            if fr is not None:
+                pre, post, seg = fr
+                y = tok.cut_point(pre, seg)
+                fr = (pre[:y], pre[y:], post)
+                enc_later.setdefault(fr[0], None)
+                enc_later.setdefault(post, None)
+            cache[key] = fr or False
+        return fr or None
+
+    frames = [frame_of(u) for u in agent_users]
+    if any(f is None for f in frames) or any(not u or u[0].isspace() for u in agent_users):
+        return full_path()
+    bad_chars = tok.added_token_chars
+    res = [float(fallback)] * (A * n)
+    conts = [stems[stem_of[i]] + pieces[i] for i in range(n)]
+    marks = [MARKER if c.endswith(("\n", " ")) else "" for c in conts]
+    # items whose rendering is not pre + api + post (api ends in other whitespace the template
+    # trims) or whose text could hold an added token: the full path
+    slow = [i for i in range(n)
+            if (conts[i] + marks[i])[-1:].isspace() or any(c in bad_chars for c in conts[i])]
+    slow_agents = {a for a in range(A) if any(c in bad_chars for c in agent_users[a])}
+    slow_set = set(slow)
+    groups: Dict[int, List[int]] = {}
+    for i in range(n):
+        if i not in slow_set:
+            groups.setdefault(stem_of[i], []).append(i)
+    # (mid + stem) -> (head part, tail part) at a pre-token boundary before the stem's end
+    split: Dict[str, Tuple[str, str]] = {}
+    for a in range(A):
+        if a in slow_agents:
+            continue
+        mid = frames[a][1]
+        for g in groups:
+            s_ = mid + stems[g]
+            if s_ not in split:
+                x = tok.cut_point(s_, 0)
+                split[s_] = (s_[:x], s_[x:])
+                enc_later.setdefault(s_[:x], None)
+                for i in groups[g]:
+                    enc_later.setdefault(s_[x:] + pieces[i] + marks[i], None)
+    todo_enc = [t for t, v in enc_later.items() if ("ids", t) not in cache]
+    for t, ids in zip(todo_enc, tok.encode_many(todo_enc) if todo_enc else []):
+        cache[("ids", t)] = ids
+    ids_of = lambda t: cache[("ids", t)]                                 # noqa: E731
+    jcache: Dict[str, str] = {}
+
+    def joined(t):
+        j = jcache.get(t)
+        if j is None:
+            ids = ids_of(t)
+            j = jcache[t] = "".join(tok.tokens(ids)) if ids else ""
+        return j
+
+    # one prompt per call against a full encode (a tokenizer outside the assumptions
+    # disables the incremental path for good)
+    probe = next(((a, i) for a in range(A) for i in range(n)
+                  if a not in slow_agents and i not in slow_set), None)
+    if probe is not None:
+        a, i = probe
+        base, mid, post = frames[a]
+        hm, tp = split[mid + stems[stem_of[i]]]
+        want = tok.encode(tok.chat_text(system or None, agent_users[a] + conts[i] + marks[i], True))
+        if want != ids_of(base) + ids_of(hm) + ids_of(tp + pieces[i] + marks[i]) + ids_of(post):
+            logger.warning("incremental re-tokenization disagrees with a full encode; "
+                           "re-tokenizing whole prompts from now on")
+            tok._inc_disabled = True
+            return full_path()
+    idss, last = [[] for _ in range(A * n)], [-1] * (A * n)
+    slow_items = []
+    decided: Dict[tuple, bool] = {}
+    for a in range(A):
+        if a in slow_agents:
+            slow_items += [(a, i) for i in range(n)]
+            continue
+        slow_items += [(a, i) for i in slow]
+        u = agent_users[a]
+        base, mid, post = frames[a]
+        jb, jq = joined(base), joined(post)
+        per = _min_period(u)
+        for g, items in groups.items():
+            hm, tp = split[mid + stems[g]]
+            jh = jb + joined(hm)
+            tkeys = [tp + pieces[i] + marks[i] for i in items]
+            f = jh.find(u)
+            longest = max(len(joined(t)) for t in tkeys)
+            # u occurs first at f; any other occurrence overlapping the search region starts
+            # at least min(period(u), len(u)) after f, and there is none when the text after
+            # f is shorter than that plus len(u)
+            unique = f >= 0 and len(jh) + longest + len(jq) - f - len(u) < min(per, len(u))
+            rest_h = jh[f + len(u):] if unique else ""
+            hid = None
+            for i, t in zip(items, tkeys):
+                if unique:
+                    key = (rest_h, t, post, i)
+                    hit = decided.get(key)
+                    if hit is None:
+                        hit = decided[key] = (rest_h + joined(t) + jq).startswith(conts[i])
+                    lo = f if hit else -1
+                else:
+                    lo = (jh + joined(t) + jq).find(u + conts[i])
+                if lo < 0:
+                    continue
+                if hid is None:
+                    hid = ids_of(base) + ids_of(hm)
+                ids = hid + ids_of(t) + ids_of(post)
+                end = lo + len(u) + len(conts[i])
+                j = a * n + i
+                idss[j] = ids
+                last[j] = bisect.bisect_left(list(itertools.accumulate(map(len, tok.tokens(ids)))), end)
+    if slow_items:
+        vals = text_compat_last(engine, tok, [system] * len(slow_items),
+                                [agent_users[a] + conts[i] for a, i in slow_items], fallback)
+        for (a, i), v in zip(slow_items, vals):
+            res[a * n + i] = v
+    _last_logprobs(engine, idss, last, res)
     return res
 
 

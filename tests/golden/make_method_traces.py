@@ -51,7 +51,15 @@ FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
             # C1 at its full horizon: the same Llama-3.2-1B-shaped fixture, beam 4 x 8
             # attempts over 50 tokens (configs/appendix/llama/scenario_1/beam_search.yaml:33-38
             # max_tokens 50): beams whose histories span two 32-slot tiles
-            "c1long": ("llama-3.2-1b-shaped-fixture", "method_traces_c1_long.json")}
+            "c1long": ("llama-3.2-1b-shaped-fixture", "method_traces_c1_long.json"),
+            # finite lookahead at the reference's main-body setting (configs/main_body/
+            # scenario_1.yaml:47-49: branching_factor 2, max_depth 4) on the C1-shaped
+            # fixture: 16 paths of 4 tokens per step, the depth-dependent seed schedule
+            # path_seed + i * (max_depth + 1) (finite_lookahead.py:298-301, 376-377)
+            "fl4": ("llama-3.2-1b-shaped-fixture", "method_traces_fl4.json"),
+            # Gemma-2's real head shape (C3: head_dim 256, query_pre_attn_scalar 256) with
+            # both soft-caps and the fixture's 8-token sliding window, 16 agents
+            "gemma256": ("tiny-gemma-d256-fixture", "method_traces_gemma256.json")}
 BPE_DIR = os.path.join(HERE, "bpe_fixture")
 # untied LM head: with the random tied embedding a shallow model's residual stream makes
 # the last token's own logit ~45 sigma above the rest (every draw repeats it); an
@@ -60,13 +68,14 @@ C1_OVERRIDES = {"n_layers": 2, "tie_embeddings": False}
 # the 16-agent Gemma-2 fixture with 64-wide heads (the stream attention kernels serve head
 # dims 64 / 128 / 256), so the same trace also pins the bf16 stream-decode path
 WIDE_OVERRIDES = {"head_dim": 64, "query_pre_attn_scalar": 64.0}
+GEMMA256_OVERRIDES = {"head_dim": 256, "query_pre_attn_scalar": 256.0}
 
 
 def fixture_model(family: str = "llama3"):
     """The seeded fixture model (CPU fp32) and tokenizer shared by both sides."""
     Mm = importlib.import_module(PKG + ".model")
     T = importlib.import_module(PKG + ".tokenizer")
-    if family in ("c1", "c1long"):
+    if family in ("c1", "c1long", "fl4"):
         cfg = Mm.preset("llama-3.2-1b", **C1_OVERRIDES)
         tok = T.CharTokenizer("llama3", vocab_size=cfg.vocab)
     elif family == "bpe":
@@ -76,7 +85,8 @@ def fixture_model(family: str = "llama3"):
         tok = T.CharTokenizer("llama3" if family == "llama3" else "gemma2")
         name = "tiny-llama" if family == "llama3" else "tiny-gemma"
         cfg = Mm.preset(name, vocab=tok.vocab_size,
-                        **(WIDE_OVERRIDES if family == "wide" else {}))
+                        **(WIDE_OVERRIDES if family == "wide" else
+                           GEMMA256_OVERRIDES if family == "gemma256" else {}))
     model = Mm.Model(cfg, "cpu", torch.float32, seed=WEIGHT_SEED)
     return cfg, model, tok
 
@@ -96,6 +106,22 @@ C1_RUNS = [
 C1_LONG_RUNS = [
     ("beam_search", {"beam_width": 4, "max_tokens": 50, "max_sampling_attempts": 8, "seed": 1,
                      "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+]
+
+
+FL4_RUNS = [
+    ("finite_lookahead", {"branching_factor": 2, "max_depth": 4, "max_tokens": 3, "seed": 11,
+                          "api_delay": 0, "log_level": "WARNING"}),
+]
+
+
+GEMMA256_RUNS = [
+    ("beam_search", {"beam_width": 4, "max_tokens": 4, "max_sampling_attempts": 8, "seed": 31,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+    ("best_of_n", {"n": 8, "max_tokens": 8, "seed": 27, "temperature": 1.0, "api_delay": 0,
+                   "log_level": "WARNING"}),
+    ("finite_lookahead", {"branching_factor": 2, "max_depth": 3, "max_tokens": 2, "seed": 29,
+                          "api_delay": 0, "log_level": "WARNING"}),
 ]
 
 
@@ -155,7 +181,7 @@ def main() -> None:
     scen = yaml.safe_load(open(os.path.join(args.reference, "configs", "appendix", "llama",
                                             "scenario_1", "beam_search.yaml")))["scenario"]
     issue, opinions = scen["issue"], dict(scen["agent_opinions"])
-    if args.family == "wide":
+    if args.family in ("wide", "gemma256"):
         texts = list(opinions.values())
         opinions = {f"Agent {i + 1}": f"{texts[i % len(texts)]} (participant {i + 1})"
                     for i in range(WIDE_AGENTS)}
@@ -182,17 +208,21 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
-           "family": ("llama3" if args.family in ("c1", "c1long", "bpe")
-                      else "gemma2" if args.family == "wide" else args.family),
+           "family": ("llama3" if args.family in ("c1", "c1long", "fl4", "bpe")
+                      else "gemma2" if args.family in ("wide", "gemma256") else args.family),
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
-    if args.family in ("c1", "c1long"):
+    if args.family in ("c1", "c1long", "fl4"):
         out["preset_overrides"] = dict(C1_OVERRIDES)
         out["tokenizer_vocab"] = cfg.vocab
     if args.family == "bpe":
         out["tokenizer"] = "bpe_fixture"
     if args.family == "wide":
         out["preset_overrides"] = dict(WIDE_OVERRIDES)
+    if args.family == "gemma256":
+        out["preset_overrides"] = dict(GEMMA256_OVERRIDES)
     runs = (C1_RUNS if args.family == "c1" else C1_LONG_RUNS if args.family == "c1long"
+            else FL4_RUNS if args.family == "fl4"
+            else GEMMA256_RUNS if args.family == "gemma256"
             else BPE_RUNS if args.family == "bpe"
             else WIDE_RUNS if args.family == "wide" else None) or [
         ("best_of_n", {"n": 4, "max_tokens": 24, "seed": 7, "temperature": 1.0, "api_delay": 0,
@@ -232,6 +262,38 @@ def main() -> None:
 
             gen._calculate_candidate_rewards = rec_rewards
             gen._calculate_egalitarian_welfare = rec_welfare
+        if method == "finite_lookahead" and args.family in ("fl4", "gemma256"):
+            # the reference's tree of every step and every one-token draw, so the bf16 replay
+            # can teacher-force the tree (its draws from bf16 logits could flip near-ties of
+            # the Gumbel argmax): each draw keyed by (statement + path so far, seed) -- the
+            # draw is a function of that prompt and seed (finite_lookahead.py:296-334)
+            static = gen._create_reference_continuation_prompt(issue, opinions, "")
+            extra["fl_steps"], extra["fl_draws"] = [], []
+            orig_tree = gen._generate_tree_paths
+            orig_first = gen._get_first_token_of_best_path
+            orig_gen_text = finite_lookahead.generate_text
+
+            def rec_tree(issue_, ops_, current, *a, **k):
+                paths = orig_tree(issue_, ops_, current, *a, **k)
+                extra["fl_steps"].append({"current": current, "paths": [list(p) for p in paths]})
+                return paths
+
+            def rec_first(*a, **k):
+                t = orig_first(*a, **k)
+                extra["fl_steps"][-1]["next_token"] = t
+                return t
+
+            def rec_gen_text(*a, **k):
+                out_text = orig_gen_text(*a, **k)
+                up = k.get("user_prompt")
+                assert up is not None and up.startswith(static) and k.get("max_tokens") == 1
+                extra["fl_draws"].append({"suffix": up[len(static):], "seed": k.get("seed"),
+                                          "text": out_text})
+                return out_text
+
+            gen._generate_tree_paths = rec_tree
+            gen._get_first_token_of_best_path = rec_first
+            finite_lookahead.generate_text = rec_gen_text
         if method == "mcts":
             extra["steps"] = []
             orig_best = gen._select_best_child
@@ -244,12 +306,14 @@ def main() -> None:
 
             gen._select_best_child = rec_best
         stmt = gen.generate_statement(issue, opinions)
+        if method == "finite_lookahead" and "fl_draws" in extra:
+            finite_lookahead.generate_text = orig_gen_text
         out["runs"].append({"method": method, "config": mcfg, "statement": stmt,
                             "pre_brushup": getattr(gen, "pre_brushup_statement", None),
                             "calls": list(calls), **extra})
         print(f"{method}: {stmt!r} ({len(calls)} scoring calls)")
 
-    if args.family == "c1long":      # tail-only echo log-probs: every recorded tail finite
+    if args.family in ("c1long", "fl4"):   # method runs only (no evaluator pass)
         import math
         assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
                    if v is not None), "a recorded tail reaches past the computed positions"

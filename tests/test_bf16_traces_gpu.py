@@ -232,3 +232,94 @@ def test_evaluator_fused_against_reference(bf16_traces):
             worst = max(worst, e)
             assert e <= TOL_BF16, (rec["statement"][:20], k, got[k], ref)
     _report(f"{traces['_file']} evaluator", "max_abs_avg_logprob_err", worst)
+
+
+class _FLTeacher:
+    """Teacher forcing of the finite-lookahead stream path (FiniteLookaheadGenerator._teacher)
+    onto a reference trace that recorded its tree and draws (make_method_traces.py fl4 /
+    gemma256): every one-token draw is the reference's (keyed by statement + path so far and
+    the reference's seed, finite_lookahead.py:296-334, 375-377), so the stream path scores
+    the reference's own trees; per step the product's per-(agent, path) rewards are compared
+    with the reference's (mean of the last len(path) span log-probs of its recorded calls,
+    finite_lookahead.py:490-520) and its choice with the reference's max-min (:527), then
+    the reference's path is committed."""
+
+    def __init__(self, traces, run, tok, dev):
+        prompts = importlib.import_module(mp.PKG + ".methods.prompts")
+        self.tok, self.dev = tok, dev
+        self.steps = run["fl_steps"]
+        self.draws = {(d["suffix"], d["seed"]): d["text"] for d in run["fl_draws"]}
+        self.users = [prompts.FL["agent_user"].format(issue=traces["issue"], opinion=op)
+                      for op in traces["agent_opinions"].values()]
+        self.tail = {c["user"]: c["tail"] for c in run["calls"]}
+        self.k = 0
+        self.max_err, self.checked, self.differing, self.errs = 0.0, 0, 0, []
+
+    def draws(self, frontier, bf, depth, kid):
+        cur = self.steps[self.k]["current"]
+        out = []
+        for n in frontier:
+            row = []
+            for i in range(bf):
+                seed = n.seed + i * (depth + 1)
+                text = self.draws[(cur + "".join(n.strs), seed)]
+                if text == "":
+                    row.append(self.tok.eos_ids[0])
+                else:
+                    ids = self.tok.encode(text)
+                    assert len(ids) == 1, (text, ids)
+                    row.append(ids[0])
+            out.append(row)
+        return torch.tensor(out, dtype=kid.dtype, device=kid.device)
+
+    def choose(self, chains, U, W, b):
+        st = self.steps[self.k]
+        paths = [ch[-1].strs for ch in chains]
+        assert paths == st["paths"], (self.k, "the forced tree is not the reference's")
+        Uc = U.double().cpu()
+        W_ref = []
+        for p, path in enumerate(paths):
+            stmt = st["current"] + "".join(path)
+            u_ref = []
+            for a, u in enumerate(self.users):
+                tail = self.tail[u + stmt]
+                vals = tail[-len(path):]
+                ref = sum(vals) / len(vals)
+                u_ref.append(ref)
+                e = abs(float(Uc[a, p]) - ref)
+                self.max_err = max(self.max_err, e)
+                self.checked += 1
+                if e > TOL_BF16:
+                    self.errs.append(f"step {self.k} path {p} agent {a}: {float(Uc[a, p]):.5f} "
+                                     f"vs reference {ref:.5f}")
+            W_ref.append(min(u_ref))
+        b_ref = max(range(len(paths)), key=lambda i: W_ref[i])       # first max (:527)
+        assert paths[b_ref][0] == st["next_token"], (self.k, paths[b_ref], st["next_token"])
+        if b != b_ref:
+            self.differing += 1
+            gap = W_ref[b_ref] - W_ref[b]
+            assert gap <= 2 * TOL_BF16, (self.k, b, b_ref, gap)
+        self.k += 1
+        return b_ref
+
+
+def test_lookahead_stream_teacher_forced_against_reference(bf16_traces):
+    traces, eng, tok = bf16_traces
+    methods = importlib.import_module(mp.PKG + ".methods")
+    runs = [r for r in traces["runs"] if r["method"] == "finite_lookahead" and "fl_draws" in r]
+    if not runs:
+        pytest.skip("trace records no lookahead tree")
+    for run in runs:
+        gen = methods.get_method_generator("finite_lookahead", dict(run["config"]),
+                                           traces["model_id"])
+        teacher = gen._teacher = _FLTeacher(traces, run, tok, eng.device)
+        stmt = gen.generate_statement(traces["issue"], dict(traces["agent_opinions"]))
+        assert gen.decode_path == "stream-tree", gen.decode_path
+        assert teacher.k == len(run["fl_steps"]), (teacher.k, len(run["fl_steps"]))
+        assert stmt == run["statement"], (stmt, run["statement"])
+        tag = f"{traces['_file']} lookahead bf {run['config']['branching_factor']} " \
+              f"d {run['config']['max_depth']}"
+        _report(tag, "max_abs_reward_err", teacher.max_err)
+        _report(tag, "rewards_checked", teacher.checked)
+        _report(tag, "choices_within_2tol_differing", teacher.differing)
+        assert not teacher.errs, "\n".join(teacher.errs[:20])

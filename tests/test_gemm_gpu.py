@@ -61,6 +61,22 @@ def test_gemm_strided_operands_and_out(ops, dev):
     assert torch.all(ob[:, N:] == 0)
 
 
+@pytest.mark.parametrize("col0", [0, 4])
+def test_gemm_split_k_into_strided_out(ops, dev, col0):
+    """A K split folds its partials with 16-byte stores: an out whose rows are only 8-byte
+    aligned (ld % 8 == 4, or a 4-column offset) must still get the split's exact result."""
+    M, N, K = 24, 256, 512
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.1).to(dev, torch.bfloat16)
+    want = ops.gemm(x, w, splits=4, variant=2)
+    ob = torch.zeros(M, N + 132, device=dev, dtype=torch.bfloat16)     # ld % 8 == 4
+    view = ob[:, col0:col0 + N]
+    ops.gemm(x, w, splits=4, variant=2, out=view)
+    assert torch.equal(view, want)
+    assert torch.all(ob[:, :col0] == 0) and torch.all(ob[:, col0 + N:] == 0)
+
+
 @pytest.mark.parametrize("variant", [1, 2, 4])
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
 @pytest.mark.parametrize("M,F,K", [(20, 512, 256), (272, 1024, 448), (300, 256, 128)])

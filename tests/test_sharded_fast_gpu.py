@@ -94,15 +94,8 @@ def _worker(rank, world, port, q):
             ops.vocab_sample = real
         if gs.decode_path != "stream-tree":
             out["errors"].append(f"FL decode path {gs.decode_path}")
-        for k, (a, b) in enumerate(zip(gs.trace, ge.trace)):
-            if a["paths"] != b["paths"]:
-                out["errors"].append(f"FL step {k}: trees differ")
-                break
-            d = max(abs(x - y) for x, y in zip(a["rewards"], b["rewards"]))
-            if a["best"] != b["best"]:
-                break
-            if d > tl.TOL_BF16:
-                out["errors"].append(f"FL step {k}: rewards differ by {d}")
+        out["errors"] += [f"FL {e}" for e in
+                          tl.check_fl_traces(gs.trace, ge.trace, len(opinions), "nash", ss, se)]
         out["fl"] = (ss, se)
         R.clear_engines()
         dist.barrier()

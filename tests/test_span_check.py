@@ -50,3 +50,25 @@ def test_span_check_agrees_with_the_reference_extraction(bpe, user, expect):
     else:
         assert where == U.SPAN_ELSEWHERE and kept
     assert U.span_found_at_user(bpe, SYSTEM, user) == (where == U.SPAN_AT_USER)
+
+
+def test_ascii_shortcut_only_for_tokenizers_whose_strings_join_to_the_text(bpe):
+    """The "found nowhere" shortcut searches the rendered ASCII text instead of the joined
+    token strings; a tokenizer whose normalizer changes ASCII text (here: lowercasing)
+    must not take it, and span_check must then agree with the reference's extraction."""
+    from tokenizers import normalizers
+
+    T = importlib.import_module(PKG + ".tokenizer")
+    U = importlib.import_module(PKG + ".utils")
+    assert bpe.ascii_joins_text()
+    low = T.BPETokenizer(os.path.join(HERE, "golden", "bpe_fixture"), "llama3", vocab_size=4096,
+                         use_config=True)
+    low.tk.normalizer = normalizers.Lowercase()
+    assert not low.ascii_joins_text()
+    assert U._ascii_text_of(low) is None and U._ascii_text_of(bpe) is not None
+    for user in ("genetic data should stay private.", "Genetic Data Should Stay Private."):
+        ids, _ = low.render_chat(SYSTEM, user)
+        _, lps = U.extract_user_prompt_logprobs(
+            SimpleNamespace(tokens=low.tokens(ids), token_logprobs=list(range(len(ids)))), user)
+        where = U.span_check(low, SYSTEM, user)
+        assert (where == U.SPAN_NONE) == (not lps), (user, where)
