@@ -174,7 +174,7 @@ def parse():
                          "('' disables)")
     ap.add_argument("--method-bon", type=int, default=1,
                     help="1: time BASELINE C2 through BestOfNGenerator.score_candidates too")
-    ap.add_argument("--method-text-steps", type=int, default=4,
+    ap.add_argument("--method-text-steps", type=int, default=8,
                     help="steps of a short statement timed with the re-tokenized text semantics")
     ap.add_argument("--method-statements", type=int, default=1,
                     help="timed generate_statement calls per method config")
@@ -189,6 +189,10 @@ def parse():
     ap.add_argument("--selftest-launch", action="store_true",
                     help="only launch the ranks, check the world size and print the agent split "
                          "(no GPU work; CPU-testable with --backend gloo)")
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="diagnostics, one GPU: run the method legs as rank 0 of an N-rank job "
+                         "(its agent shard, the sharded fast loop over a one-rank RCCL "
+                         "communicator): the per-GPU shapes of BASELINE's 8-GPU configs")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per launch (optional)")
     return ap.parse_args()
@@ -223,6 +227,30 @@ def init_dist(args):
         import torch.distributed as dist
         if world > 1:
             dist.init_process_group("gloo" if args.backend == "gloo" else args.backend)
+        return world, rank, local
+    if world == 1 and args.emulate_ranks > 1:
+        # rank 0 of an emulated N-rank job: a one-rank process group (collectives are the
+        # identity over it) and every method's agent shard as rank 0 of N would hold it
+        torch.cuda.set_device(0)
+        torch.distributed.init_process_group(
+            "nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+            device_id=torch.device("cuda", 0))
+        par = importlib.import_module(PKG_DIR + ".parallel")
+        n_emu = args.emulate_ranks
+        par.method_shard = lambda n_agents, config=None: par.AgentShard(n_agents, 0, n_emu)
+
+        def gather_emulated(U_local, shard, group=None):
+            # the other ranks' agents stand in as copies of this rank's rows (same shape
+            # and device work as the all-gather's result; values are not compared)
+            if shard.world == 1:
+                return U_local
+            pad = torch.full((shard.max_local(), U_local.shape[1]), float("nan"),
+                             dtype=U_local.dtype, device=U_local.device)
+            pad[:U_local.shape[0]] = U_local
+            return torch.cat([pad] * shard.world, 0)[
+                torch.as_tensor(shard.global_order(), device=U_local.device)]
+
+        par.gather_agents = gather_emulated
         return world, rank, local
     if world > 1 or os.environ.get("CS_BENCH_FORCE_SHARDED") == "1":
         if args.backend == "gloo":   # rehearsal: every rank on the one visible GPU
@@ -530,7 +558,9 @@ def method_leg_fl(name, args, world, rank, dev):
     k_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) if ev else None
     rows = float(np.mean([r for _, _, r in ev])) if ev else 0.0
     alg = rows * V * 2 + rows * 4 * 4 * 2
-    out = {"workload": mc["desc"], "agents": A, "agents_per_gpu": len(range(rank, A, world)),
+    out = {"workload": mc["desc"], "agents": A,
+           "agents_per_gpu": len(range(rank, A, max(world, args.emulate_ranks))),
+           **({"emulated_ranks": args.emulate_ranks} if args.emulate_ranks > 1 else {}),
            "branching_factor": mc["branching_factor"], "max_depth": mc["max_depth"],
            "decode_steps_per_s": 1.0 / step_s, "ms_per_step": step_s * 1e3,
            "paths_per_step": n_paths, "scorings_per_s": A * n_paths / step_s,
@@ -601,10 +631,17 @@ def method_leg(name, args, world, rank, dev):
     # the step alone: the same graph (advance + LM head + cs_beam_decode_step) replayed with
     # no host walk in between -> what the host adds per step
     graph_ms = None
+    n_ranks = max(world, args.emulate_ranks)
+    mine = list(range(rank, A, n_ranks))
     if world == 1:
-        graph_ms = _graph_step_ms(eng, tok, opinions, mc, dev)
+        # the rank's own agents' step (emulated ranks: the per-GPU shape, without the
+        # sharded loop's all-reduce and select graphs)
+        ops_l = list(opinions.items())
+        graph_ms = _graph_step_ms(eng, tok, dict(ops_l[a] for a in mine),
+                                  dict(mc, agents=len(mine)), dev)
     out = {"workload": mc["desc"], "agents": A, "beams": B, "top_k": K,
-           "agents_per_gpu": len(range(rank, A, world)),
+           "agents_per_gpu": len(mine),
+           **({"emulated_ranks": n_ranks} if args.emulate_ranks > 1 else {}),
            "decode_steps_per_s": 1.0 / step_s, "ms_per_step": step_s * 1e3,
            "scorings_per_s": A * B * K / step_s,
            "statement_s": float(np.median([r["statement_s"] for r in runs])),
@@ -631,7 +668,9 @@ def method_leg(name, args, world, rank, dev):
         gen.generate_statement(SCENARIO_ISSUE, opinions)
         _barrier_sync(world)
         d = np.diff(np.asarray(gen.step_times))
-        ms = _max_over_ranks(float(np.median(d[1:] if d.size > 1 else d)) * 1e3, world, dev)
+        # steps 0-2 run eagerly or capture the two step graphs: the steady steps after them
+        ms = _max_over_ranks(float(np.median(d[3:] if d.size > 4 else d[1:] if d.size > 1 else d))
+                             * 1e3, world, dev)
         n_cand = sum(len(s_["candidates"]) for s_ in gen.step_log)
         out["retokenize_text"] = {
             "ms_per_step": ms, "steps": gen.steps_run, "decode_path": gen.decode_path,

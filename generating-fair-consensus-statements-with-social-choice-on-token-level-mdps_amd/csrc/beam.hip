@@ -492,8 +492,21 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
 #define CS_PROP_PRIO 2   // instruction-issue priority of the proposer waves
 #endif
 #ifndef CS_DECODE_KP1024
-#define CS_DECODE_KP1024 8   // proposer keys per lane in the 1024-thread blocks (4 or this)
+#define CS_DECODE_KP1024 8   // proposer keys per lane in the 1024-thread fp32 blocks (4 or this)
 #endif
+#ifndef CS_DECODE_RAWKEYS
+#define CS_DECODE_RAWKEYS 1  // 16-bit logits: the proposer keeps the raw values, not 32-bit keys
+#endif
+#ifndef CS_DECODE_KP1024_RAW
+#define CS_DECODE_KP1024_RAW 16   // proposer elements per lane then (1024-thread blocks)
+#endif
+// elements per lane of a 1024-thread proposer chunk: 16-bit logits are held raw (two per
+// register) and their order keys recomputed on each pass, so twice the elements fit the
+// registers of the 32-bit keys -- half the proposer workgroups, and C3's whole grid
+// (256 agent rows + 16 beams x 16 chunks) is resident in one round on 256 CUs
+constexpr int kp1024(int dtype) {
+  return (CS_DECODE_RAWKEYS && dtype != CS_F32) ? CS_DECODE_KP1024_RAW : CS_DECODE_KP1024;
+}
 #ifndef CS_DECODE_UN1024
 #define CS_DECODE_UN1024 2   // 16-byte vectors in flight per lane in the 1024-thread rows
 #endif
@@ -519,8 +532,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
 // 16 would spill) that still gives >= 128 proposer workgroups, else 4 (few beams, e.g.
 // C5's B = 8), so the proposer finishes under the agent-row stream (tools/beam_ab.py
 // --sweep; profiles/r01f_beam_ab*.jsonl).  CS_DECODE_KP overrides (4, 8 or 16).
-int decode_kp(int32_t B, int64_t vocab, int32_t block, int32_t K) {
-  const int big = block >= 1024 ? CS_DECODE_KP1024 : 16;
+int decode_kp(int32_t B, int64_t vocab, int32_t block, int32_t K, int dtype) {
+  const int big = block >= 1024 ? kp1024(dtype) : 16;
   if (const char* e = getenv("CS_DECODE_KP")) {
     const int v = atoi(e);
     if (v == 4 || v == big) return v;
@@ -622,39 +635,84 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     const int64_t v0 = static_cast<int64_t>(chunk) * CH;
     const int n = static_cast<int>(min(static_cast<int64_t>(CH), vocab - v0));
     // 32-bit order keys in registers (the token id is implied by (j, lane)): half the
-    // registers of 64-bit composite keys, so the 1024-thread variant does not spill
-    uint32_t okey[KP];
+    // registers of 64-bit composite keys, so the 1024-thread variant does not spill.  RAW
+    // (16-bit logits): the raw values instead, two per register, each pass recomputing the
+    // identical key order_key(softcap(x)) from them (a few VALU ops per element per pass)
+    constexpr bool RAW = CS_DECODE_RAWKEYS && DT != CS_F32;
+    constexpr int NWORD = RAW ? (KP + 1) / 2 : KP;
+    uint32_t okey[NWORD];
     constexpr int EPV = Elt<DT>::kPerVec;
+    constexpr int RG = KP < EPV ? KP : EPV;   // RAW: consecutive elements per lane group
     const bool vec = KP % EPV == 0 && ref_vec && n == CH;
     if (vec) {
       // whole 16-byte-aligned chunk: KP / EPV non-temporal 16-byte loads per lane, all in
-      // flight at once (element (j / EPV * BLOCK + tid) * EPV + j % EPV in okey[j])
+      // flight at once (element (j / EPV * BLOCK + tid) * EPV + j % EPV in okey[j]; RAW: in
+      // half j % 2 of word j / 2, the loaded vectors as they are)
       const u32x4* vp = reinterpret_cast<const u32x4*>(rp + v0 * Elt<DT>::kSize);
       u32x4 q[KP / EPV > 0 ? KP / EPV : 1];
 #pragma unroll
       for (int j = 0; j < KP / EPV; ++j) q[j] = __builtin_nontemporal_load(vp + j * BLOCK + tid);
 #pragma unroll
       for (int j = 0; j < KP / EPV; ++j) {
-        float v[EPV];
-        unpack_vec<DT>(q[j], v);
+        if constexpr (RAW) {
 #pragma unroll
-        for (int e = 0; e < EPV; ++e)
-          okey[j * EPV + e] = order_key(CAP ? softcap_fn(v[e], cap, inv_cap) : v[e]);
+          for (int e = 0; e < 4; ++e) okey[j * 4 + e] = q[j][e];
+        } else {
+          float v[EPV];
+          unpack_vec<DT>(q[j], v);
+#pragma unroll
+          for (int e = 0; e < EPV; ++e)
+            okey[j * EPV + e] = order_key(CAP ? softcap_fn(v[e], cap, inv_cap) : v[e]);
+        }
       }
     } else {
+      if constexpr (RAW) {
+#pragma unroll
+        for (int w = 0; w < NWORD; ++w) okey[w] = 0u;
+      }
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
-        const int i = tid + BLOCK * j;
-        float x = 0.0f;
-        if (i < n) x = load_one<DT>(rp, v0 + i);
-        okey[j] = order_key(CAP ? softcap_fn(x, cap, inv_cap) : x);
+        // RAW: the vector path's element order (one index formula for both paths; groups
+        // of min(KP, EPV) consecutive elements per lane)
+        const int i = RAW ? (j / RG * BLOCK + tid) * RG + j % RG : tid + BLOCK * j;
+        if constexpr (RAW) {
+          const uint32_t b = i < n ? reinterpret_cast<const uint16_t*>(rp)[v0 + i] : 0u;
+          okey[j >> 1] |= b << ((j & 1) * 16);
+        } else {
+          float x = 0.0f;
+          if (i < n) x = load_one<DT>(rp, v0 + i);
+          okey[j] = order_key(CAP ? softcap_fn(x, cap, inv_cap) : x);
+        }
       }
     }
+    auto key32 = [&](int j) -> uint32_t {   // the order key of element j
+      if constexpr (RAW) {
+        const uint32_t b = (okey[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+        float x;
+        if constexpr (DT == CS_BF16) x = __uint_as_float(b << 16);
+        else x = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(b)));
+        return order_key(CAP ? softcap_fn(x, cap, inv_cap) : x);
+      } else {
+        return okey[j];
+      }
+    };
+    // RAW: before each pass over the keys the raw words are named as modified (an empty
+    // asm), so the compiler recomputes the keys per pass instead of hoisting all KP of them
+    // out of the radix loop into registers (which spills at 64 VGPRs)
+    int lbase = tid * RG;    // RAW: element j of this lane is lbase + (j / RG) * BLOCK * RG + j % RG
+    auto fresh = [&]() {
+      if constexpr (RAW) {
+#pragma unroll
+        for (int w = 0; w < NWORD; ++w) asm volatile("" : "+v"(okey[w]));
+        asm volatile("" : "+v"(lbase));   // nor the KP element indices
+      }
+    };
     auto local = [&](int j) -> int {   // element of okey[j] within the chunk
+      if constexpr (RAW) return lbase + (j / RG) * (BLOCK * RG) + j % RG;
       return vec ? (j / EPV * BLOCK + tid) * EPV + j % EPV : tid + BLOCK * j;
     };
     auto key_of = [&](int j) -> unsigned long long {
-      return (static_cast<unsigned long long>(okey[j]) << 32) |
+      return (static_cast<unsigned long long>(key32(j)) << 32) |
              static_cast<unsigned long long>(0xffffffffu - static_cast<uint32_t>(v0 + local(j)));
     };
     if (tid == 0) sm_n = 0u;
@@ -664,13 +722,15 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     // the agent-row stream more than the bound saves; profiles/r01h_decode_wave_bound.jsonl)
     if (CS_WB_ON(BLOCK, K)) {
       uint32_t lm = 0u;
+      fresh();
 #pragma unroll
       for (int j = 0; j < KP; ++j)
-        if (local(j) < n) lm = max(lm, okey[j]);
+        if (local(j) < n) lm = max(lm, key32(j));
       const uint32_t t = wave_bound<BLOCK>(lm, K, sm_tw);
+      fresh();
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
-        if (local(j) < n && okey[j] >= t) {
+        if (local(j) < n && key32(j) >= t) {
           const uint32_t at = atomicAdd(&sm_n, 1u);
           if (at < kTopkCand) sel_cand[at] = key_of(j);
         }
@@ -685,11 +745,13 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     if (!have) {
       const RadixCut cut = radix_select<BLOCK>(
           [&](auto f) {
+            fresh();
 #pragma unroll
             for (int j = 0; j < KP; ++j)
               if (local(j) < n) f(key_of(j));
           },
           static_cast<uint32_t>(K), static_cast<uint32_t>(2 * K + 64), hist, sm_tw, sm_res);
+      fresh();
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
         if (local(j) < n) {
@@ -1029,7 +1091,7 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   const int64_t rows = static_cast<int64_t>(A) * B;
   d.plan = plan_split(rows, vocab, dtype);
   d.block = d.plan.nsplit > 1 ? 256 : 1024;
-  d.kp = decode_kp(B, vocab, d.block, K);
+  d.kp = decode_kp(B, vocab, d.block, K, dtype);
   const int64_t ch = static_cast<int64_t>(d.kp) * d.block;
   d.nchunk_p = static_cast<int32_t>((vocab + ch - 1) / ch);
   d.lse_off = kBeamCounterBytes + 2 * sizeof(uint32_t) * kBeamMaxBeams;
@@ -1137,7 +1199,7 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
       else CS_DECODE_GO(DTV, CAPV, FIXV, 256, 8, 16);                                             \
     } else {                                                                                       \
       if (d.kp == 4) CS_DECODE_GO(DTV, CAPV, FIXV, 1024, CS_DECODE_UN1024, 4);                    \
-      else CS_DECODE_GO(DTV, CAPV, FIXV, 1024, CS_DECODE_UN1024, CS_DECODE_KP1024);               \
+      else CS_DECODE_GO(DTV, CAPV, FIXV, 1024, CS_DECODE_UN1024, kp1024(DTV));                   \
     }                                                                                              \
   } while (0)
   if (dtype == CS_F32) {

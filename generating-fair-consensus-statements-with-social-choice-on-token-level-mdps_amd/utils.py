@@ -420,9 +420,11 @@ def text_compat_last_stems(engine, tok, system: Optional[str], agent_users: Sequ
     marks = [MARKER if c.endswith(("\n", " ")) else "" for c in conts]
     # items whose rendering is not pre + api + post (api ends in other whitespace the template
     # trims) or whose text could hold an added token: the full path
-    slow = [i for i in range(n)
-            if (conts[i] + marks[i])[-1:].isspace() or any(c in bad_chars for c in conts[i])]
-    slow_agents = {a for a in range(A) if any(c in bad_chars for c in agent_users[a])}
+    def holds_added(text):
+        return any(c in text for c in bad_chars)
+
+    slow = [i for i in range(n) if (conts[i] + marks[i])[-1:].isspace() or holds_added(conts[i])]
+    slow_agents = {a for a in range(A) if holds_added(agent_users[a])}
     slow_set = set(slow)
     groups: Dict[int, List[int]] = {}
     for i in range(n):
@@ -469,9 +471,10 @@ def text_compat_last_stems(engine, tok, system: Optional[str], agent_users: Sequ
                            "re-tokenizing whole prompts from now on")
             tok._inc_disabled = True
             return full_path()
-    idss, last = [[] for _ in range(A * n)], [-1] * (A * n)
+    found: Dict[int, Tuple[List[int], int]] = {}      # a * n + i -> (prompt ids, last index)
     slow_items = []
-    decided: Dict[tuple, bool] = {}
+    ginfo: Dict[str, tuple] = {}           # per (mid + stem): the candidates' tails, joined
+    decided: Dict[tuple, List[int]] = {}   # per (mid + stem, head rest, post): the hits
     for a in range(A):
         if a in slow_agents:
             slow_items += [(a, i) for i in range(n)]
@@ -480,43 +483,62 @@ def text_compat_last_stems(engine, tok, system: Optional[str], agent_users: Sequ
         u = agent_users[a]
         base, mid, post = frames[a]
         jb, jq = joined(base), joined(post)
-        per = _min_period(u)
+        per = min(_min_period(u), len(u))
         for g, items in groups.items():
-            hm, tp = split[mid + stems[g]]
-            jh = jb + joined(hm)
-            tkeys = [tp + pieces[i] + marks[i] for i in items]
+            key_s = mid + stems[g]
+            info = ginfo.get(key_s)
+            if info is None:
+                hm, tp = split[key_s]
+                tkeys = [tp + pieces[i] + marks[i] for i in items]
+                jts = [joined(t) for t in tkeys]
+                info = ginfo[key_s] = (hm, tkeys, jts, max(map(len, jts)), joined(hm))
+            hm, tkeys, jts, longest, jhm = info
+            jh = jb + jhm
             f = jh.find(u)
-            longest = max(len(joined(t)) for t in tkeys)
             # u occurs first at f; any other occurrence overlapping the search region starts
             # at least min(period(u), len(u)) after f, and there is none when the text after
             # f is shorter than that plus len(u)
-            unique = f >= 0 and len(jh) + longest + len(jq) - f - len(u) < min(per, len(u))
-            rest_h = jh[f + len(u):] if unique else ""
-            hid = None
-            for i, t in zip(items, tkeys):
-                if unique:
-                    key = (rest_h, t, post, i)
-                    hit = decided.get(key)
-                    if hit is None:
-                        hit = decided[key] = (rest_h + joined(t) + jq).startswith(conts[i])
-                    lo = f if hit else -1
-                else:
-                    lo = (jh + joined(t) + jq).find(u + conts[i])
-                if lo < 0:
-                    continue
-                if hid is None:
-                    hid = ids_of(base) + ids_of(hm)
+            if f >= 0 and len(jh) + longest + len(jq) - f - len(u) < per:
+                rest_h = jh[f + len(u):]
+                dkey = (key_s, rest_h, jq)
+                hits = decided.get(dkey)
+                if hits is None:
+                    hits = decided[dkey] = [x for x, (i, jt) in enumerate(zip(items, jts))
+                                            if (rest_h + jt + jq).startswith(conts[i])]
+                los = [(x, f) for x in hits]
+            else:
+                los = []
+                for x, (i, jt) in enumerate(zip(items, jts)):
+                    lo = (jh + jt + jq).find(u + conts[i])
+                    if lo >= 0:
+                        los.append((x, lo))
+            if not los:
+                continue
+            hid = ids_of(base) + ids_of(hm)
+            hends = list(itertools.accumulate(map(len, tok.tokens(hid)))) if hid else []
+            for x, lo in los:
+                i, t = items[x], tkeys[x]
                 ids = hid + ids_of(t) + ids_of(post)
                 end = lo + len(u) + len(conts[i])
-                j = a * n + i
-                idss[j] = ids
-                last[j] = bisect.bisect_left(list(itertools.accumulate(map(len, tok.tokens(ids)))), end)
+                if end <= len(jh):
+                    k = bisect.bisect_left(hends, end)
+                elif end <= len(jh) + len(jts[x]):
+                    tends = list(itertools.accumulate(map(len, tok.tokens(ids_of(t)))))
+                    k = len(hid) + bisect.bisect_left(tends, end - len(jh))
+                else:
+                    k = bisect.bisect_left(list(itertools.accumulate(map(len, tok.tokens(ids)))), end)
+                found[a * n + i] = (ids, k)
     if slow_items:
         vals = text_compat_last(engine, tok, [system] * len(slow_items),
                                 [agent_users[a] + conts[i] for a, i in slow_items], fallback)
         for (a, i), v in zip(slow_items, vals):
             res[a * n + i] = v
-    _last_logprobs(engine, idss, last, res)
+    if found:
+        js = list(found)
+        sub = [float(fallback)] * len(js)
+        _last_logprobs(engine, [found[j][0] for j in js], [found[j][1] for j in js], sub)
+        for j, v in zip(js, sub):
+            res[j] = v
     return res
 
 

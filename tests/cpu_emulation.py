@@ -48,8 +48,14 @@ def _tk(W, k, with_values=True):
     return (out[0], vals[0]) if W.dim() == 1 else (out, vals)
 
 
-def _vs(logits, seeds, *, temperature=1.0, vocab=None, softcap=0.0, workspace=None):
+def _capped(logits, softcap):
+    """The logits the kernels draw from: cap * tanh(x / cap) when soft-capped (Gemma-2)."""
     x = logits.detach().float().double().numpy()
+    return softcap * np.tanh(x / softcap) if softcap and softcap > 0 else x
+
+
+def _vs(logits, seeds, *, temperature=1.0, vocab=None, softcap=0.0, workspace=None):
+    x = _capped(logits, softcap)
     sd = seeds.reshape(x.shape[0], -1).numpy().astype(np.int64)
     ids = np.zeros(sd.shape, dtype=np.int32)
     lps = np.zeros(sd.shape, dtype=np.float32)
@@ -61,7 +67,7 @@ def _vs(logits, seeds, *, temperature=1.0, vocab=None, softcap=0.0, workspace=No
 
 
 def _vt(logits, k, *, vocab=None, softcap=0.0, workspace=None):
-    ids, vals = orc.vocab_topk(logits.detach().double().numpy(), k)
+    ids, vals = orc.vocab_topk(_capped(logits, softcap), k)
     return torch.as_tensor(ids), torch.as_tensor(vals, dtype=torch.float32)
 
 

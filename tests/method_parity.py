@@ -28,7 +28,11 @@ TOL = 1e-3
 # + 16 agents on the Gemma-2 fixture with beam width 8, BoN N = 8, FL bf 3 (wider than the
 # appendix scenario; ~1 min of the CPU suite)
 TRACE_FILES = ["method_traces.json", "method_traces_gemma.json", "method_traces_bpe.json",
-               "method_traces_wide.json"]
+               "method_traces_wide.json",
+               # Gemma-2's real head shape (head_dim 256, query_pre_attn_scalar 256, both
+               # soft-caps, the 8-token sliding window) with 16 agents; its lookahead run
+               # records the reference's tree and draws (make_method_traces.py gemma256)
+               "method_traces_gemma256.json"]
 # BASELINE C1 shape (Llama-3.2-1B widths and vocabulary, 2 layers; beam 4, BoN N = 8, FL
 # bf 3 / depth 2): replayed on the GPU (the CPU emulation of its 128,256-wide LM head
 # over ~700 reference scoring calls is too slow for the CPU suite)

@@ -41,7 +41,13 @@ pytestmark = pytest.mark.gpu
 
 # absolute per-agent log-prob tolerance of the bf16 path against the fp32 reference
 TOL_BF16 = 0.06
-BF16_TRACE_FILES = ["method_traces_c1.json", "method_traces_wide.json"]
+# ... and of its MEAN over a trace (absolute and signed): bf16 rounding scatters the errors
+# around zero, so a systematic error of a few 1e-2 that TOL_BF16 alone would let through
+# moves the mean (measured means are printed and recorded in DESIGN.md)
+TOL_BF16_MEAN = 0.01
+BF16_TRACE_FILES = ["method_traces_c1.json", "method_traces_wide.json",
+                    # Gemma-2 head_dim 256 (C3's head shape), soft-caps, sliding window
+                    "method_traces_gemma256.json"]
 _REPORT = {}
 
 
@@ -103,7 +109,8 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
         orig_walk = gen._walk
         orig_final = gen._final
         st = {"step": 0, "beams": [""], "R_ref": {"": [0.0] * A}, "R_bf": {"": [0.0] * A},
-              "U_ref_of": {}, "max_err": 0.0, "checked": 0, "sel_checked": 0,
+              "U_ref_of": {}, "max_err": 0.0, "sum_err": 0.0, "sum_signed": 0.0, "checked": 0,
+              "sel_checked": 0,
               "sel_waived": 0, "errs": []}
 
         def propose(s_, ref_idx, bias, seed, tok_):
@@ -132,6 +139,8 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
                 for a in range(A):
                     e = abs(inc[a] - ref[a])
                     st["max_err"] = max(st["max_err"], e)
+                    st["sum_err"] += e
+                    st["sum_signed"] += inc[a] - ref[a]
                     st["checked"] += 1
                     if e > TOL_BF16:
                         st["errs"].append(f"step {st['step']} cand {texts[i][-8:]!r} agent {a}: "
@@ -187,10 +196,16 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
         assert st["step"] == len(ref_steps)
         tag = f"{traces['_file']} beam {run['config']['beam_width']}"
         _report(tag, "max_abs_increment_err", st["max_err"])
+        mean_abs = st["sum_err"] / max(1, st["checked"])
+        mean_signed = st["sum_signed"] / max(1, st["checked"])
+        _report(tag, "mean_abs_increment_err", mean_abs)
+        _report(tag, "mean_signed_increment_err", mean_signed)
         _report(tag, "increments_checked", st["checked"])
         _report(tag, "selections_checked", st["sel_checked"])
         _report(tag, "selections_within_2tol_differing", st["sel_waived"])
         assert not st["errs"], "\n".join(st["errs"][:20])
+        # bf16 rounding errors scatter around zero: a systematic error shows in the mean
+        assert mean_abs <= TOL_BF16_MEAN and abs(mean_signed) <= TOL_BF16_MEAN, (mean_abs, mean_signed)
         # the final choice over cumulative rewards (errors add up over the steps)
         if st["final_gap"] > 2 * TOL_BF16 * st["step"]:
             assert stmt == run["statement"], (stmt, run["statement"], st["final_gap"])
@@ -248,12 +263,13 @@ class _FLTeacher:
         prompts = importlib.import_module(mp.PKG + ".methods.prompts")
         self.tok, self.dev = tok, dev
         self.steps = run["fl_steps"]
-        self.draws = {(d["suffix"], d["seed"]): d["text"] for d in run["fl_draws"]}
+        self.table = {(d["suffix"], d["seed"]): d["text"] for d in run["fl_draws"]}
         self.users = [prompts.FL["agent_user"].format(issue=traces["issue"], opinion=op)
                       for op in traces["agent_opinions"].values()]
         self.tail = {c["user"]: c["tail"] for c in run["calls"]}
         self.k = 0
         self.max_err, self.checked, self.differing, self.errs = 0.0, 0, 0, []
+        self.sum_err = self.sum_signed = 0.0
 
     def draws(self, frontier, bf, depth, kid):
         cur = self.steps[self.k]["current"]
@@ -262,7 +278,7 @@ class _FLTeacher:
             row = []
             for i in range(bf):
                 seed = n.seed + i * (depth + 1)
-                text = self.draws[(cur + "".join(n.strs), seed)]
+                text = self.table[(cur + "".join(n.strs), seed)]
                 if text == "":
                     row.append(self.tok.eos_ids[0])
                 else:
@@ -288,6 +304,8 @@ class _FLTeacher:
                 u_ref.append(ref)
                 e = abs(float(Uc[a, p]) - ref)
                 self.max_err = max(self.max_err, e)
+                self.sum_err += e
+                self.sum_signed += float(Uc[a, p]) - ref
                 self.checked += 1
                 if e > TOL_BF16:
                     self.errs.append(f"step {self.k} path {p} agent {a}: {float(Uc[a, p]):.5f} "
@@ -320,6 +338,11 @@ def test_lookahead_stream_teacher_forced_against_reference(bf16_traces):
         tag = f"{traces['_file']} lookahead bf {run['config']['branching_factor']} " \
               f"d {run['config']['max_depth']}"
         _report(tag, "max_abs_reward_err", teacher.max_err)
+        mean_abs = teacher.sum_err / max(1, teacher.checked)
+        mean_signed = teacher.sum_signed / max(1, teacher.checked)
+        _report(tag, "mean_abs_reward_err", mean_abs)
+        _report(tag, "mean_signed_reward_err", mean_signed)
         _report(tag, "rewards_checked", teacher.checked)
         _report(tag, "choices_within_2tol_differing", teacher.differing)
         assert not teacher.errs, "\n".join(teacher.errs[:20])
+        assert mean_abs <= TOL_BF16_MEAN and abs(mean_signed) <= TOL_BF16_MEAN, (mean_abs, mean_signed)
