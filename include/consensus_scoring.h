@@ -435,6 +435,29 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
 /* cs_gemm_splits — the K split cs_gemm_bf16 takes for splits <= 0 (>= 1; 0 on a bad shape). */
 int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant);
 
+/*
+ * cs_gemm_bf16_streamk — cs_gemm_bf16 (variants 2-4, plain or gated; variant 1 maps to 3 /
+ * 2) with the tiles' K steps divided evenly over `blocks` workgroups (stream-K; blocks <= 0:
+ * one per CU): every CU gets the same number of K steps, with no partly idle last round of
+ * tiles.  A tile cut by a workgroup boundary is finished by the workgroup holding its first
+ * K step, which adds the later pieces' fp32 accumulators in piece order (a fixed order:
+ * deterministic, and equal to cs_gemm_bf16 within fp32 reassociation).  workspace: at least
+ * cs_gemm_streamk_workspace_size() bytes, 256-byte aligned (its hand-off flags are cleared
+ * on `stream` by the call itself).  Same operand rules as cs_gemm_bf16 (y required).
+ *
+ * Replaces: the same projections of the remote forward as cs_gemm_bf16
+ *   (src/utils.py:249-259).
+ */
+int cs_gemm_bf16_streamk(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y,
+                         int64_t ldy, int64_t M, int64_t N, int64_t K, int gated, int act,
+                         int variant, int32_t blocks, void* workspace, size_t workspace_bytes,
+                         cs_stream_t stream);
+
+/* cs_gemm_streamk_workspace_size — bytes of workspace cs_gemm_bf16_streamk needs (0 on a
+ * bad shape). */
+size_t cs_gemm_streamk_workspace_size(int64_t M, int64_t N, int64_t K, int gated, int variant,
+                                      int32_t blocks);
+
 #ifdef __cplusplus
 }
 #endif

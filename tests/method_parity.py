@@ -36,7 +36,13 @@ TRACE_FILES = ["method_traces.json", "method_traces_gemma.json", "method_traces_
 # BASELINE C1 shape (Llama-3.2-1B widths and vocabulary, 2 layers; beam 4, BoN N = 8, FL
 # bf 3 / depth 2): replayed on the GPU (the CPU emulation of its 128,256-wide LM head
 # over ~700 reference scoring calls is too slow for the CPU suite)
-GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json"]
+GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json",
+                                  # BASELINE C1 at its full 50-token horizon (beam 4 x 8
+                                  # attempts; histories span two 32-slot V^T tiles)
+                                  "method_traces_c1_long.json",
+                                  # finite lookahead at the reference's main-body setting
+                                  # (branching 2, depth 4) on the C1-shaped fixture
+                                  "method_traces_fl4.json"]
 
 
 def load_traces(name: str = "method_traces.json"):

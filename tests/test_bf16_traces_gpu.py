@@ -47,7 +47,11 @@ TOL_BF16 = 0.06
 TOL_BF16_MEAN = 0.01
 BF16_TRACE_FILES = ["method_traces_c1.json", "method_traces_wide.json",
                     # Gemma-2 head_dim 256 (C3's head shape), soft-caps, sliding window
-                    "method_traces_gemma256.json"]
+                    "method_traces_gemma256.json",
+                    # C1 at 50 tokens: the bf16 step graphs over two V^T tiles of history
+                    "method_traces_c1_long.json",
+                    # lookahead branching 2 / depth 4, teacher-forced on the reference's trees
+                    "method_traces_fl4.json"]
 _REPORT = {}
 
 

@@ -123,3 +123,48 @@ def test_split_partials_folded_by_add_rms_norm_is_bitwise(ops, dev, M, d, K, spl
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
     assert torch.equal(a_got, a_ref)
+
+
+@pytest.mark.parametrize("M,N,K,gated,variant", [
+    (520, 57344 // 8, 8192 // 4, 0, 2),     # C5 rows (2 row blocks), cut tiles
+    (272, 8192, 3584, 0, 2),                # C3 q|k|v shape
+    (272, 3584, 4096, 0, 3),                # 128-column tiles
+    (37, 2048, 1024, 0, 2),                 # ragged rows, few units per block
+    (520, 2 * 3584, 2048, 1, 2),            # gated (act(gate) * up epilogue)
+    (20, 256, 128, 0, 2),                   # fewer units than CUs
+])
+def test_gemm_streamk_matches_the_unsplit_gemm(ops, dev, M, N, K, gated, variant):
+    """Stream-K (splits = -1): within fp32 reassociation of the unsplit kernel, and bitwise
+    run to run (pieces are added in a fixed order)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    ref = ops.gemm(x, w, gated=bool(gated), splits=1, variant=variant)
+    got = ops.gemm(x, w, gated=bool(gated), splits=-1, variant=variant)
+    again = ops.gemm(x, w, gated=bool(gated), splits=-1, variant=variant)
+    assert torch.equal(got, again)
+    want = x.float() @ w.float().t()
+    if gated:
+        F = N // 2
+        want = ops.gated_act(want[:, :F].to(torch.bfloat16), want[:, F:].to(torch.bfloat16), "silu")
+        assert (got.float() - ref.float()).abs().max() <= 0.02 * ref.float().abs().max() + 1e-2
+    else:
+        assert torch.all((got.float() - want).abs() <= _tol(want))
+        # bf16 outputs of two fp32 sums of the same terms: at most one rounding step apart
+        assert torch.all((got.float() - ref.float()).abs() <= 2 * _tol(want))
+
+
+def test_gemm_streamk_finishes_when_the_grid_is_not_resident(ops, dev):
+    """Twice as many workgroups as CUs: heads wait for pieces whose workgroups are not yet
+    resident, time out and compute them themselves -- the same bits as the resident run."""
+    M, N, K = 272, 4096, 2048
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    base = ops.gemm(x, w, splits=-1, variant=2, sk_blocks=n_cu)
+    over = ops.gemm(x, w, splits=-1, variant=2, sk_blocks=2 * n_cu)
+    torch.cuda.synchronize()
+    want = x.float() @ w.float().t()
+    assert torch.all((over.float() - want).abs() <= _tol(want))
+    assert torch.all((base.float() - want).abs() <= _tol(want))

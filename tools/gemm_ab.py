@@ -111,7 +111,8 @@ def main():
             scale = ref.abs().max().item()
             t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), splits=sp, variant=var)
                                for i in range(calls)]) / calls * 1e3
-            eff = int(ops._lib.load().cs_gemm_splits(M, N, K, gated, var)) if sp <= 0 else sp
+            eff = ("sk" if sp < 0 else
+                   int(ops._lib.load().cs_gemm_splits(M, N, K, gated, var)) if sp == 0 else sp)
             yb = y.contiguous().view(torch.int16).to(torch.int64)
             ysig = int(((yb * torch.arange(1, yb.numel() + 1, device=dev).view_as(yb)) % 1000003).sum().item())
             rec = {"lib": os.path.basename(args.lib) or "tree", "ysig": ysig,
