@@ -589,7 +589,7 @@ template <int MT, int NT, int GATED, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 1) void sk_gemm_kernel(
     const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
     uint16_t* __restrict__ Y, int64_t ldy, int64_t M, int64_t n_out, int64_t gate_off, int nk,
-    int m_blocks, int units, uint32_t* __restrict__ flags, float* __restrict__ slots,
+    int n_tiles, int units, uint32_t* __restrict__ flags, float* __restrict__ slots,
     int act) {
   using S = Ws2Shape<MT, NT, WAVES>;
   __shared__ __align__(16) unsigned char lds[S::kLds];
@@ -644,8 +644,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void sk_gemm_kernel(
     const int tile = __builtin_amdgcn_readfirstlane(u / nk);
     const int k0 = u - tile * nk;
     const int len = min(nk - k0, u1 - u);
-    const int nt = __builtin_amdgcn_readfirstlane(tile / m_blocks);
-    const int m0 = (tile - nt * m_blocks) * S::kRows;
+    // tiles row-block-major: with G a multiple of 16, workgroups b and b + G / m_blocks
+    // (the same XCD) take the same column tile's K range of two row blocks at about the
+    // same time, so W is read from HBM once and from that XCD's L2 the second time
+    const int mb = __builtin_amdgcn_readfirstlane(tile / n_tiles);
+    const int nt = tile - mb * n_tiles;
+    const int m0 = mb * S::kRows;
     if (!first) __syncthreads();     // every wave is done with the previous segment's LDS
     first = false;
     gf32x4 acc[MT][NT];
@@ -792,19 +796,19 @@ void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t
 template <int MT, int NT, int GATED>
 void launch_sk(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
                int64_t ldw, uint16_t* Y, int64_t ldy, int64_t M, int64_t n_out, int64_t gate_off,
-               int nk, int m_blocks, int units, uint32_t* flags, float* slots, int act) {
+               int nk, int n_tiles, int units, uint32_t* flags, float* slots, int act) {
   hipLaunchKernelGGL((sk_gemm_kernel<MT, NT, GATED, 8>), dim3(blocks), dim3(512), 0, st, X, ldx, W,
-                     ldw, Y, ldy, M, n_out, gate_off, nk, m_blocks, units, flags, slots, act);
+                     ldw, Y, ldy, M, n_out, gate_off, nk, n_tiles, units, flags, slots, act);
 }
 
 template <int NT, int GATED>
 void dispatch_sk(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
                  const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, int64_t M, int64_t n_out,
-                 int64_t gate_off, int nk, int m_blocks, int units, uint32_t* flags,
+                 int64_t gate_off, int nk, int n_tiles, int units, uint32_t* flags,
                  float* slots, int act) {
 #define CS_SK_CASE(V)                                                                            \
   case V:                                                                                        \
-    launch_sk<V, NT, GATED>(blocks, st, X, ldx, W, ldw, Y, ldy, M, n_out, gate_off, nk, m_blocks, \
+    launch_sk<V, NT, GATED>(blocks, st, X, ldx, W, ldw, Y, ldy, M, n_out, gate_off, nk, n_tiles,  \
                             units, flags, slots, act);                                           \
     break;
   switch (mt) {
@@ -1008,15 +1012,15 @@ int cs_gemm_bf16_streamk(const void* x, int64_t ldx, const void* w, int64_t ldw,
   const uint16_t* Wp = static_cast<const uint16_t*>(w);
   uint16_t* Y = static_cast<uint16_t*>(y);
   const int nk = static_cast<int>(K / kGemmBK);
-  const int mbi = static_cast<int>(p.mb);
+  const int nti = static_cast<int>(p.n_tiles);
   if (gated)
-    dispatch_sk<2, 1>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N / 2, N / 2, nk, mbi,
+    dispatch_sk<2, 1>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N / 2, N / 2, nk, nti,
                       static_cast<int>(p.units), flags, slots, act);
   else if (p.variant == 3)
-    dispatch_sk<1, 0>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N, 0, nk, mbi,
+    dispatch_sk<1, 0>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N, 0, nk, nti,
                       static_cast<int>(p.units), flags, slots, 0);
   else
-    dispatch_sk<2, 0>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N, 0, nk, mbi,
+    dispatch_sk<2, 0>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N, 0, nk, nti,
                       static_cast<int>(p.units), flags, slots, 0);
   return check_launch("cs_gemm_bf16_streamk");
 }

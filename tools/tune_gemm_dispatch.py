@@ -7,7 +7,7 @@ model reads (ops.gemm_choice; read-only at run time).
 Shapes: the q|k|v, output, gate|up (plain and with the gated activation fused), down and
 LM-head GEMMs of the C1 / C3 / C5 beam-search decode steps, at every agent shard of 1, 2,
 4 and 8 ranks (M = (agents / ranks + 1) * beams: the agents' streams plus the reference
-policy's).
+policy's), and of C4's lookahead-tree segments (--configs c4).
 
     python tools/tune_gemm_dispatch.py [--out gpurun_out/gemm_dispatch.json] [--install]
 """
@@ -27,7 +27,19 @@ R = importlib.import_module(PKG + ".runtime")
 ops = importlib.import_module(PKG + ".ops")
 model = importlib.import_module(PKG + ".model")
 
-CONFIGS = {"c1": ("llama-3.2-1b", 4, 4), "c3": ("gemma-2-9b", 16, 16), "c5": ("llama-3.3-70b", 64, 8)}
+CONFIGS = {"c1": ("llama-3.2-1b", 4, 4), "c3": ("gemma-2-9b", 16, 16), "c5": ("llama-3.3-70b", 64, 8),
+           "c4": ("llama-3.1-8b", 32, 0)}
+# C4's lookahead tree (branching 4, depth 4): the forward segments of tree levels 1-3 under
+# every prompt (the agents' plus the reference policy's: (a + 1) x 4^d rows) and the last
+# level's segment with the committed token (a x 65 rows), a = agents on the rank
+C4_LEVELS = (4, 16, 64)
+
+
+def rows_of(cname: str, A: int, B: int, w: int):
+    a = A // w + (1 if A % w else 0)
+    if cname == "c4":
+        return [(a + 1) * n for n in C4_LEVELS] + [a * 65]
+    return [(a + 1) * B]
 
 
 def shapes_of(preset: str):
@@ -66,7 +78,12 @@ def main() -> int:
     ap.add_argument("--configs", default="c1,c3,c5")
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--install", action="store_true")
+    ap.add_argument("--merge", type=int, default=1,
+                    help="1: keep the installed table's entries for shapes this run does not measure")
     ap.add_argument("--variants", default="2,3,4")
+    ap.add_argument("--sk", type=int, default=0,
+                    help="1: also time the stream-K form (splits = -1, cs_gemm_bf16_streamk; "
+                         "slower than the split-K form on every C5 shape in r04d)")
     args = ap.parse_args()
     print("tuning:", R.use_gemm_tuning(), file=sys.stderr)
     dev = torch.device("cuda:0")
@@ -75,7 +92,7 @@ def main() -> int:
     calls = 20
     for cname in args.configs.split(","):
         preset, A, B = CONFIGS[cname]
-        Ms = sorted({(A // w + (1 if A % w else 0) + 1) * B for w in map(int, args.worlds.split(","))})
+        Ms = sorted({m for w in map(int, args.worlds.split(",")) for m in rows_of(cname, A, B, w)})
         for name, N, K, gated, act in shapes_of(preset):
             nw = max(2, min(20, (700 << 20) // (N * K * 2) + 1))
             ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05 for _ in range(nw)]
@@ -96,8 +113,10 @@ def main() -> int:
                 best = ("torch", 0, 0, t_torch)
                 cands = []
                 for var in map(int, args.variants.split(",")):
-                    for sp in ((1,) if gated else (1, 2, 4, 8, 16)):
-                        if K % (64 * sp) or K // (64 * sp) < 2 or (var in (2, 4) and N % 256):
+                    for sp in ((1,) if gated else (1, 2, 4, 8, 16)) + ((-1,) if args.sk else ()):
+                        if var in (2, 4) and N % 256:
+                            continue
+                        if sp > 0 and (K % (64 * sp) or K // (64 * sp) < 2):
                             continue
                         t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), act=act,
                                                     splits=sp, variant=var)
@@ -115,6 +134,16 @@ def main() -> int:
                                                      "us": round(best[3], 2),
                                                      "torch_us": round(t_torch, 2)}
             del ws
+    if args.merge:
+        # keep the installed table's choices for the shapes not measured in this run
+        inst = os.path.join(REPO, PKG, "tuned", "gemm_dispatch_mi355x.json")
+        if os.path.exists(inst):
+            with open(inst) as f:
+                old = json.load(f)
+            seen = {f"{r['M']},{r['N']},{r['K']},{r['gated']}" for r in record}
+            table = {**{k: v for k, v in old.get("table", {}).items() if k not in seen}, **table}
+            record = [r for r in old.get("measured", [])
+                      if f"{r['M']},{r['N']},{r['K']},{r['gated']}" not in seen] + record
     out = {"device": torch.cuda.get_device_name(0), "torch": torch.__version__,
            "hip": torch.version.hip, "library": ops._lib.version(),
            "note": "shapes absent here run on hipBLASLt (torch)", "table": table,
