@@ -38,6 +38,8 @@ SHAPES = {
     "r8c3_qkv": (48, 8192, 3584, 0), "r8c3_gu_gated": (48, 28672, 3584, 1),
     "r8c3_down": (48, 3584, 14336, 0), "r8c5_qkv": (72, 10240, 8192, 0),
     "r8c5_gu_gated": (72, 57344, 8192, 1), "r8c5_down": (72, 8192, 28672, 0),
+    "r8c3_o": (48, 3584, 4096, 0), "r8c5_o": (72, 8192, 8192, 0),
+    "r8c3_lmhead": (48, 256000, 3584, 0), "r8c5_lmhead": (72, 128256, 8192, 0),
 }
 
 
@@ -70,6 +72,9 @@ def main():
     ap.add_argument("--msweep", default="", help="torch only: comma list of M for the C3 shapes")
     ap.add_argument("--lib", default="", help="time this build of the library (read before import)")
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--warm", action="store_true",
+                    help="one weight matrix for every call (L2 / Infinity-Cache resident when it "
+                         "fits): the rate the kernel reaches when HBM is not what bounds it")
     args = ap.parse_args()
     print("tuning:", R.use_gemm_tuning(), file=sys.stderr)
     dev = torch.device("cuda:0")
@@ -91,7 +96,7 @@ def main():
             continue
         torch.manual_seed(0)
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-        nw = max(2, min(20, (700 << 20) // (N * K * 2) + 1))
+        nw = 1 if args.warm else max(2, min(20, (700 << 20) // (N * K * 2) + 1))
         ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05 for _ in range(nw)]
         calls = 20
         # correctness on ws[0]
@@ -115,7 +120,7 @@ def main():
                    int(ops._lib.load().cs_gemm_splits(M, N, K, gated, var)) if sp == 0 else sp)
             yb = y.contiguous().view(torch.int16).to(torch.int64)
             ysig = int(((yb * torch.arange(1, yb.numel() + 1, device=dev).view_as(yb)) % 1000003).sum().item())
-            rec = {"lib": os.path.basename(args.lib) or "tree", "ysig": ysig,
+            rec = {"lib": os.path.basename(args.lib) or "tree", "ysig": ysig, "warm": args.warm,
                    "shape": name, "M": M, "N": N, "K": K, "impl": f"cs_gemm_v{var}", "splits": eff,
                    "us": round(t, 2), "weight_GBps": round(N * K * 2 / t / 1e3, 1),
                    "TFLOPs": round(2 * M * N * K / t / 1e6, 1), "max_err": err, "ref_max": scale}
@@ -135,8 +140,8 @@ def main():
                 for i in range(calls):
                     x @ ws[i % nw].t()
         t = timed(tfn) / calls * 1e3
-        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "impl": "torch", "us": round(t, 2),
-                          "weight_GBps": round(N * K * 2 / t / 1e3, 1),
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "impl": "torch", "warm": args.warm,
+                          "us": round(t, 2), "weight_GBps": round(N * K * 2 / t / 1e3, 1),
                           "TFLOPs": round(2 * M * N * K / t / 1e6, 1)}), flush=True)
         del ws
 
