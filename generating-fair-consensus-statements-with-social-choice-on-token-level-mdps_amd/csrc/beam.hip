@@ -1091,6 +1091,10 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   const int64_t rows = static_cast<int64_t>(A) * B;
   d.plan = plan_split(rows, vocab, dtype);
   d.block = d.plan.nsplit > 1 ? 256 : 1024;
+  if (const char* e = getenv("CS_DECODE_BLOCK")) {   // A/B: 256 or 1024 whatever the split
+    const int v = atoi(e);
+    if (v == 256 || v == 1024) d.block = v;
+  }
   d.kp = decode_kp(B, vocab, d.block, K, dtype);
   const int64_t ch = static_cast<int64_t>(d.kp) * d.block;
   d.nchunk_p = static_cast<int32_t>((vocab + ch - 1) / ch);

@@ -723,6 +723,162 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<gu16x8*>(Y + m * ldy + n) = o;
 }
 
+// thin_gemm_kernel<MT, FT, GATED, WAVES, RING>: the per-rank step shapes (M <= 80 rows: C1
+// 20, C3 48 at 8 ranks, C5 72), where the weight stream is latency-bound -- the split-K
+// kernels above reach 2-5 TB/s there and ~25 % more when the weights sit in the Infinity
+// Cache (profiles/r04f_gemm_r8_*.jsonl).  No barrier and no LDS in the main loop: a
+// workgroup owns 16 * FT output features (GATED: 16 gate features and their 16 up
+// features), its WAVES waves split the K steps (64 deep) evenly, and each wave streams its
+// slice of W and of X (L2-resident) straight into MFMA fragments through a RING-deep
+// register ring (plain loads; the compiler's counted vmcnt keeps the later slots in flight).
+// A lane reads 32 contiguous bytes of its W row per step (4 lanes = one 128-B line) and the
+// same k range of its X row; the two 16-B halves feed the step's two 32-deep MFMAs, so k is
+// permuted identically in both operands.  At the end the waves' fp32 accumulators meet in
+// LDS and are folded in wave order (deterministic), then rounded to bf16 (GATED: act(gate)
+// * up with cs_gated_act's roundings).  K % 64 == 0, M <= 16 * MT.
+template <int MT, int FT, int GATED, int WAVES, int RING>
+__global__ __launch_bounds__(64 * WAVES, 1) void thin_gemm_kernel(
+    const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
+    uint16_t* __restrict__ Y, int64_t ldy, int64_t M, int64_t gate_off, int nsteps, int act) {
+  static_assert(!GATED || FT == 2, "the gated form pairs one gate tile with one up tile");
+  __shared__ gf32x4 red[WAVES][FT * MT][64];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t f0 = static_cast<int64_t>(blockIdx.x) * (GATED ? 16 : 16 * FT);
+  const int s0 = wv * nsteps / WAVES;
+  const int s1 = (wv + 1) * nsteps / WAVES;
+  const int koff = 16 * (lane >> 4);
+  const uint16_t* wp[FT];
+#pragma unroll
+  for (int j = 0; j < FT; ++j) {
+    const int64_t row = GATED ? (j ? gate_off : 0) + f0 + (lane & 15) : f0 + 16 * j + (lane & 15);
+    wp[j] = W + row * ldw + koff;
+  }
+  const uint16_t* xp[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    int64_t row = 16 * i + (lane & 15);
+    if (row > M - 1) row = M - 1;     // padded rows read a real row; their results are dropped
+    xp[i] = X + row * ldx + koff;
+  }
+  gf32x4 acc[FT][MT];
+#pragma unroll
+  for (int j = 0; j < FT; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[j][i] = gf32x4{0.f, 0.f, 0.f, 0.f};
+
+  gbf16x8 wr[RING][FT][2];
+  gbf16x8 xr[RING][MT][2];
+  const int last = s1 > s0 ? s1 - 1 : s0;
+  auto load = [&](int r, int s) {
+    s = s < last ? s : last;           // past the slice: re-read its last step (a cache hit)
+    const int64_t o = static_cast<int64_t>(s) * 64;
+#pragma unroll
+    for (int j = 0; j < FT; ++j) {
+      wr[r][j][0] = *reinterpret_cast<const gbf16x8*>(wp[j] + o);
+      wr[r][j][1] = *reinterpret_cast<const gbf16x8*>(wp[j] + o + 8);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      xr[r][i][0] = *reinterpret_cast<const gbf16x8*>(xp[i] + o);
+      xr[r][i][1] = *reinterpret_cast<const gbf16x8*>(xp[i] + o + 8);
+    }
+  };
+  auto compute = [&](int r) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < FT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[r][j][q], xr[r][i][q], acc[j][i], 0, 0, 0);
+  };
+  cs_static_for<RING>([&](auto r) { load(r, s0 + r); });
+  int s = s0;
+  for (; s + RING <= s1; s += RING) {
+    cs_static_for<RING>([&](auto r) {
+      compute(r);
+      load(r, s + RING + r);
+    });
+  }
+  cs_static_for<RING>([&](auto r) {
+    if (s + r < s1) compute(r);
+  });
+
+  // fold the waves' partial sums in wave order; fold unit u (a row tile i and, unless
+  // gated, a feature tile j) is finished by wave u % WAVES
+#pragma unroll
+  for (int j = 0; j < FT; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) red[wv][j * MT + i][lane] = acc[j][i];
+  __syncthreads();
+  constexpr int kUnits = GATED ? MT : FT * MT;
+  for (int u = wv; u < kUnits; u += WAVES) {
+    if (GATED) {
+      const int i = u;
+      const int64_t m = 16 * i + (lane & 15);
+      gf32x4 g = red[0][i][lane], up = red[0][MT + i][lane];
+      for (int w = 1; w < WAVES; ++w) {
+        g += red[w][i][lane];
+        up += red[w][MT + i][lane];
+      }
+      if (m < M) {
+        gu16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = gbf(gto_bf(g[e]));
+          const float uv = gbf(gto_bf(up[e]));
+          const uint16_t a = gto_bf(act ? g_gelu_tanh(gv) : g_silu(gv));
+          o[e] = gto_bf(gbf(a) * uv);
+        }
+        *reinterpret_cast<gu16x4*>(Y + m * ldy + f0 + 4 * (lane >> 4)) = o;
+      }
+    } else {
+      const int j = u / MT, i = u - j * MT;
+      const int64_t m = 16 * i + (lane & 15);
+      gf32x4 a = red[0][u][lane];
+      for (int w = 1; w < WAVES; ++w) a += red[w][u][lane];
+      if (m < M) {
+        gu16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = gto_bf(a[e]);
+        *reinterpret_cast<gu16x4*>(Y + m * ldy + f0 + 16 * j + 4 * (lane >> 4)) = o;
+      }
+    }
+  }
+}
+
+// thin variants: 5 = 16 features x 8 waves, 6 = 32 features x 8 waves, 7 = 16 features x
+// 16 waves (gated: one gate + one up tile, 8 / 8 / 16 waves)
+constexpr int kThinMaxRows = 80;
+bool thin_variant(int variant) { return variant >= 5 && variant <= 7; }
+int thin_ft(int variant, int gated) { return gated || variant == 6 ? 2 : 1; }
+int thin_waves(int variant) { return variant == 7 ? 16 : 8; }
+
+template <int MT, int FT, int GATED, int WAVES, int RING>
+void launch_thin(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
+                 int64_t ldw, uint16_t* Y, int64_t ldy, int64_t M, int64_t gate_off, int nsteps,
+                 int act) {
+  hipLaunchKernelGGL((thin_gemm_kernel<MT, FT, GATED, WAVES, RING>), dim3(blocks), dim3(64 * WAVES),
+                     0, st, X, ldx, W, ldw, Y, ldy, M, gate_off, nsteps, act);
+}
+
+// row tiles 1..MAXMT (the caller keeps mt <= MAXMT)
+template <int FT, int GATED, int WAVES, int RING, int MAXMT>
+void dispatch_thin(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
+                   const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, int64_t M,
+                   int64_t gate_off, int nsteps, int act) {
+  if constexpr (MAXMT > 1) {
+    if (mt < MAXMT) {
+      dispatch_thin<FT, GATED, WAVES, RING, MAXMT - 1>(mt, blocks, st, X, ldx, W, ldw, Y, ldy, M,
+                                                       gate_off, nsteps, act);
+      return;
+    }
+  }
+  launch_thin<MAXMT, FT, GATED, WAVES, RING>(blocks, st, X, ldx, W, ldw, Y, ldy, M, gate_off,
+                                             nsteps, act);
+}
+
 template <int MW, int GATED>
 void launch_ws(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
                int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
@@ -847,6 +1003,7 @@ int64_t ws2_grid(int64_t cells, int64_t mblocks) {
 
 int resolve_variant(int variant, int64_t N, int gated) {
   if (variant == 0) variant = 2;
+  if (thin_variant(variant)) return variant;
   if ((variant == 2 || variant == 4) && N % 256) variant = gated ? 1 : 3;
   if (variant == 3 && gated) variant = 2;
   return variant;
@@ -858,7 +1015,7 @@ extern "C" {
 
 int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant) {
   if (M <= 0 || N <= 0 || K <= 0 || N % 128) return 0;
-  if (gated) return 1;
+  if (gated || thin_variant(variant)) return 1;
   variant = resolve_variant(variant, N, gated);
   const int64_t tiles = gemm_tiles(variant, M, N, gated);
   // fill the 256 CUs (one 512-thread workgroup each) while keeping >= 8 K steps per split
@@ -873,7 +1030,7 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
   if (M == 0) return CS_OK;
   if (!x || !w) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
-  if (variant < 0 || variant > 4) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..4");
+  if (variant < 0 || variant > 7) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..7");
   if (N % 128) return fail(CS_ERR_INVALID, "cs_gemm_bf16: N must be a multiple of 128");
   if (gated && splits > 1)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
@@ -893,6 +1050,33 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   // the split-K fold writes 16-byte vectors of 8 features at y + m * ldy + n
   if (splits > 1 && y && (ldy % 8 || reinterpret_cast<uintptr_t>(y) & 15))
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: a K split needs y 16-byte aligned and ldy % 8 == 0");
+  if (thin_variant(variant)) {
+    if (M > kThinMaxRows || K % kGemmBK || splits > 1 || !y)
+      return fail(CS_ERR_INVALID, "cs_gemm_bf16: variants 5-7 take M <= 80, K % 64 == 0, no K split");
+    const int ft = thin_ft(variant, gated);
+    const int64_t n_out = gated ? N / 2 : N;
+    const int64_t blocks = gated ? n_out / 16 : n_out / (16 * ft);
+    const int mt = static_cast<int>((M + 15) / 16);
+    const int nsteps = static_cast<int>(K / kGemmBK);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint16_t* X = static_cast<const uint16_t*>(x);
+    const uint16_t* Wp = static_cast<const uint16_t*>(w);
+    uint16_t* Y = static_cast<uint16_t*>(y);
+    const int b = static_cast<int>(blocks);
+    if (gated) {
+      if (variant == 7 && mt <= 3)    // (16 gated waves spill at 4-5 row tiles: 8 waves there)
+        dispatch_thin<2, 1, 16, 2, 3>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, M, n_out, nsteps, act);
+      else
+        dispatch_thin<2, 1, 8, 3, 5>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, M, n_out, nsteps, act);
+    } else if (variant == 5) {
+      dispatch_thin<1, 0, 8, 3, 5>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, M, 0, nsteps, 0);
+    } else if (variant == 6) {
+      dispatch_thin<2, 0, 8, 3, 5>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, M, 0, nsteps, 0);
+    } else {
+      dispatch_thin<1, 0, 16, 2, 5>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, M, 0, nsteps, 0);
+    }
+    return check_launch("cs_gemm_bf16");
+  }
   const int64_t tiles = gemm_tiles(variant, M, N, gated);
   const int64_t blocks = tiles * splits;
   if (blocks > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
@@ -977,7 +1161,7 @@ extern "C" {
 
 size_t cs_gemm_streamk_workspace_size(int64_t M, int64_t N, int64_t K, int gated, int variant,
                                       int32_t blocks) {
-  if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % kGemmBK) return 0;
+  if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % kGemmBK || variant < 0 || variant > 4) return 0;
   return sk_plan(M, N, K, gated, variant, blocks).total;
 }
 

@@ -93,6 +93,54 @@ def test_gated_gemm_equals_gemm_then_gated_act(ops, dev, act, M, F, K, variant):
     assert torch.equal(got, want)
 
 
+THIN_SHAPES = [
+    # M, N, K            what it covers
+    (1, 128, 64),        # one row, one K step: 7 of the 8 waves have no step
+    (5, 256, 640),       # 10 K steps over 8 / 16 waves (uneven slices)
+    (20, 3072, 2048),    # C1 q|k|v
+    (48, 3584, 4096),    # C3 output projection at 8 ranks
+    (72, 1024, 8192),    # C5's 8-rank row count, long K
+    (80, 384, 14336),    # the thin form's row limit, C3 down's K
+]
+
+
+@pytest.mark.parametrize("variant", [5, 6, 7])
+@pytest.mark.parametrize("M,N,K", THIN_SHAPES)
+def test_thin_gemm_matches_fp32_product(ops, dev, M, N, K, variant):
+    """Variants 5-7 (M <= 80: each wave streams its own K slice, waves folded in order)."""
+    g = torch.Generator(device="cpu").manual_seed(M * 11 + N + K)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = ops.gemm(x, w, variant=variant)
+    assert y.shape == (M, N)
+    assert torch.all((y.float() - ref).abs() <= _tol(ref)), (y.float() - ref).abs().max().item()
+    assert torch.equal(y, ops.gemm(x, w, variant=variant)), "not bitwise reproducible"
+
+
+@pytest.mark.parametrize("variant", [5, 7])
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+@pytest.mark.parametrize("M,F,K", [(20, 512, 256), (48, 1024, 448), (72, 256, 1024)])
+def test_thin_gated_gemm_equals_thin_gemm_then_gated_act(ops, dev, act, M, F, K, variant):
+    """The thin gated form rounds the same fp32 sums as the thin plain form with the same
+    wave count (16 waves only up to 3 row tiles, else 8), then applies cs_gated_act."""
+    g = torch.Generator(device="cpu").manual_seed(F + K + M)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(2 * F, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    plain = variant if (variant != 7 or M <= 48) else 5
+    gu = ops.gemm(x, w, variant=plain)
+    want = ops.gated_act(gu[:, :F], gu[:, F:], act)
+    got = ops.gemm(x, w, gated=True, act=act, variant=variant)
+    assert torch.equal(got, want)
+
+
+def test_thin_gemm_rejects_more_than_80_rows(ops, dev):
+    x = torch.zeros(81, 128, device=dev, dtype=torch.bfloat16)
+    w = torch.zeros(128, 128, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(ops.CSError):
+        ops.gemm(x, w, variant=5)
+
+
 def test_gemm_rejects_unsupported_shapes(ops, dev):
     x = torch.zeros(4, 100, device=dev, dtype=torch.bfloat16)
     w = torch.zeros(128, 100, device=dev, dtype=torch.bfloat16)

@@ -41,7 +41,10 @@ def main():
     for name, (A, B, K, V, cap, dt) in {"c1": (4, 4, 10, 128256, 0.0, torch.float32),
                                          "c3": (16, 16, 50, 256000, 30.0, torch.bfloat16),
                                          "c3nocap": (16, 16, 50, 256000, 0.0, torch.bfloat16),
-                                         "c5": (64, 8, 32, 128256, 0.0, torch.bfloat16)}.items():
+                                         "c5": (64, 8, 32, 128256, 0.0, torch.bfloat16),
+                                         # per-rank shapes at 8 ranks (agents sharded)
+                                         "r8c3": (2, 16, 50, 256000, 30.0, torch.bfloat16),
+                                         "r8c5": (8, 8, 32, 128256, 0.0, torch.bfloat16)}.items():
         g = torch.Generator(device=dev).manual_seed(1)
         x = (torch.randn(A * B, V, generator=g, device=dev) * 3).to(dt)
         ref = (torch.randn(B, V, generator=g, device=dev) * 3).to(dt)
@@ -67,6 +70,18 @@ def main():
         wd = ops.Workspace(zeroed=True)
         r["decode_us"] = timed(lambda: ops.beam_decode_step(ref, x, R, K, "min", n_order=B,
                                                             softcap=cap, workspace=wd))
+        if "--blocks" in sys.argv:
+            for blk in (256, 1024):
+                for kp in ("", "4"):
+                    os.environ["CS_DECODE_BLOCK"] = str(blk)
+                    if kp:
+                        os.environ["CS_DECODE_KP"] = kp
+                    wd2 = ops.Workspace(zeroed=True)
+                    r[f"decode_block{blk}{'_kp' + kp if kp else ''}_us"] = timed(
+                        lambda: ops.beam_decode_step(ref, x, R, K, "min", n_order=B, softcap=cap,
+                                                     workspace=wd2))
+                    os.environ.pop("CS_DECODE_KP", None)
+            os.environ.pop("CS_DECODE_BLOCK")
         if "--sweep" in sys.argv:
             for kp in (4, 8, 16):
                 for rf in (0, 1):

@@ -80,7 +80,7 @@ def main() -> int:
     ap.add_argument("--install", action="store_true")
     ap.add_argument("--merge", type=int, default=1,
                     help="1: keep the installed table's entries for shapes this run does not measure")
-    ap.add_argument("--variants", default="2,3,4")
+    ap.add_argument("--variants", default="2,3,4,5,6,7")
     ap.add_argument("--sk", type=int, default=0,
                     help="1: also time the stream-K form (splits = -1, cs_gemm_bf16_streamk; "
                          "slower than the split-K form on every C5 shape in r04d)")
@@ -113,7 +113,10 @@ def main() -> int:
                 best = ("torch", 0, 0, t_torch)
                 cands = []
                 for var in map(int, args.variants.split(",")):
-                    for sp in ((1,) if gated else (1, 2, 4, 8, 16)) + ((-1,) if args.sk else ()):
+                    if var >= 5 and M > 80:
+                        continue                 # the thin form takes at most 80 rows
+                    for sp in ((1,) if gated or var >= 5 else (1, 2, 4, 8, 16)) + \
+                            ((-1,) if args.sk and var < 5 else ()):
                         if var in (2, 4) and N % 256:
                             continue
                         if sp > 0 and (K % (64 * sp) or K // (64 * sp) < 2):
