@@ -28,6 +28,7 @@ EXPORTED = (
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
     "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits", "cs_gemm_bf16_streamk",
+    "cs_gemm_bf16_packed", "cs_gemm_pack",
     "cs_gemm_streamk_workspace_size", "cs_add_rms_norm_splitk",
 )
 
@@ -130,6 +131,11 @@ def load():
     L.cs_gemm_bf16.restype = ctypes.c_int
     L.cs_gemm_splits.argtypes = [i64, i64, i64, ctypes.c_int, ctypes.c_int]
     L.cs_gemm_splits.restype = i64
+    L.cs_gemm_bf16_packed.argtypes = [vp, i64, vp, vp, i64, i64, i64, i64, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.cs_gemm_bf16_packed.restype = ctypes.c_int
+    L.cs_gemm_pack.argtypes = [vp, i64, i64, i64, vp, vp]
+    L.cs_gemm_pack.restype = ctypes.c_int
     L.cs_gemm_bf16_streamk.argtypes = [vp, i64, vp, i64, vp, i64, i64, i64, i64, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int32, vp,
                                        ctypes.c_size_t, vp]

@@ -280,7 +280,11 @@ struct Ws2Shape {
 
 // the tile (column tile nt, rows m0 ..) accumulated over nk K steps from kbase into acc:
 // the whole software pipeline of a ws2 workgroup (every wave calls it; LDS free on entry)
-template <int MT, int NT, int GATED, int WAVES>
+// PACKED: W in the fragment-major layout of cs_gemm_pack (ldw = K): the 16-row tile T's
+// 64-deep K step s is 2 KB at ((T * K / 64 + s) * 2 + sub) * 512 elements, lane-linear (lane
+// l's 16 B = row l % 16, k 8 * (l / 16) of half `sub`), so each fragment load is ONE
+// contiguous 1 KB and a wave's whole W stream for a tile is one sequential run.
+template <int MT, int NT, int GATED, int WAVES, bool PACKED = false>
 __device__ __forceinline__ void ws2_accumulate(
     unsigned char* lds, const uint16_t* __restrict__ X, int64_t ldx,
     const uint16_t* __restrict__ W, int64_t ldw, int64_t M, int64_t gate_off, int64_t nt,
@@ -309,7 +313,12 @@ __device__ __forceinline__ void ws2_accumulate(
     } else {
       row = nt * kBN + wv * 16 * NT + 16 * j + (lane & 15);
     }
-    wp[j] = W + row * ldw + kbase + 8 * (lane >> 4);
+    if constexpr (PACKED) {
+      const int64_t tile = (row - (lane & 15)) >> 4;
+      wp[j] = W + ((tile * (ldw / kGemmBK) + kbase / kGemmBK) * 2) * 512 + 8 * lane;
+    } else {
+      wp[j] = W + row * ldw + kbase + 8 * (lane >> 4);
+    }
   }
   const uint16_t* xsrc[kG];
   int xdst[kG];
@@ -338,11 +347,11 @@ __device__ __forceinline__ void ws2_accumulate(
   };
   auto load_w = [&](gbf16x8 (&w)[NT][2], int kt) {
     kt = kt < nk ? kt : nk - 1;
-    const int64_t o = static_cast<int64_t>(kt) * kGemmBK;
+    const int64_t o = static_cast<int64_t>(kt) * (PACKED ? 1024 : kGemmBK);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       w[j][0] = asm_load16(wp[j] + o);
-      w[j][1] = asm_load16(wp[j] + o + 32);
+      w[j][1] = asm_load16(wp[j] + o + (PACKED ? 512 : 32));
     }
   };
   const int xr = lane & 15;
@@ -535,7 +544,7 @@ __device__ __forceinline__ void ws2_store(const gf32x4 (&acc)[MT][NT], uint16_t*
 // W goes to registers through inline-asm loads, so the compiler's waits never drain the
 // DMA queue: one counted s_waitcnt vmcnt per step (this step's X and W landed, the next
 // two steps' loads still in flight) + a raw s_barrier.
-template <int MT, int NT, int GATED, int WAVES>
+template <int MT, int NT, int GATED, int WAVES, bool PACKED = false>
 __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
     const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
     uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
@@ -558,7 +567,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
   const int64_t m0 = static_cast<int64_t>(mb) * S::kRows;
   const int64_t kbase = static_cast<int64_t>(sp) * nk * kGemmBK;
   gf32x4 acc[MT][NT];
-  ws2_accumulate<MT, NT, GATED, WAVES>(lds, X, ldx, W, ldw, M, gate_off, nt, m0, kbase, nk, acc);
+  ws2_accumulate<MT, NT, GATED, WAVES, PACKED>(lds, X, ldx, W, ldw, M, gate_off, nt, m0, kbase, nk,
+                                               acc);
   ws2_store<MT, NT, GATED, WAVES>(acc, Y, ldy, P, M, n_out, nt, m0, sp, act);
 }
 
@@ -922,24 +932,24 @@ void ws2_rows(int64_t M, int* mt, int64_t* mblocks, int max_tiles = 18) {
   *mblocks = (tiles + v - 1) / v;
 }
 
-template <int MT, int NT, int GATED, int WAVES>
+template <int MT, int NT, int GATED, int WAVES, bool PACKED>
 void launch_ws2(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
                 int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M, int64_t n_out,
                 int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
-  hipLaunchKernelGGL((ws2_gemm_kernel<MT, NT, GATED, WAVES>), dim3(blocks), dim3(64 * WAVES), 0, st,
-                     X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act,
+  hipLaunchKernelGGL((ws2_gemm_kernel<MT, NT, GATED, WAVES, PACKED>), dim3(blocks), dim3(64 * WAVES),
+                     0, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, n_tiles, splits, act,
                      m_blocks);
 }
 
-template <int NT, int GATED, int WAVES>
+template <int NT, int GATED, int WAVES, bool PACKED>
 void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
                   const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, float* P, int64_t M,
                   int64_t n_out, int64_t gate_off, int nk, int n_tiles, int splits, int act,
                   int m_blocks) {
 #define CS_WS2_CASE(V)                                                                          \
   case V:                                                                                       \
-    launch_ws2<V, NT, GATED, WAVES>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out, gate_off, nk, \
-                                    n_tiles, splits, act, m_blocks);                            \
+    launch_ws2<V, NT, GATED, WAVES, PACKED>(blocks, st, X, ldx, W, ldw, Y, ldy, P, M, n_out,    \
+                                            gate_off, nk, n_tiles, splits, act, m_blocks);      \
     break;
   switch (mt) {
     CS_WS2_CASE(2) CS_WS2_CASE(4) CS_WS2_CASE(8) CS_WS2_CASE(9) CS_WS2_CASE(12) CS_WS2_CASE(17)
@@ -1024,10 +1034,22 @@ int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant) 
   return s;
 }
 
-int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy,
-                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act, int variant,
-                 float* workspace, cs_stream_t stream) {
+}  // extern "C"
+
+namespace {
+// cs_gemm_bf16 (packed = false) and cs_gemm_bf16_packed (W in cs_gemm_pack's layout: the ws2
+// variants 2-4 only, ldw = K)
+int gemm_impl(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy,
+              int64_t M, int64_t N, int64_t K, int splits, int gated, int act, int variant,
+              float* workspace, cs_stream_t stream, bool packed) {
   if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, "cs_gemm_bf16: bad shape");
+  if (packed) {
+    if (variant == 0) variant = 2;
+    if (variant < 2 || variant > 4)
+      return fail(CS_ERR_INVALID, "cs_gemm_bf16_packed: variants 2-4 (the ws2 kernels) only");
+    if (K % kGemmBK) return fail(CS_ERR_INVALID, "cs_gemm_bf16_packed: K must be a multiple of 64");
+    ldw = K;
+  }
   if (M == 0) return CS_OK;
   if (!x || !w) return fail(CS_ERR_INVALID, "cs_gemm_bf16: NULL pointer");
   if (variant < 0 || variant > 7) return fail(CS_ERR_INVALID, "cs_gemm_bf16: variant must be 0..7");
@@ -1035,6 +1057,8 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   if (gated && splits > 1)
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: the gated form takes no K split");
   variant = resolve_variant(variant, N, gated);
+  if (packed && variant != 2 && variant != 3 && variant != 4)
+    return fail(CS_ERR_INVALID, "cs_gemm_bf16_packed: N must be a multiple of 256 for this variant");
   if (splits <= 0) splits = static_cast<int>(cs_gemm_splits(M, N, K, gated, variant));
   if (!y && (splits <= 1 || gated))
     return fail(CS_ERR_INVALID, "cs_gemm_bf16: y may be NULL only with a K split (partials kept)");
@@ -1105,12 +1129,26 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     const int b = static_cast<int>(grid);
     const int mbi = static_cast<int>(mb);
     if (gated) {
-      dispatch_ws2<2, 1, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk, n_tiles, 1,
-                            act, mbi);
+      if (packed)
+        dispatch_ws2<2, 1, 8, true>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                    n_tiles, 1, act, mbi);
+      else
+        dispatch_ws2<2, 1, 8, false>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                     n_tiles, 1, act, mbi);
     } else if (variant == 3) {
-      dispatch_ws2<1, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
+      if (packed)
+        dispatch_ws2<1, 0, 8, true>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits,
+                                    0, mbi);
+      else
+        dispatch_ws2<1, 0, 8, false>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles,
+                                     splits, 0, mbi);
     } else {
-      dispatch_ws2<2, 0, 8>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits, 0, mbi);
+      if (packed)
+        dispatch_ws2<2, 0, 8, true>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles, splits,
+                                    0, mbi);
+      else
+        dispatch_ws2<2, 0, 8, false>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, Pp, M, N, 0, nk, n_tiles,
+                                     splits, 0, mbi);
     }
   }
   if (splits > 1 && !gated && Y) {     // y == NULL: the caller folds the partials itself
@@ -1119,6 +1157,53 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
                        0, st, workspace, splits, M, N, Y, ldy);
   }
   return check_launch("cs_gemm_bf16");
+}
+
+// Wp[((T * ns + s) * 2 + h) * 512 + 8 l + e] = W[16 T + l % 16][64 s + 32 h + 8 (l / 16) + e]
+__global__ __launch_bounds__(256) void gemm_pack_kernel(const uint16_t* __restrict__ W, int64_t ldw,
+                                                        int64_t n_vec, int64_t ns,
+                                                        uint16_t* __restrict__ Wp) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;   // one 16-B vector
+  if (v >= n_vec) return;
+  const int l = static_cast<int>(v & 63);
+  const int64_t blk = v >> 6;                    // (T * ns + s) * 2 + h
+  const int h = static_cast<int>(blk & 1);
+  const int64_t ts = blk >> 1;
+  const int64_t T = ts / ns, st = ts - T * ns;
+  const int64_t row = 16 * T + (l & 15);
+  const int64_t col = 64 * st + 32 * h + 8 * (l >> 4);
+  *reinterpret_cast<gu32x4*>(Wp + 8 * v) = *reinterpret_cast<const gu32x4*>(W + row * ldw + col);
+}
+}  // namespace
+
+extern "C" {
+
+int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy,
+                 int64_t M, int64_t N, int64_t K, int splits, int gated, int act, int variant,
+                 float* workspace, cs_stream_t stream) {
+  return gemm_impl(x, ldx, w, ldw, y, ldy, M, N, K, splits, gated, act, variant, workspace, stream,
+                   false);
+}
+
+int cs_gemm_bf16_packed(const void* x, int64_t ldx, const void* w_packed, void* y, int64_t ldy,
+                        int64_t M, int64_t N, int64_t K, int splits, int gated, int act,
+                        int variant, float* workspace, cs_stream_t stream) {
+  return gemm_impl(x, ldx, w_packed, K, y, ldy, M, N, K, splits, gated, act, variant, workspace,
+                   stream, true);
+}
+
+int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packed,
+                 cs_stream_t stream) {
+  if (!w || !w_packed) return fail(CS_ERR_INVALID, "cs_gemm_pack: NULL pointer");
+  if (N <= 0 || K <= 0 || N % 16 || K % kGemmBK || ldw < K || ldw % 8)
+    return fail(CS_ERR_INVALID, "cs_gemm_pack: need N % 16 == 0, K % 64 == 0, ldw >= K, ldw % 8 == 0");
+  if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(w_packed)) & 15)
+    return fail(CS_ERR_INVALID, "cs_gemm_pack: operands must be 16-byte aligned");
+  const int64_t n_vec = N * K / 8;
+  hipLaunchKernelGGL(gemm_pack_kernel, dim3(static_cast<uint32_t>((n_vec + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(w), ldw, n_vec,
+                     K / kGemmBK, static_cast<uint16_t*>(w_packed));
+  return check_launch("cs_gemm_pack");
 }
 
 }  // extern "C"

@@ -23,6 +23,7 @@ available offline and throughput is independent of weight values.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field, replace
 from typing import Dict, List, Optional, Sequence
 
@@ -110,6 +111,9 @@ class Model:
         self.w = weights if weights is not None else self._init(seed)
         self.inv_freq = rope_inv_freq(cfg, self.device)
         self._fuse()
+        # cs_gemm_pack'ed copies of the decode-step weights the dispatch table runs packed
+        # (pack_decode_weights; None until the first stream forward)
+        self.wp: Optional[Dict[str, object]] = None
 
     def _fuse(self) -> None:
         """Per layer one [q; k; v] and one [gate; up] weight, so each is ONE GEMM; the
@@ -359,11 +363,60 @@ class Model:
         W = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
         if h.is_cuda and h.dim() == 2 and h.dtype == W.dtype == torch.bfloat16:
             from . import ops   # local: model.py stays importable without the library
-            if ops.gemm_choice(h.shape[0], W.shape[0], W.shape[1]) is not None:
-                return ops.linear(h, W, out=out)
+            pw = (self.wp or {}).get("lm_head")
+            if ops.gemm_choice(h.shape[0], W.shape[0], W.shape[1], packed=pw is not None) is not None:
+                return ops.linear(h, W, out=out, packed=pw)
         if out is not None:
             return torch.matmul(h.to(W.dtype), W.t(), out=out)
         return h.to(W.dtype) @ W.t()
+
+    # --- packed decode weights ----------------------------------------------------
+    def decode_weights(self) -> Dict[str, tuple]:
+        """name -> (weight, gated) of every GEMM weight a stream forward runs."""
+        out = {"lm_head": (self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"], False)}
+        for i in range(self.cfg.n_layers):
+            p = f"l{i}."
+            out[p + "qkv"] = (self.wf[p + "qkv"], False)
+            out[p + "wo"] = (self.w[p + "wo"], False)
+            out[p + "gate_up"] = (self.wf[p + "gate_up"], True)
+            out[p + "w_down"] = (self.w[p + "w_down"], False)
+        return out
+
+    @torch.no_grad()
+    def pack_decode_weights(self, reserve_bytes: Optional[int] = None) -> int:
+        """Keep a cs_gemm_pack'ed copy (ops.gemm_pack: fragment-major, every weight load one
+        contiguous 1 KB) of each decode weight the dispatch table runs packed at some row
+        count, while the device keeps ``reserve_bytes`` free (default: 1/6 of the device, at
+        least 32 GB: the first stream forward runs after its prefix caches and K/V histories
+        exist, and the reserve leaves room for a second decode state of the same shape, e.g.
+        the re-tokenized text path's, plus activations, logits and graph pools).  The weights whose
+        packed form saves the most time per byte (ops.gemm_pack_gain) go first, so a partial
+        budget (a 70B replica) packs where it pays most.  CS_GEMM_PACK=0 turns packing off.
+        Returns the bytes packed."""
+        from . import ops
+        self.wp = {}
+        if (os.environ.get("CS_GEMM_PACK", "1") == "0" or self.device.type != "cuda"
+                or self.dtype != torch.bfloat16):
+            return 0
+        free, total = torch.cuda.mem_get_info(self.device)
+        if reserve_bytes is None:
+            reserve_bytes = max(32 << 30, total // 6)
+        budget = free - reserve_bytes
+        cands = []
+        for name, (w, gated) in self.decode_weights().items():
+            if w.shape[0] % 16 or w.shape[1] % 64:
+                continue
+            gain = ops.gemm_pack_gain(w.shape[0], w.shape[1], gated)
+            if gain > 0.0:
+                cands.append((gain / (w.numel() * w.element_size()), name, w))
+        cands.sort(key=lambda c: -c[0])
+        used = 0
+        for _, name, w in cands:
+            nbytes = w.numel() * w.element_size()
+            if nbytes <= budget - used:
+                self.wp[name] = ops.gemm_pack(w)
+                used += nbytes
+        return used
 
     # --- stream forward over shared prefixes (HIP attention) ----------------------
     def attn_scale(self) -> float:
@@ -403,12 +456,15 @@ class Model:
         g2 = c.family == "gemma2"
         act = "gelu_tanh" if g2 else "silu"
         eps = c.rms_eps
+        if self.wp is None and not torch.cuda.is_current_stream_capturing():
+            self.pack_decode_weights()
+        wp = self.wp or {}
         h = self._embed(tokens).contiguous()                 # the residual stream [n_tok, d]
         # every residual add + RMSNorm is one cs_add_rms_norm launch; h is updated in place
         x = ops.add_rms_norm(h, self.w["l0.attn_norm"], eps, plus_one=g2)
         for i in range(c.n_layers):
             p = f"l{i}."
-            qkv = ops.linear(x, self.wf[p + "qkv"])
+            qkv = ops.linear(x, self.wf[p + "qkv"], packed=wp.get(p + "qkv"))
             q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
             ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
                            hist_k[i], hist_vt[i], group_prefix=group_prefix)
@@ -419,14 +475,15 @@ class Model:
                                      group_prefix=group_prefix,
                                      prefix_len_host=getattr(pfx, "lens_host", None),
                                      group_prefix_host=group_prefix_host)
-            o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"])
+            o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"], packed=wp.get(p + "wo"))
             # Gemma-2's post-attention / post-MLP norms of the branch ride in the residual
             # add's launch (b_weight): one cs_add_rms_norm per residual add
             x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2,
                                  b_weight=self.w[p + "post_attn_norm"] if g2 else None)
             # a K-split down projection hands its partials to the residual add's launch
-            y = ops.linear(ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act),
-                           self.w[p + "w_down"], fold=False)
+            y = ops.linear(ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act,
+                                      packed=wp.get(p + "gate_up")),
+                           self.w[p + "w_down"], fold=False, packed=wp.get(p + "w_down"))
             nxt = self.w[f"l{i + 1}.attn_norm"] if i + 1 < c.n_layers else self.w["norm"]
             x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2,
                                  b_weight=self.w[p + "post_mlp_norm"] if g2 else None)

@@ -742,11 +742,14 @@ GEMM_DISPATCH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned"
 _gemm_table: Optional[dict] = None
 
 
-def gemm_choice(M: int, N: int, K: int, gated: bool = False) -> Optional[dict]:
+def gemm_choice(M: int, N: int, K: int, gated: bool = False,
+                packed: bool = False) -> Optional[dict]:
     """The cs_gemm_bf16 tile variant and K split measured faster than hipBLASLt for this
     exact shape on MI355X (tools/tune_gemm_dispatch.py -> tuned/gemm_dispatch_mi355x.json,
-    read only), or None: the shape stays on hipBLASLt.  CS_GEMM_DISPATCH=0 turns the table
-    off, CS_GEMM_DISPATCH=<file> reads another one."""
+    read only), or None: the shape stays on hipBLASLt.  packed: the caller holds the weight's
+    cs_gemm_pack'ed copy, so the packed form's entry counts too ({"packed": True, ...} when it
+    is the fastest).  CS_GEMM_DISPATCH=0 turns the table off, CS_GEMM_DISPATCH=<file> reads
+    another one."""
     global _gemm_table
     if _gemm_table is None:
         env = os.environ.get("CS_GEMM_DISPATCH", "")
@@ -756,17 +759,54 @@ def gemm_choice(M: int, N: int, K: int, gated: bool = False) -> Optional[dict]:
             with open(path) as f:
                 table = json.load(f).get("table", {})
         _gemm_table = table
-    return _gemm_table.get(f"{M},{N},{K},{int(bool(gated))}")
+    e = _gemm_table.get(f"{M},{N},{K},{int(bool(gated))}")
+    if e is None:
+        return None
+    if packed and "packed" in e:
+        return {"variant": int(e["packed"]["variant"]), "splits": int(e["packed"]["splits"]),
+                "packed": True}
+    if "variant" in e:
+        return {"variant": int(e["variant"]), "splits": int(e["splits"]), "packed": False}
+    return None
+
+
+def gemm_pack_gain(N: int, K: int, gated: bool = False) -> float:
+    """The largest time (µs) the packed form saves on an [N, K] weight at any row count the
+    dispatch table measured (against the faster of hipBLASLt and the unpacked cs_gemm_bf16);
+    0 when no row count runs it packed.  A model keeps cs_gemm_pack'ed copies of the weights
+    with a gain, the most per byte first."""
+    gemm_choice(1, N, K, gated)                 # loads the table
+    if hasattr(_gemm_table, "packs"):           # a computed table (tests)
+        return 1.0 if _gemm_table.packs(N, K, gated) else 0.0
+    tail = f",{N},{K},{int(bool(gated))}"
+    gain = 0.0
+    for k, v in _gemm_table.items():
+        if k.endswith(tail) and "packed" in v:
+            ref = min(float(v.get("us", float("inf"))), float(v.get("torch_us", float("inf"))))
+            gain = max(gain, ref - float(v["packed"]["us"]) if ref < float("inf") else 1.0)
+    return gain
+
+
+def gemm_packs(N: int, K: int, gated: bool = False) -> bool:
+    """Whether the dispatch table runs an [N, K] weight packed at some row count."""
+    return gemm_pack_gain(N, K, gated) > 0.0
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "silu",
-           out: Optional[torch.Tensor] = None, fold: bool = True):
+           out: Optional[torch.Tensor] = None, fold: bool = True,
+           packed: Optional["PackedWeight"] = None):
     """y = x @ w.T (gated: act(gate) * up of the fused gate|up weight) on whichever GEMM the
-    dispatch table measured faster for this shape: cs_gemm_bf16 or hipBLASLt (+ cs_gated_act).
+    dispatch table measured faster for this shape: cs_gemm_bf16 (on the packed copy
+    ``packed`` of w when given and fastest) or hipBLASLt (+ cs_gated_act).
     fold=False: a K-split cs_gemm_bf16 returns its unfolded SplitPartials (for an
     add_rms_norm to fold); every other path returns the bf16 tensor as usual."""
     if x.is_cuda and x.dim() == 2:
-        ch = gemm_choice(x.shape[0], w.shape[0], w.shape[1], gated)
+        ch = gemm_choice(x.shape[0], w.shape[0], w.shape[1], gated, packed=packed is not None)
+        if ch is not None and ch["packed"] and gemm_ok(x, w, gated):
+            if not fold and not gated and out is None and ch["splits"] > 1:
+                return gemm_packed_partials(x, packed, splits=ch["splits"], variant=ch["variant"])
+            return gemm_packed(x, packed, gated=gated, act=act, splits=ch["splits"],
+                               variant=ch["variant"], out=out)
         if ch is not None and gemm_ok(x, w, gated):
             if not fold and not gated and out is None and int(ch["splits"]) > 1:
                 return gemm_partials(x, w, splits=int(ch["splits"]), variant=int(ch["variant"]))
@@ -864,6 +904,82 @@ def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "s
                         part.data_ptr() if part is not None else None, _stream())
     _lib.check(rc, "cs_gemm_bf16")
     return out
+
+
+class PackedWeight:
+    """A [N, K] bf16 weight in cs_gemm_pack's fragment-major layout: each 16-row tile's
+    64-deep K step is 2 KB of lane-ordered MFMA fragments, so cs_gemm_bf16_packed reads its
+    weight stream in contiguous 1 KB pieces.  ``data`` is the packed [N * K] tensor."""
+
+    def __init__(self, data: torch.Tensor, N: int, K: int):
+        self.data, self.N, self.K = data, int(N), int(K)
+
+    @property
+    def shape(self):
+        return (self.N, self.K)
+
+
+def gemm_pack(w: torch.Tensor) -> PackedWeight:
+    """The packed copy of w [N, K] (cs_gemm_pack; N % 16 == 0, K % 64 == 0)."""
+    L = _lib.load()
+    if w.dim() != 2 or w.dtype != torch.bfloat16 or w.stride(1) != 1:
+        raise CSError("gemm_pack needs a bf16 [N, K] tensor with unit column stride")
+    N, K = w.shape
+    _require_cuda(w)
+    out = torch.empty(N * K, dtype=torch.bfloat16, device=w.device)
+    rc = L.cs_gemm_pack(w.data_ptr(), w.stride(0), N, K, out.data_ptr(), _stream())
+    _lib.check(rc, "cs_gemm_pack")
+    return PackedWeight(out, N, K)
+
+
+def gemm_packed(x: torch.Tensor, pw: PackedWeight, *, gated: bool = False, act: str = "silu",
+                splits: int = 0, variant: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ops.gemm on a packed weight (cs_gemm_bf16_packed, variants 0 / 2 / 3 / 4): bitwise the
+    unpacked result."""
+    L = _lib.load()
+    M, K = x.shape
+    N = pw.N
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1 or K != pw.K:
+        raise CSError("gemm_packed needs bf16 x [M, K] matching the packed weight")
+    n_out = N // 2 if gated else N
+    if out is None:
+        out = torch.empty(M, n_out, dtype=torch.bfloat16, device=x.device)
+    if out.shape != (M, n_out) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
+        raise CSError("out must be a bf16 [M, N] tensor with unit column stride")
+    _require_cuda(x, pw.data, out)
+    if gated:
+        splits = 1
+    elif splits <= 0:
+        splits = int(L.cs_gemm_splits(M, N, K, 0, variant))
+    ldx = x.stride(0) if M > 1 else K
+    ldy = out.stride(0) if M > 1 else n_out
+    if splits > 1 and (ldy % 8 or out.data_ptr() % 16):
+        out.copy_(gemm_packed(x, pw, splits=splits, variant=variant))
+        return out
+    part = (torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
+            if splits > 1 else None)
+    rc = L.cs_gemm_bf16_packed(x.data_ptr(), ldx, pw.data.data_ptr(), out.data_ptr(), ldy, M, N,
+                               K, splits, int(bool(gated)), {"silu": 0, "gelu_tanh": 1}[act],
+                               variant, part.data_ptr() if part is not None else None, _stream())
+    _lib.check(rc, "cs_gemm_bf16_packed")
+    return out
+
+
+def gemm_packed_partials(x: torch.Tensor, pw: PackedWeight, *, splits: int,
+                         variant: int = 0) -> SplitPartials:
+    """gemm_partials on a packed weight (cs_gemm_bf16_packed with y = NULL)."""
+    L = _lib.load()
+    M, K = x.shape
+    N = pw.N
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1 or K != pw.K or splits < 2:
+        raise CSError("gemm_packed_partials needs bf16 x [M, K] matching the weight, splits >= 2")
+    _require_cuda(x, pw.data)
+    part = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    ldx = x.stride(0) if M > 1 else K
+    rc = L.cs_gemm_bf16_packed(x.data_ptr(), ldx, pw.data.data_ptr(), None, 0, M, N, K, splits, 0,
+                               0, variant, part.data_ptr(), _stream())
+    _lib.check(rc, "cs_gemm_bf16_packed")
+    return SplitPartials(part)
 
 
 def gemm_partials(x: torch.Tensor, w: torch.Tensor, *, splits: int, variant: int = 0) -> SplitPartials:

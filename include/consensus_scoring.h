@@ -438,6 +438,27 @@ int cs_gemm_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
 int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant);
 
 /*
+ * cs_gemm_pack — W [N, K] (row stride ldw) into the fragment-major layout of
+ * cs_gemm_bf16_packed: 16-row tile T, 64-deep K step s, half h (k 32h .. 32h + 31) is 1 KB at
+ * element ((T * K / 64 + s) * 2 + h) * 512, lane-linear (lane l's 8 elements = row 16T + l % 16,
+ * k 64s + 32h + 8 (l / 16) .. + 7).  A pure permutation (N * K elements out); N % 16 == 0,
+ * K % 64 == 0, 16-byte aligned.  Done once per weight, at model load.
+ *
+ * cs_gemm_bf16_packed — cs_gemm_bf16 (variants 0, 2, 3, 4; same splits, gated, act, workspace
+ * rules) on a packed W: every weight-fragment load is one contiguous 1 KB and each wave's W
+ * stream one sequential run, instead of 16 rows x 64 B.  Bitwise equal to cs_gemm_bf16 on the
+ * unpacked W.
+ *
+ * Replaces: the same projections of the remote forward as cs_gemm_bf16
+ *   (src/utils.py:249-259).
+ */
+int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packed,
+                 cs_stream_t stream);
+int cs_gemm_bf16_packed(const void* x, int64_t ldx, const void* w_packed, void* y, int64_t ldy,
+                        int64_t M, int64_t N, int64_t K, int splits, int gated, int act,
+                        int variant, float* workspace, cs_stream_t stream);
+
+/*
  * cs_gemm_bf16_streamk — cs_gemm_bf16 (variants 2-4, plain or gated; variant 1 maps to 3 /
  * 2) with the tiles' K steps divided evenly over `blocks` workgroups (stream-K; blocks <= 0:
  * one per CU): every CU gets the same number of K steps, with no partly idle last round of

@@ -65,31 +65,51 @@ class _EveryShape(dict):
         return {"variant": 2 if N % 256 == 0 else 3, "splits": 1}
 
 
+class _EveryShapePacked(_EveryShape):
+    """Every shape cs_gemm_bf16 takes, on the packed-weight form (cs_gemm_pack'ed copies,
+    cs_gemm_bf16_packed)."""
+
+    def get(self, key, default=None):
+        e = super().get(key, default)
+        return {"packed": e} if e is not default else default
+
+    def packs(self, N, K, gated):
+        return N % 128 == 0 and K % 64 == 0
+
+
 @pytest.fixture(scope="module", params=[(f, r) for f in BF16_TRACE_FILES
-                                        for r in ("dispatch", "cs_gemm")],
+                                        for r in ("dispatch", "cs_gemm", "packed")],
                 ids=lambda p: f"{p[0]}-{p[1]}")
 def bf16_traces(request, dev):
     fname, route = request.param
     ops = importlib.import_module(mp.PKG + ".ops")
     t = mp.load_traces(fname)
-    t["_file"] = fname if route == "dispatch" else f"{fname} (every GEMM on cs_gemm)"
+    t["_file"] = fname if route == "dispatch" else (
+        f"{fname} (every GEMM on cs_gemm)" if route == "cs_gemm" else
+        f"{fname} (every GEMM on cs_gemm, packed weights)")
     eng, tok = mp.register_fixture_engine(t, dev, dtype=torch.bfloat16)
     assert eng.model.fused_ok(), "fixture heads must be served by the stream kernels"
     saved_table, saved_gemm = ops._gemm_table, ops.gemm
+    saved_packed = ops.gemm_packed
     calls = [0]
-    if route == "cs_gemm":
-        def counted(*a, **k):
-            calls[0] += 1
-            return saved_gemm(*a, **k)
-        ops._gemm_table = _EveryShape()
-        ops.gemm = counted
+    if route in ("cs_gemm", "packed"):
+        def counted(fn):
+            def run(*a, **k):
+                calls[0] += 1
+                return fn(*a, **k)
+            return run
+        ops._gemm_table = _EveryShape() if route == "cs_gemm" else _EveryShapePacked()
+        if route == "cs_gemm":
+            ops.gemm = counted(saved_gemm)
+        else:
+            ops.gemm_packed = counted(saved_packed)
     try:
         yield t, eng, tok
     finally:
-        ops._gemm_table, ops.gemm = saved_table, saved_gemm
+        ops._gemm_table, ops.gemm, ops.gemm_packed = saved_table, saved_gemm, saved_packed
         importlib.import_module(mp.PKG + ".runtime").clear_engines()
-    if route == "cs_gemm" and fname == "method_traces_c1.json":
-        assert calls[0] > 0, "no GEMM of the C1 fixture went through cs_gemm_bf16"
+    if route != "dispatch" and fname == "method_traces_c1.json":
+        assert calls[0] > 0, f"no GEMM of the C1 fixture went through the {route} route"
 
 
 def _report(name, key, value):

@@ -141,6 +141,65 @@ def test_thin_gemm_rejects_more_than_80_rows(ops, dev):
         ops.gemm(x, w, variant=5)
 
 
+@pytest.mark.parametrize("variant", [2, 3, 4])
+@pytest.mark.parametrize("M,N,K,gated", [
+    (20, 3072, 2048, 0), (48, 3584, 4096, 0), (72, 1024, 8192, 0), (272, 8192, 3584, 0),
+    (300, 512, 640, 0), (48, 1024, 448, 1), (272, 2048, 512, 1),
+])
+def test_packed_weight_gemm_is_bitwise_the_unpacked(ops, dev, M, N, K, gated, variant):
+    """cs_gemm_pack + cs_gemm_bf16_packed: the same fragments reach the same MFMAs, only
+    their addresses change -- bitwise the unpacked cs_gemm_bf16, for every K split."""
+    if variant in (2, 4) and N % 256:
+        pytest.skip("256-column tiles")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + gated)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    pw = ops.gemm_pack(w)
+    for sp in ((1,) if gated else (0, 1, 2, 4)):
+        if sp > 1 and K % (64 * sp):
+            continue
+        want = ops.gemm(x, w, gated=bool(gated), splits=sp, variant=variant)
+        got = ops.gemm_packed(x, pw, gated=bool(gated), splits=sp, variant=variant)
+        assert torch.equal(got, want), sp
+
+
+def test_gemm_pack_is_the_documented_permutation(ops, dev):
+    N, K = 32, 128
+    w = torch.arange(N * K, device=dev, dtype=torch.float32).view(N, K).to(torch.bfloat16)
+    p = ops.gemm_pack(w).data.view(-1)
+    T, s, h, lane, e = 1, 1, 1, 37, 5
+    at = ((T * (K // 64) + s) * 2 + h) * 512 + 8 * lane + e
+    assert p[at] == w[16 * T + lane % 16, 64 * s + 32 * h + 8 * (lane // 16) + e]
+    assert torch.equal(p.sort().values, w.view(-1).sort().values)
+
+
+def test_linear_runs_the_packed_copy_where_the_table_says_so(ops, dev):
+    """ops.linear with a cs_gemm_pack'ed copy takes the table's packed entry (plain, gated and
+    the unfolded K-split partials), bitwise the unpacked kernel of the same variant / split;
+    without the copy the unpacked entry; gemm_packs names the packed weights."""
+    M, N, K = 48, 1024, 512
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(dev, torch.bfloat16)
+    pw = ops.gemm_pack(w)
+    table = {f"{M},{N},{K},0": {"variant": 3, "splits": 2, "packed": {"variant": 3, "splits": 2}},
+             f"{M},{N},{K},1": {"packed": {"variant": 2, "splits": 1}}}
+    saved = ops._gemm_table
+    ops._gemm_table = table
+    try:
+        assert ops.gemm_choice(M, N, K)["packed"] is False
+        assert ops.gemm_choice(M, N, K, packed=True)["packed"] is True
+        assert ops.gemm_choice(M, N, K, True) is None            # no unpacked gated entry
+        assert ops.gemm_packs(N, K) and ops.gemm_packs(N, K, True) and not ops.gemm_packs(N, 2 * K)
+        assert torch.equal(ops.linear(x, w, packed=pw), ops.linear(x, w))
+        assert torch.equal(ops.linear(x, w, fold=False, packed=pw).part,
+                           ops.linear(x, w, fold=False).part)
+        got = ops.linear(x, w, gated=True, act="silu", packed=pw)
+        assert torch.equal(got, ops.gemm(x, w, gated=True, act="silu", variant=2))
+    finally:
+        ops._gemm_table = saved
+
+
 def test_gemm_rejects_unsupported_shapes(ops, dev):
     x = torch.zeros(4, 100, device=dev, dtype=torch.bfloat16)
     w = torch.zeros(128, 100, device=dev, dtype=torch.bfloat16)

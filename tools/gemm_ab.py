@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--msweep", default="", help="torch only: comma list of M for the C3 shapes")
     ap.add_argument("--lib", default="", help="time this build of the library (read before import)")
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--packed", action="store_true",
+                    help="also time cs_gemm_bf16_packed on cs_gemm_pack'ed copies of the weights")
     ap.add_argument("--warm", action="store_true",
                     help="one weight matrix for every call (L2 / Infinity-Cache resident when it "
                          "fits): the rate the kernel reaches when HBM is not what bounds it")
@@ -125,6 +127,18 @@ def main():
                    "us": round(t, 2), "weight_GBps": round(N * K * 2 / t / 1e3, 1),
                    "TFLOPs": round(2 * M * N * K / t / 1e6, 1), "max_err": err, "ref_max": scale}
             print(json.dumps(rec), flush=True)
+        if args.packed:
+            pws = [ops.gemm_pack(wi) for wi in ws]
+            for var in [int(v) for v in args.variants.split(",") if int(v) in (0, 2, 3, 4)]:
+                y = ops.gemm_packed(x, pws[0], gated=bool(gated), variant=var)
+                same = bool(torch.equal(y, ops.gemm(x, ws[0], gated=bool(gated), variant=var)))
+                t = timed(lambda: [ops.gemm_packed(x, pws[i % nw], gated=bool(gated), variant=var)
+                                   for i in range(calls)]) / calls * 1e3
+                print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "warm": args.warm,
+                                  "impl": f"cs_gemm_v{var}_packed", "us": round(t, 2),
+                                  "weight_GBps": round(N * K * 2 / t / 1e3, 1),
+                                  "bitwise_equal_unpacked": same}), flush=True)
+            del pws
         if args.no_torch:
             del ws
             continue

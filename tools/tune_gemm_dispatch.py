@@ -78,6 +78,8 @@ def main() -> int:
     ap.add_argument("--configs", default="c1,c3,c5")
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--install", action="store_true")
+    ap.add_argument("--packed", type=int, default=1,
+                    help="1: also time cs_gemm_bf16_packed (weights in cs_gemm_pack's layout)")
     ap.add_argument("--merge", type=int, default=1,
                     help="1: keep the installed table's entries for shapes this run does not measure")
     ap.add_argument("--variants", default="2,3,4,5,6,7")
@@ -96,6 +98,7 @@ def main() -> int:
         for name, N, K, gated, act in shapes_of(preset):
             nw = max(2, min(20, (700 << 20) // (N * K * 2) + 1))
             ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05 for _ in range(nw)]
+            pws = [ops.gemm_pack(w) for w in ws] if args.packed else []
             for M in Ms:
                 x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
                 if gated:
@@ -127,16 +130,40 @@ def main() -> int:
                         cands.append({"variant": var, "splits": sp, "us": round(t, 2)})
                         if t < best[3]:
                             best = ("cs_gemm", var, sp, t)
+                # the packed-weight form (cs_gemm_bf16_packed on cs_gemm_pack'ed copies): used
+                # by a model that holds the packed copy of this weight, when it beats both
+                pbest = None
+                pcands = []
+                for var in ((2, 3, 4) if args.packed else ()):
+                    for sp in ((1,) if gated else (1, 2, 4, 8, 16)):
+                        if var in (2, 4) and N % 256:
+                            continue
+                        if K % (64 * sp) or K // (64 * sp) < 2:
+                            continue
+                        t = timed(lambda: [ops.gemm_packed(x, pws[i % nw], gated=bool(gated),
+                                                           act=act, splits=sp, variant=var)
+                                           for i in range(calls)]) / calls * 1e3
+                        pcands.append({"variant": var, "splits": sp, "us": round(t, 2)})
+                        if pbest is None or t < pbest[2]:
+                            pbest = (var, sp, t)
                 rec = {"config": cname, "gemm": name, "M": M, "N": N, "K": K, "gated": gated,
                        "torch_us": round(t_torch, 2), "cs_gemm": cands, "choice": best[0],
                        "best_us": round(best[3], 2)}
+                if args.packed:
+                    rec["cs_gemm_packed"] = pcands
                 record.append(rec)
                 print(json.dumps(rec), flush=True)
+                ent = {}
                 if best[0] == "cs_gemm":
-                    table[f"{M},{N},{K},{gated}"] = {"variant": best[1], "splits": best[2],
-                                                     "us": round(best[3], 2),
-                                                     "torch_us": round(t_torch, 2)}
-            del ws
+                    ent = {"variant": best[1], "splits": best[2], "us": round(best[3], 2),
+                           "torch_us": round(t_torch, 2)}
+                if pbest is not None and pbest[2] < best[3]:
+                    ent["packed"] = {"variant": pbest[0], "splits": pbest[1],
+                                     "us": round(pbest[2], 2)}
+                    ent["torch_us"] = round(t_torch, 2)
+                if ent:
+                    table[f"{M},{N},{K},{gated}"] = ent
+            del ws, pws
     if args.merge:
         # keep the installed table's choices for the shapes not measured in this run
         inst = os.path.join(REPO, PKG, "tuned", "gemm_dispatch_mi355x.json")
