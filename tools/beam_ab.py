@@ -82,6 +82,23 @@ def main():
                                                      workspace=wd2))
                     os.environ.pop("CS_DECODE_KP", None)
             os.environ.pop("CS_DECODE_BLOCK")
+        if "--knobs" in sys.argv:
+            # --knobs "CS_TARGET_WGS=512,CS_DECODE_BLOCK=1024;CS_TARGET_WGS=768" : each ';' group
+            # is one setting of the host planning knobs, timed on the fused decode launch
+            for grp in sys.argv[sys.argv.index("--knobs") + 1].split(";"):
+                kv = dict(x.split("=") for x in grp.split(",") if x)
+                old_env = {k: os.environ.get(k) for k in kv}
+                os.environ.update(kv)
+                wdk = ops.Workspace(zeroed=True)
+                try:
+                    r["decode[" + grp + "]_us"] = timed(lambda: ops.beam_decode_step(
+                        ref, x, R, K, "min", n_order=B, softcap=cap, workspace=wdk))
+                finally:
+                    for k, v in old_env.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
         if "--sweep" in sys.argv:
             for kp in (4, 8, 16):
                 for rf in (0, 1):
