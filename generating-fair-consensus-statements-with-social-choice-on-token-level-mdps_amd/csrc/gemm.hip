@@ -1159,6 +1159,27 @@ int gemm_impl(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, i
   return check_launch("cs_gemm_bf16");
 }
 
+// Reads [p, p + bytes) once with 16-byte loads (default cache policy, so the lines land in
+// the Infinity Cache) and keeps nothing: run on a side stream while the step's attention /
+// norm launches leave HBM idle, it turns the next GEMM's weight stream into cache hits.
+// `sink` is written only when `keep` is set (never in use), so the loads cannot be dropped.
+__global__ __launch_bounds__(256) void prefetch_kernel(const gu32x4* __restrict__ p, int64_t n_vec,
+                                                       uint32_t* __restrict__ sink, int keep) {
+  uint32_t acc = 0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256 * 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 * 4 + threadIdx.x; i < n_vec; i += stride) {
+    gu32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = i + u * 256;
+      v[u] = j < n_vec ? p[j] : gu32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+  }
+  if (keep) sink[static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x] = acc;
+}
+
 // Wp[((T * ns + s) * 2 + h) * 512 + 8 l + e] = W[16 T + l % 16][64 s + 32 h + 8 (l / 16) + e]
 __global__ __launch_bounds__(256) void gemm_pack_kernel(const uint16_t* __restrict__ W, int64_t ldw,
                                                         int64_t n_vec, int64_t ns,
@@ -1190,6 +1211,18 @@ int cs_gemm_bf16_packed(const void* x, int64_t ldx, const void* w_packed, void* 
                         int variant, float* workspace, cs_stream_t stream) {
   return gemm_impl(x, ldx, w_packed, K, y, ldy, M, N, K, splits, gated, act, variant, workspace,
                    stream, true);
+}
+
+int cs_prefetch(const void* p, int64_t bytes, int32_t blocks, cs_stream_t stream) {
+  if (bytes < 0 || blocks < 0) return fail(CS_ERR_INVALID, "cs_prefetch: negative size");
+  if (bytes == 0) return CS_OK;
+  if (!p || reinterpret_cast<uintptr_t>(p) & 15 || bytes % 16)
+    return fail(CS_ERR_INVALID, "cs_prefetch: p must be 16-byte aligned, bytes a multiple of 16");
+  if (blocks == 0) blocks = 256;
+  hipLaunchKernelGGL(prefetch_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const gu32x4*>(p), bytes / 16,
+                     nullptr, 0);
+  return check_launch("cs_prefetch");
 }
 
 int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packed,

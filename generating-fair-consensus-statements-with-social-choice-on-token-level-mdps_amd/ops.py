@@ -932,6 +932,16 @@ def gemm_pack(w: torch.Tensor) -> PackedWeight:
     return PackedWeight(out, N, K)
 
 
+def prefetch(t: "torch.Tensor | PackedWeight", blocks: int = 0) -> None:
+    """Read a weight once on the current stream so it lands in the Infinity Cache
+    (cs_prefetch); meant for a side stream beside launches that leave HBM idle."""
+    L = _lib.load()
+    d = t.data if isinstance(t, PackedWeight) else t
+    _require_cuda(d)
+    rc = L.cs_prefetch(d.data_ptr(), d.numel() * d.element_size(), int(blocks), _stream())
+    _lib.check(rc, "cs_prefetch")
+
+
 def gemm_packed(x: torch.Tensor, pw: PackedWeight, *, gated: bool = False, act: str = "silu",
                 splits: int = 0, variant: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """ops.gemm on a packed weight (cs_gemm_bf16_packed, variants 0 / 2 / 3 / 4): bitwise the

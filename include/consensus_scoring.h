@@ -454,6 +454,18 @@ int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant);
  */
 int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packed,
                  cs_stream_t stream);
+
+/*
+ * cs_prefetch — read [p, p + bytes) once (16-byte loads, default cache policy) over `blocks`
+ * workgroups (0: 256) and discard it, so the bytes land in the Infinity Cache.  p 16-byte
+ * aligned, bytes % 16 == 0.  An experiment aid (tools/prefetch_ab.py): a side-stream prefetch
+ * of the next GEMM's weight beside a 30 us HBM-idle phase made the 8-rank decode GEMMs
+ * slower, not faster (profiles/r04q_prefetch_ab.jsonl), so the decode step does not use it.
+ *
+ * Replaces: nothing in the reference (its forward is remote); a scheduling aid of the
+ *   decode step's weight stream.
+ */
+int cs_prefetch(const void* p, int64_t bytes, int32_t blocks, cs_stream_t stream);
 int cs_gemm_bf16_packed(const void* x, int64_t ldx, const void* w_packed, void* y, int64_t ldy,
                         int64_t M, int64_t N, int64_t K, int splits, int gated, int act,
                         int variant, float* workspace, cs_stream_t stream);
