@@ -865,6 +865,8 @@ __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) 
 struct RopeParams {
   const __bf16* qkv;
   int64_t ldqkv;
+  const float* part;        // rope_place_kernel<P, true>: fp32 K-split partials [splits][n_tok][ldqkv]
+  int32_t splits;
   const float* inv_freq;
   const int32_t* plen;
   const int32_t* gpfx;
@@ -885,7 +887,20 @@ struct RopeParams {
 // a per-thread loop over the heads serialised one memory round trip per head.
 constexpr int kRopeItems = 256;
 
-template <int P>
+// fp32 -> bf16, round to nearest even, quiet NaN: the rounding of cs_gemm_bf16's split-K
+// fold (gemm.hip gto_bf), so a fold done here is bitwise the fold done there
+__device__ __forceinline__ __bf16 rope_to_bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  const uint16_t h = (u & 0x7fffffffu) > 0x7f800000u
+                         ? static_cast<uint16_t>((u >> 16) | 0x40)
+                         : static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  return __builtin_bit_cast(__bf16, h);
+}
+
+// FOLD: the projection arrives as a K-split GEMM's unfolded fp32 partials (r.part), summed
+// here in split order and rounded as cs_gemm_bf16's own fold would -- one launch and one
+// bf16 round trip fewer per layer, bitwise the same q / K / V.
+template <int P, bool FOLD = false>
 __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r, int32_t n_split) {
   typedef __bf16 vec_t __attribute__((ext_vector_type(P)));
   __shared__ float cs[128], sn[128];                // D / 2 <= 128
@@ -910,9 +925,43 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r, int32_t n
   for (int item = split * kRopeItems + threadIdx.x; item < lim; item += 256) {
     const int hh = item / nq;
     const int i0 = P * (item - hh * nq);
-    const __bf16* src = row + static_cast<int64_t>(hh) * r.D + i0;
-    const vec_t a = *reinterpret_cast<const vec_t*>(src);
-    const vec_t b = *reinterpret_cast<const vec_t*>(src + half);
+    vec_t a, b;
+    if constexpr (FOLD) {
+      const int64_t off = tok * r.ldqkv + static_cast<int64_t>(hh) * r.D + i0;
+      const int64_t sstride = r.n_tok * r.ldqkv;
+      float fa[P], fb[P];
+#pragma unroll
+      for (int e = 0; e < P; e += 4) {
+        const f32x4 va = *reinterpret_cast<const f32x4*>(r.part + off + e);
+        const f32x4 vb = *reinterpret_cast<const f32x4*>(r.part + off + half + e);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          fa[e + c] = va[c];
+          fb[e + c] = vb[c];
+        }
+      }
+      for (int sp = 1; sp < r.splits; ++sp) {
+#pragma unroll
+        for (int e = 0; e < P; e += 4) {
+          const f32x4 va = *reinterpret_cast<const f32x4*>(r.part + sp * sstride + off + e);
+          const f32x4 vb = *reinterpret_cast<const f32x4*>(r.part + sp * sstride + off + half + e);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            fa[e + c] += va[c];
+            fb[e + c] += vb[c];
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < P; ++e) {
+        a[e] = rope_to_bf(fa[e]);
+        b[e] = rope_to_bf(fb[e]);
+      }
+    } else {
+      const __bf16* src = row + static_cast<int64_t>(hh) * r.D + i0;
+      a = *reinterpret_cast<const vec_t*>(src);
+      b = *reinterpret_cast<const vec_t*>(src + half);
+    }
     if (hh >= r.H + r.Hkv) {                         // v: transposed placement, no rotation
       if (r.skip_v) continue;
       const int g = hh - r.H - r.Hkv;
@@ -1327,20 +1376,61 @@ int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
                             S_src, S_dst, Hkv, ld_hist, D, stream);
 }
 
+}  // extern "C"
+
+namespace {
+int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t splits,
+                    const float* inv_freq, const int32_t* prefix_len, const int32_t* group_prefix,
+                    int32_t n_groups, const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
+                    int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
+                    int64_t ld_hist, cs_stream_t stream);
+}  // namespace
+
+extern "C" {
+
 int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const int32_t* prefix_len,
                   const int32_t* group_prefix, int32_t n_groups, const int32_t* hist_base,
                   int32_t n_str, int32_t T, int32_t H, int32_t Hkv, int32_t D, void* q_out,
                   void* k_hist, void* vt_hist, int64_t ld_hist, cs_stream_t stream) {
+  if (!qkv) return fail(CS_ERR_INVALID, "cs_rope_place: NULL pointer");
+  return rope_place_impl(qkv, ld_qkv, nullptr, 1, inv_freq, prefix_len, group_prefix, n_groups,
+                         hist_base, n_str, T, H, Hkv, D, q_out, k_hist, vt_hist, ld_hist, stream);
+}
+
+int cs_rope_place_splitk(const float* part, int32_t splits, const float* inv_freq,
+                         const int32_t* prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                         const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
+                         int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
+                         int64_t ld_hist, cs_stream_t stream) {
+  if (!part || splits < 1) return fail(CS_ERR_INVALID, "cs_rope_place_splitk: need partials, splits >= 1");
+  if (T >= 32) return fail(CS_ERR_INVALID, "cs_rope_place_splitk: T < 32 only (fold first for chunks)");
+  if (reinterpret_cast<uintptr_t>(part) % 16 || D % 16)
+    return fail(CS_ERR_INVALID, "cs_rope_place_splitk: partials 16-byte aligned, head_dim % 16 == 0");
+  return rope_place_impl(nullptr, static_cast<int64_t>(H + 2 * Hkv) * D, part, splits, inv_freq,
+                         prefix_len, group_prefix, n_groups, hist_base, n_str, T, H, Hkv, D, q_out,
+                         k_hist, vt_hist, ld_hist, stream);
+}
+
+}  // extern "C"
+
+namespace {
+int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t splits,
+                    const float* inv_freq, const int32_t* prefix_len, const int32_t* group_prefix,
+                    int32_t n_groups, const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
+                    int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
+                    int64_t ld_hist, cs_stream_t stream) {
   if (n_groups < 0 || n_str < 0 || T < 0) return fail(CS_ERR_INVALID, "cs_rope_place: negative size");
   if (n_groups == 0 || n_str == 0 || T == 0) return CS_OK;
   if (H <= 0 || Hkv <= 0 || D <= 0 || D % 2 != 0 || ld_qkv < static_cast<int64_t>(H + 2 * Hkv) * D)
     return fail(CS_ERR_INVALID, "cs_rope_place: bad head layout");
   if (ld_hist < T) return fail(CS_ERR_INVALID, "cs_rope_place: ld_hist < T");
-  if (!qkv || !inv_freq || !prefix_len || !hist_base || !q_out || !k_hist || !vt_hist)
+  if (!inv_freq || !prefix_len || !hist_base || !q_out || !k_hist || !vt_hist)
     return fail(CS_ERR_INVALID, "cs_rope_place: NULL pointer");
   RopeParams r;
   r.qkv = static_cast<const __bf16*>(qkv);
   r.ldqkv = ld_qkv;
+  r.part = part;
+  r.splits = splits;
   r.inv_freq = inv_freq;
   r.plen = prefix_len;
   r.gpfx = group_prefix;
@@ -1362,17 +1452,21 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
   const int64_t n_vwg = static_cast<int64_t>(n_groups) * n_str * Hkv * n_tiles;
   {
     const char* e = getenv("CS_ROPE_VTILE");
-    r.skip_v = (T >= 32 && ld_hist % 32 == 0 && ld_qkv % 8 == 0 &&
+    r.skip_v = (!part && T >= 32 && ld_hist % 32 == 0 && ld_qkv % 8 == 0 &&
                 reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && n_vwg <= 0x7fffffffLL &&
                 !(e && atoi(e) == 0)) ? 1 : 0;
   }
   // 8-pair (16-byte) items when every head's halves are 16-byte aligned, else 4-pair
-  const bool p8 = ld_qkv % 8 == 0 && reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && D % 16 == 0;
+  const bool p8 = part ? true
+                       : (ld_qkv % 8 == 0 && reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && D % 16 == 0);
   const int64_t n_items = static_cast<int64_t>(H + 2 * Hkv) * (D / 2) / (p8 ? 8 : 4);
   const int64_t n_split = (n_items + kRopeItems - 1) / kRopeItems;
   if (r.n_tok * n_split > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many tokens");
   const dim3 grid(static_cast<uint32_t>(r.n_tok * n_split));
-  if (p8)
+  if (part)
+    hipLaunchKernelGGL((rope_place_kernel<8, true>), grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+                       r, static_cast<int32_t>(n_split));
+  else if (p8)
     hipLaunchKernelGGL(rope_place_kernel<8>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), r,
                        static_cast<int32_t>(n_split));
   else
@@ -1383,5 +1477,4 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
                        static_cast<hipStream_t>(stream), r, static_cast<int32_t>(n_tiles));
   return check_launch("cs_rope_place");
 }
-
-}  // extern "C"
+}  // namespace

@@ -100,6 +100,14 @@ def rope_inv_freq(cfg: ModelConfig, device) -> torch.Tensor:
     return inv.to(torch.float32)
 
 
+# where a K-split projection's partials are folded in the stream forward: q|k|v inside
+# cs_rope_place_splitk (CS_FOLD_IN_ROPE=0: in cs_gemm_bf16's own launch); the output
+# projection in its own launch (CS_FOLD_IN_NORM=1: inside the residual add's
+# cs_add_rms_norm -- within noise, 0.4 ms slower at C5; profiles/r04s_fold_ab.jsonl)
+_FOLD_IN_ROPE = os.environ.get("CS_FOLD_IN_ROPE", "1") != "0"
+_FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "0") == "1"
+
+
 class Model:
     """Decoder weights + forward.  ``dtype`` is the weight/activation dtype."""
 
@@ -464,7 +472,10 @@ class Model:
         x = ops.add_rms_norm(h, self.w["l0.attn_norm"], eps, plus_one=g2)
         for i in range(c.n_layers):
             p = f"l{i}."
-            qkv = ops.linear(x, self.wf[p + "qkv"], packed=wp.get(p + "qkv"))
+            # a K-split q|k|v (decode steps, T < 32) hands its partials to cs_rope_place, a
+            # K-split output projection to the residual add: no fold launches
+            qkv = ops.linear(x, self.wf[p + "qkv"], packed=wp.get(p + "qkv"),
+                             fold=T >= 32 or c.head_dim % 16 != 0 or not _FOLD_IN_ROPE)
             q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
             ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
                            hist_k[i], hist_vt[i], group_prefix=group_prefix)
@@ -475,7 +486,8 @@ class Model:
                                      group_prefix=group_prefix,
                                      prefix_len_host=getattr(pfx, "lens_host", None),
                                      group_prefix_host=group_prefix_host)
-            o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"], packed=wp.get(p + "wo"))
+            o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"], packed=wp.get(p + "wo"),
+                           fold=not _FOLD_IN_NORM)
             # Gemma-2's post-attention / post-MLP norms of the branch ride in the residual
             # add's launch (b_weight): one cs_add_rms_norm per residual add
             x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2,

@@ -616,12 +616,36 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     return out
 
 
-def rope_place(qkv: torch.Tensor, inv_freq: torch.Tensor, prefix_len: torch.Tensor,
+def rope_place(qkv: "torch.Tensor | SplitPartials", inv_freq: torch.Tensor, prefix_len: torch.Tensor,
                hist_base: torch.Tensor, n_str: int, T: int, H: int, Hkv: int, D: int,
                q_out: torch.Tensor, k_hist: torch.Tensor, vt_hist: torch.Tensor, *,
                group_prefix: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """RoPE of the fused projection + placement of q / the new K, V (cs_rope_place)."""
+    """RoPE of the fused projection + placement of q / the new K, V (cs_rope_place).  qkv
+    may be a K-split GEMM's unfolded SplitPartials (T < 32): folded inside the launch
+    (cs_rope_place_splitk), bitwise the folded projection."""
     L = _lib.load()
+    if isinstance(qkv, SplitPartials):
+        part = qkv.part
+        S, Hkv2, ldh, Dk = k_hist.shape
+        n_tok = part.shape[1]
+        if (part.dim() != 3 or part.dtype != torch.float32 or not part.is_contiguous()
+                or part.shape[2] != (H + 2 * Hkv) * D):
+            raise CSError("qkv partials must be contiguous float32 [splits, n_tok, (H + 2 Hkv) D]")
+        if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32):
+            raise CSError("k_hist [S, Hkv, ldh, D] / vt_hist [S, Hkv, ldh/32, D, 32] layout mismatch")
+        if n_tok != S * T or S % n_str != 0:
+            raise CSError("qkv rows must be streams x T")
+        if tuple(q_out.shape) != (n_tok, H, D) or q_out.dtype != torch.bfloat16 or not q_out.is_contiguous():
+            raise CSError("q_out must be a contiguous [n_tok, H, D] bfloat16 tensor")
+        _require_cuda(part, inv_freq, prefix_len, hist_base, q_out, k_hist, vt_hist, group_prefix)
+        rc = L.cs_rope_place_splitk(part.data_ptr(), part.shape[0], inv_freq.data_ptr(),
+                                    prefix_len.data_ptr(),
+                                    group_prefix.data_ptr() if group_prefix is not None else None,
+                                    S // n_str, hist_base.data_ptr(), n_str, T, H, Hkv, D,
+                                    q_out.data_ptr(), k_hist.data_ptr(), vt_hist.data_ptr(), ldh,
+                                    _stream())
+        _lib.check(rc, "cs_rope_place_splitk")
+        return q_out
     if qkv.dim() != 2 or qkv.dtype != torch.bfloat16 or qkv.stride(1) != 1:
         raise CSError("qkv must be a 2-D bfloat16 tensor with unit column stride")
     n_tok = qkv.shape[0]

@@ -336,6 +336,21 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
                   void* k_hist, void* vt_hist, int64_t ld_hist, cs_stream_t stream);
 
 /*
+ * cs_rope_place_splitk — cs_rope_place on a K-split projection's unfolded fp32 partials
+ * part [splits][n_tok][(H + 2 Hkv) D] (cs_gemm_bf16 with y = NULL): each element is summed in
+ * split order and rounded to bf16 exactly as cs_gemm_bf16's own fold would, then rotated and
+ * placed -- bitwise cs_gemm_bf16 (folded) followed by cs_rope_place, one launch fewer.
+ * T < 32, head_dim % 16 == 0, part 16-byte aligned.
+ *
+ * Replaces: as cs_rope_place (src/utils.py:249-259).
+ */
+int cs_rope_place_splitk(const float* part, int32_t splits, const float* inv_freq,
+                         const int32_t* prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                         const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
+                         int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
+                         int64_t ld_hist, cs_stream_t stream);
+
+/*
  * cs_hist_gather — beam reordering of the per-stream K/V history (the cs_prefix_attention
  * layouts, all L layers in one buffer): for every layer l and stream s, the filled slots
  * j < *hist_base of stream parent[s] are copied,

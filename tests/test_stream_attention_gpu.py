@@ -543,3 +543,36 @@ def test_append_prefix_tokens_equals_prefill_of_the_longer_prompts(dev):
     tgt = torch.randint(0, 512, (12, 6), generator=g).to(dev).to(torch.int32)
     d = (eng.rows_logprobs(h1.reshape(12, -1), tgt) - eng.rows_logprobs(h2.reshape(12, -1), tgt)).abs().max()
     assert float(d) < 5e-2
+
+
+@pytest.mark.parametrize("D,H,Hkv,T,splits", [(64, 8, 2, 3, 4), (128, 32, 8, 1, 2),
+                                               (256, 16, 8, 2, 8), (128, 64, 8, 1, 1)])
+def test_rope_place_folds_split_partials_bitwise(ops, dev, D, H, Hkv, T, splits):
+    """cs_rope_place_splitk on a K-split projection's fp32 partials == the partials summed in
+    split order, rounded to bf16 (cs_gemm_bf16's own fold), then cs_rope_place -- bitwise, for
+    q, the rotated K and the placed V."""
+    M = importlib.import_module(PKG + ".model")
+    cfg = M.preset("tiny-llama", head_dim=D, n_heads=H, n_kv_heads=Hkv)
+    inv = M.rope_inv_freq(cfg, dev)
+    g = torch.Generator(device="cpu").manual_seed(D + H + splits)
+    n_prefix, n_str = 3, 2
+    S = n_prefix * n_str
+    hb = 5
+    ldh = _ceil32(hb + T)
+    width = (H + 2 * Hkv) * D
+    part = (torch.randn(splits, S * T, width, generator=g) * 2).to(dev)
+    folded = part[0].clone()
+    for sp in range(1, splits):
+        folded = folded + part[sp]
+    folded = folded.to(torch.bfloat16)
+    plen = torch.tensor([17, 250, 1000], dtype=torch.int32, device=dev)
+    hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
+    outs = []
+    for src in (folded, ops.SplitPartials(part)):
+        q_out = torch.empty(S * T, H, D, dtype=torch.bfloat16, device=dev)
+        kh = torch.zeros(S, Hkv, ldh, D, dtype=torch.bfloat16, device=dev)
+        vth = torch.zeros(S, Hkv, ldh // 32, D, 32, dtype=torch.bfloat16, device=dev)
+        ops.rope_place(src, inv, plen, hbt, n_str, T, H, Hkv, D, q_out, kh, vth)
+        outs.append((q_out, kh, vth))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
