@@ -91,6 +91,35 @@ def test_invalid_welfare_and_topk(pkg):
     assert L.cs_segment_reduce(d, -1, d, 1, None, None, None, None, None) == -1
 
 
+def test_round4_entry_points_validate_before_launching(pkg):
+    """The packed-weight GEMM, the thin variants, the split-K RoPE fold and the prefetch
+    reject bad arguments with a status code (no device needed: checked before any launch)."""
+    from importlib import import_module
+    L = import_module(pkg.__name__ + "._lib").load()
+    d = ctypes.c_void_p(256)
+    odd = ctypes.c_void_p(260)
+    # cs_gemm_pack: N % 16, K % 64, alignment
+    assert L.cs_gemm_pack(d, 64, 24, 64, d, None) == -1
+    assert L.cs_gemm_pack(d, 96, 32, 96, d, None) == -1
+    assert L.cs_gemm_pack(odd, 64, 32, 64, d, None) == -1
+    # cs_gemm_bf16_packed: ws2 variants only
+    assert L.cs_gemm_bf16_packed(d, 64, d, d, 128, 4, 128, 64, 1, 0, 0, 5, None, None) == -1
+    assert L.cs_gemm_bf16_packed(d, 64, d, d, 128, 4, 128, 64, 1, 0, 0, 1, None, None) == -1
+    # thin variants: at most 80 rows, no K split
+    assert L.cs_gemm_bf16(d, 64, d, 64, d, 128, 81, 128, 64, 1, 0, 0, 5, None, None) == -1
+    assert L.cs_gemm_bf16(d, 128, d, 128, d, 128, 8, 128, 128, 2, 0, 0, 6, d, None) == -1
+    assert L.cs_gemm_bf16(d, 64, d, 64, d, 128, 8, 128, 64, 1, 0, 0, 8, None, None) == -1
+    # cs_rope_place_splitk: T < 32, head_dim % 16, partials aligned
+    assert L.cs_rope_place_splitk(d, 2, d, d, None, 1, d, 1, 32, 4, 2, 64, d, d, d, 64, None) == -1
+    assert L.cs_rope_place_splitk(d, 2, d, d, None, 1, d, 1, 1, 4, 2, 40, d, d, d, 32, None) == -1
+    assert L.cs_rope_place_splitk(None, 2, d, d, None, 1, d, 1, 1, 4, 2, 64, d, d, d, 32, None) == -1
+    # cs_prefetch: alignment and size
+    assert L.cs_prefetch(odd, 64, 1, None) == -1
+    assert L.cs_prefetch(d, 24, 1, None) == -1
+    assert L.cs_prefetch(d, 0, 1, None) == 0
+    assert L.cs_last_error().decode()
+
+
 def test_missing_library_raises(pkg, monkeypatch, tmp_path):
     from importlib import import_module
     lib = import_module(pkg.__name__ + "._lib")
