@@ -70,3 +70,43 @@ def test_merge_replaces_the_measured_shapes_only(tmp_path, monkeypatch):
     assert set(m["table"]) == {"1,128,64,0", "3,128,64,0"}
     assert sorted(r["M"] for r in m["measured"]) == [1, 2, 3]
     assert [r["torch_us"] for r in m["measured"] if r["M"] == 2] == [1.0]
+
+
+def test_pack_decode_weights_orders_by_gain_per_byte_within_the_budget(monkeypatch):
+    """Model.pack_decode_weights keeps packed copies of the weights with a packed gain, the
+    most time saved per byte first, while the device keeps its reserve free (host logic:
+    the device memory query and the pack launch are stubbed)."""
+    import torch
+    M = importlib.import_module(PKG + ".model")
+    ops = importlib.import_module(PKG + ".ops")
+    cfg = M.preset("tiny-llama")
+    m = M.Model(cfg, "cpu", dtype=torch.bfloat16)
+    m.device = torch.device("cuda", 0)                 # the packing path, with stubs below
+    sizes = {n: w.numel() * 2 for n, (w, _) in m.decode_weights().items()}
+    # gains (us) by weight kind: gate|up saves the most per byte, then q|k|v; down none
+    gains = {"gate_up": 4.0, "qkv": 1.5, "wo": 0.1, "w_down": 0.0, "lm_head": 0.2}
+
+    def gain(N, K, gated=False):
+        if gated:
+            return gains["gate_up"] * N * K
+        for name, (w, g) in m.decode_weights().items():
+            if not g and tuple(w.shape) == (N, K):
+                return gains[name.split(".")[-1]] * N * K
+        return 0.0
+
+    packed = []
+    monkeypatch.setattr(ops, "gemm_pack_gain", gain)
+    monkeypatch.setattr(ops, "gemm_pack", lambda w: packed.append(tuple(w.shape)) or ("packed", w.shape))
+    gu = sum(v for n, v in sizes.items() if n.endswith("gate_up"))
+    qkv = sum(v for n, v in sizes.items() if n.endswith("qkv"))
+    budget = gu + qkv // 2                             # every gate|up, half the q|k|v
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (budget + (1 << 30), 8 << 30))
+    used = m.pack_decode_weights(reserve_bytes=1 << 30)
+    names = set(m.wp)
+    assert all(n in names for n in sizes if n.endswith("gate_up"))
+    assert not any(n.endswith("w_down") for n in names)          # no gain: never packed
+    assert used <= budget and used == sum(sizes[n] for n in names)
+    n_qkv = sum(1 for n in names if n.endswith("qkv"))
+    assert 0 < n_qkv < cfg.n_layers                     # the budget ran out inside q|k|v
+    monkeypatch.setenv("CS_GEMM_PACK", "0")
+    assert m.pack_decode_weights() == 0 and m.wp == {}
