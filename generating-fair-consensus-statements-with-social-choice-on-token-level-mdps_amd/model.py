@@ -400,7 +400,8 @@ class Model:
         the re-tokenized text path's, plus activations, logits and graph pools).  The weights whose
         packed form saves the most time per byte (ops.gemm_pack_gain) go first, so a partial
         budget (a 70B replica) packs where it pays most.  CS_GEMM_PACK=0 turns packing off.
-        Returns the bytes packed."""
+        The copies are snapshots: code that changes a weight in place after the first stream
+        forward must call this again (or set ``wp = None``).  Returns the bytes packed."""
         from . import ops
         self.wp = {}
         if (os.environ.get("CS_GEMM_PACK", "1") == "0" or self.device.type != "cuda"
