@@ -415,7 +415,11 @@ class Model:
         for name, (w, gated) in self.decode_weights().items():
             if w.shape[0] % 16 or w.shape[1] % 64:
                 continue
+            # a gate|up weight runs packed fused (gated key) or as the plain packed GEMM +
+            # cs_gated_act (plain key), whichever the table kept
             gain = ops.gemm_pack_gain(w.shape[0], w.shape[1], gated)
+            if gated:
+                gain = max(gain, ops.gemm_pack_gain(w.shape[0], w.shape[1], False))
             if gain > 0.0:
                 cands.append((gain / (w.numel() * w.element_size()), name, w))
         cands.sort(key=lambda c: -c[0])

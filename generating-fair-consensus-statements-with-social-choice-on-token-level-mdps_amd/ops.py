@@ -836,9 +836,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = 
                 return gemm_partials(x, w, splits=int(ch["splits"]), variant=int(ch["variant"]))
             return gemm(x, w, gated=gated, act=act, splits=int(ch["splits"]),
                         variant=int(ch["variant"]), out=out)
-    if gated:          # the plain GEMM (on whichever library is faster) + cs_gated_act
+    if gated:          # the plain GEMM (on whichever form is faster) + cs_gated_act
         F = w.shape[0] // 2
-        y = linear(x, w)
+        y = linear(x, w, packed=packed)
         return gated_act(y[:, :F], y[:, F:], act, out=out)
     if out is not None:
         return torch.matmul(x, w.t(), out=out)

@@ -110,3 +110,22 @@ def test_pack_decode_weights_orders_by_gain_per_byte_within_the_budget(monkeypat
     assert 0 < n_qkv < cfg.n_layers                     # the budget ran out inside q|k|v
     monkeypatch.setenv("CS_GEMM_PACK", "0")
     assert m.pack_decode_weights() == 0 and m.wp == {}
+
+
+def test_prune_drops_fused_gated_entries_that_lose_to_plain_plus_act():
+    sys.path.insert(0, REPO)
+    merge = importlib.import_module("tools.merge_gemm_dispatch")
+    table = {"48,256,64,1": {"packed": {"variant": 3, "splits": 1, "us": 50.0}},
+             "80,256,64,1": {"variant": 2, "splits": 1, "us": 40.0},
+             "48,256,64,0": {"packed": {"variant": 3, "splits": 1, "us": 38.0}}}
+    measured = [
+        {"M": 48, "N": 256, "K": 64, "gated": 1, "torch_us": 60.0, "cs_gemm": []},
+        {"M": 48, "N": 256, "K": 64, "gated": 0, "torch_us": 55.0, "cs_gemm": [{"us": 45.0}],
+         "cs_gemm_packed": [{"us": 38.0}]},
+        {"M": 80, "N": 256, "K": 64, "gated": 1, "torch_us": 70.0, "cs_gemm": []},
+        {"M": 80, "N": 256, "K": 64, "gated": 0, "torch_us": 64.0, "cs_gemm": [{"us": 50.0}]},
+    ]
+    # 48: plain packed 38 + act (60 - 55) = 43 < fused 50 -> dropped
+    # 80: plain 50 + act 6 = 56 > fused 40 -> kept
+    assert merge.prune_gated(table, measured) == ["48,256,64,1"]
+    assert "80,256,64,1" in table and "48,256,64,0" in table

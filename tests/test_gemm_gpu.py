@@ -196,6 +196,11 @@ def test_linear_runs_the_packed_copy_where_the_table_says_so(ops, dev):
                            ops.linear(x, w, fold=False).part)
         got = ops.linear(x, w, gated=True, act="silu", packed=pw)
         assert torch.equal(got, ops.gemm(x, w, gated=True, act="silu", variant=2))
+        # no gated entry: the plain GEMM's packed entry + cs_gated_act
+        del table[f"{M},{N},{K},1"]
+        got = ops.linear(x, w, gated=True, act="silu", packed=pw)
+        gu = ops.gemm_packed(x, pw, splits=2, variant=3)
+        assert torch.equal(got, ops.gated_act(gu[:, :N // 2], gu[:, N // 2:], "silu"))
     finally:
         ops._gemm_table = saved
 

@@ -1,6 +1,7 @@
 """Merge tools/tune_gemm_dispatch.py outputs (--merge 0 runs, one per config) into the
 installed selection: entries and measurements of the shapes a newer file measured replace
-the older ones.
+the older ones; then drop the fused gated entries that lose to the plain gate|up GEMM +
+cs_gated_act (prune_gated).
 
     python tools/merge_gemm_dispatch.py gpurun_out/a.json gpurun_out/b.json [--install]
 """
@@ -15,6 +16,38 @@ INSTALLED = os.path.join(REPO, PKG, "tuned", "gemm_dispatch_mi355x.json")
 
 def key(r):
     return f"{r['M']},{r['N']},{r['K']},{r['gated']}"
+
+
+def _best_plain(rec):
+    """The fastest measured form of a plain (ungated) GEMM record, in us."""
+    c = [rec["torch_us"]] + [x["us"] for x in rec.get("cs_gemm", [])] + \
+        [x["us"] for x in rec.get("cs_gemm_packed", [])]
+    return min(c)
+
+
+def prune_gated(table, measured):
+    """Drop the fused gated entries (act(gate) * up in the GEMM epilogue) that lose to the
+    plain gate|up GEMM on its fastest form + cs_gated_act: ops.linear then takes that path
+    (the plain key's entry, packed when the model holds the packed copy).  The activation's
+    cost is the measured hipBLASLt difference: (gate|up + act) - gate|up.  Returns the keys
+    dropped."""
+    recs = {key(r): r for r in measured}
+    dropped = []
+    for k, e in list(table.items()):
+        M, N, K, g = k.split(",")
+        if g != "1":
+            continue
+        rg, rp = recs.get(k), recs.get(f"{M},{N},{K},0")
+        if rg is None or rp is None:
+            continue
+        act = max(0.0, rg["torch_us"] - rp["torch_us"])
+        unfused = _best_plain(rp) + act
+        cands = ([e["us"]] if "variant" in e else []) + ([e["packed"]["us"]] if "packed" in e else [])
+        fused = min(cands) if cands else float("inf")
+        if unfused < fused:
+            del table[k]
+            dropped.append(k)
+    return dropped
 
 
 def main() -> int:
@@ -35,11 +68,13 @@ def main() -> int:
         measured = [r for r in measured if key(r) not in seen] + new["measured"]
         for k in ("device", "torch", "hip", "library"):
             base[k] = new.get(k, base.get(k))
+    dropped = prune_gated(table, measured)
     base["table"], base["measured"] = table, measured
     out = INSTALLED if a.install else (a.out or os.path.join(REPO, "gpurun_out", "gemm_dispatch_merged.json"))
     with open(out, "w") as f:
         json.dump(base, f, indent=1)
-    print(out, len(table), "entries,", sum("packed" in v for v in table.values()), "packed")
+    print(out, len(table), "entries,", sum("packed" in v for v in table.values()), "packed;",
+          len(dropped), "fused gated entries lose to the plain GEMM + cs_gated_act:", dropped)
     return 0
 
 

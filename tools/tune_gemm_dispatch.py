@@ -174,6 +174,8 @@ def main() -> int:
             table = {**{k: v for k, v in old.get("table", {}).items() if k not in seen}, **table}
             record = [r for r in old.get("measured", [])
                       if f"{r['M']},{r['N']},{r['K']},{r['gated']}" not in seen] + record
+    # fused gated entries that lose to the plain GEMM's best form + cs_gated_act
+    importlib.import_module("tools.merge_gemm_dispatch").prune_gated(table, record)
     out = {"device": torch.cuda.get_device_name(0), "torch": torch.__version__,
            "hip": torch.version.hip, "library": ops._lib.version(),
            "note": "shapes absent here run on hipBLASLt (torch)", "table": table,
