@@ -27,6 +27,11 @@ R = importlib.import_module(PKG + ".runtime")
 ops = importlib.import_module(PKG + ".ops")
 model = importlib.import_module(PKG + ".model")
 
+# projections whose K-split partials the stream forward folds in the consumer's launch
+# (q|k|v in cs_rope_place_splitk, down in cs_add_rms_norm_splitk): their split forms are
+# timed without cs_gemm_bf16's own fold
+FOLDED_BY_CONSUMER = ("qkv", "down")
+
 CONFIGS = {"c1": ("llama-3.2-1b", 4, 4), "c3": ("gemma-2-9b", 16, 16), "c5": ("llama-3.3-70b", 64, 8),
            "c4": ("llama-3.1-8b", 32, 0)}
 # C4's lookahead tree (branching 4, depth 4): the forward segments of tree levels 1-3 under
@@ -83,6 +88,7 @@ def main() -> int:
     ap.add_argument("--merge", type=int, default=1,
                     help="1: keep the installed table's entries for shapes this run does not measure")
     ap.add_argument("--variants", default="2,3,4,5,6,7")
+    ap.add_argument("--gemms", default="", help="only these shapes (e.g. qkv,down)")
     ap.add_argument("--sk", type=int, default=0,
                     help="1: also time the stream-K form (splits = -1, cs_gemm_bf16_streamk; "
                          "slower than the split-K form on every C5 shape in r04d)")
@@ -96,6 +102,8 @@ def main() -> int:
         preset, A, B = CONFIGS[cname]
         Ms = sorted({m for w in map(int, args.worlds.split(",")) for m in rows_of(cname, A, B, w)})
         for name, N, K, gated, act in shapes_of(preset):
+            if args.gemms and name not in args.gemms.split(","):
+                continue
             nw = max(2, min(20, (700 << 20) // (N * K * 2) + 1))
             ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05 for _ in range(nw)]
             pws = [ops.gemm_pack(w) for w in ws] if args.packed else []
@@ -124,9 +132,14 @@ def main() -> int:
                             continue
                         if sp > 0 and (K % (64 * sp) or K // (64 * sp) < 2):
                             continue
-                        t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated), act=act,
-                                                    splits=sp, variant=var)
-                                           for i in range(calls)]) / calls * 1e3
+                        if sp > 1 and name in FOLDED_BY_CONSUMER:
+                            t = timed(lambda: [ops.gemm_partials(x, ws[i % nw], splits=sp,
+                                                                 variant=var)
+                                               for i in range(calls)]) / calls * 1e3
+                        else:
+                            t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated),
+                                                        act=act, splits=sp, variant=var)
+                                               for i in range(calls)]) / calls * 1e3
                         cands.append({"variant": var, "splits": sp, "us": round(t, 2)})
                         if t < best[3]:
                             best = ("cs_gemm", var, sp, t)
@@ -140,9 +153,14 @@ def main() -> int:
                             continue
                         if K % (64 * sp) or K // (64 * sp) < 2:
                             continue
-                        t = timed(lambda: [ops.gemm_packed(x, pws[i % nw], gated=bool(gated),
-                                                           act=act, splits=sp, variant=var)
-                                           for i in range(calls)]) / calls * 1e3
+                        if sp > 1 and name in FOLDED_BY_CONSUMER:
+                            t = timed(lambda: [ops.gemm_packed_partials(x, pws[i % nw],
+                                                                        splits=sp, variant=var)
+                                               for i in range(calls)]) / calls * 1e3
+                        else:
+                            t = timed(lambda: [ops.gemm_packed(x, pws[i % nw], gated=bool(gated),
+                                                               act=act, splits=sp, variant=var)
+                                               for i in range(calls)]) / calls * 1e3
                         pcands.append({"variant": var, "splits": sp, "us": round(t, 2)})
                         if pbest is None or t < pbest[2]:
                             pbest = (var, sp, t)
