@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 from dataclasses import dataclass, field, replace
 from typing import Dict, List, Optional, Sequence
 
@@ -105,6 +106,7 @@ def rope_inv_freq(cfg: ModelConfig, device) -> torch.Tensor:
 # projection in its own launch (CS_FOLD_IN_NORM=1: inside the residual add's
 # cs_add_rms_norm -- within noise, 0.4 ms slower at C5; profiles/r04s_fold_ab.jsonl)
 _FOLD_IN_ROPE = os.environ.get("CS_FOLD_IN_ROPE", "1") != "0"
+_PACK_LOCK = threading.Lock()
 _FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "0") == "1"
 
 
@@ -403,9 +405,9 @@ class Model:
         The copies are snapshots: code that changes a weight in place after the first stream
         forward must call this again (or set ``wp = None``).  Returns the bytes packed."""
         from . import ops
-        self.wp = {}
         if (os.environ.get("CS_GEMM_PACK", "1") == "0" or self.device.type != "cuda"
                 or self.dtype != torch.bfloat16):
+            self.wp = {}
             return 0
         free, total = torch.cuda.mem_get_info(self.device)
         if reserve_bytes is None:
@@ -424,11 +426,13 @@ class Model:
                 cands.append((gain / (w.numel() * w.element_size()), name, w))
         cands.sort(key=lambda c: -c[0])
         used = 0
+        wp = {}
         for _, name, w in cands:
             nbytes = w.numel() * w.element_size()
             if nbytes <= budget - used:
-                self.wp[name] = ops.gemm_pack(w)
+                wp[name] = ops.gemm_pack(w)
                 used += nbytes
+        self.wp = wp          # published whole: a concurrent forward sees all or nothing
         return used
 
     # --- stream forward over shared prefixes (HIP attention) ----------------------
@@ -470,7 +474,11 @@ class Model:
         act = "gelu_tanh" if g2 else "silu"
         eps = c.rms_eps
         if self.wp is None and not torch.cuda.is_current_stream_capturing():
-            self.pack_decode_weights()
+            # once per model; a concurrent first forward waits here, so every forward (and
+            # every graph captured after its thread's first eager forward) uses the same copies
+            with _PACK_LOCK:
+                if self.wp is None:
+                    self.pack_decode_weights()
         wp = self.wp or {}
         h = self._embed(tokens).contiguous()                 # the residual stream [n_tok, d]
         # every residual add + RMSNorm is one cs_add_rms_norm launch; h is updated in place
