@@ -918,14 +918,17 @@ int ws_mw(int64_t M) {
   return static_cast<int>(mw < kGemmMaxMW ? mw : kGemmMaxMW);
 }
 
-// ws2: row tiles per workgroup (instantiated counts) and row blocks for M rows
-constexpr int kWs2MT[] = {2, 4, 8, 9, 12, 17, 18};
-void ws2_rows(int64_t M, int* mt, int64_t* mblocks, int max_tiles = 18) {
+// ws2: row tiles per workgroup (instantiated counts) and row blocks for M rows. The 5-tile
+// block is taken on packed weights only (per-rank C5, 72 rows: 1-2% over 8 tiles there,
+// profiles/r04af_ws2_mt5_ab.jsonl); on row-major weights it measured slower (gate|up 194 -> 224 us).
+constexpr int kWs2MT[] = {2, 4, 5, 8, 9, 12, 17, 18};
+void ws2_rows(int64_t M, int* mt, int64_t* mblocks, int max_tiles = 18, bool packed = false) {
   const int64_t tiles = (M + 15) / 16;
   const int64_t mb = (tiles + max_tiles - 1) / max_tiles;
   const int64_t per = (tiles + mb - 1) / mb;
   int v = 18;
   for (int c : kWs2MT) {
+    if (c == 5 && !packed) continue;
     if (c >= per) { v = c; break; }
   }
   *mt = v;
@@ -952,7 +955,8 @@ void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t
                                             gate_off, nk, n_tiles, splits, act, m_blocks);      \
     break;
   switch (mt) {
-    CS_WS2_CASE(2) CS_WS2_CASE(4) CS_WS2_CASE(8) CS_WS2_CASE(9) CS_WS2_CASE(12) CS_WS2_CASE(17)
+    CS_WS2_CASE(2) CS_WS2_CASE(4) CS_WS2_CASE(5) CS_WS2_CASE(8) CS_WS2_CASE(9) CS_WS2_CASE(12)
+    CS_WS2_CASE(17)
     CS_WS2_CASE(18)
     default: break;
   }
@@ -1122,7 +1126,7 @@ int gemm_impl(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, i
   } else {
     int mt;
     int64_t mb;
-    ws2_rows(M, &mt, &mb, variant_max_tiles(variant));
+    ws2_rows(M, &mt, &mb, variant_max_tiles(variant), packed);
     const int n_tiles = static_cast<int>(N / variant_bn(variant, gated));
     const int64_t grid = ws2_grid(static_cast<int64_t>(n_tiles) * splits, mb);
     if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");

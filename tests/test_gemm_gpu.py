@@ -145,6 +145,8 @@ def test_thin_gemm_rejects_more_than_80_rows(ops, dev):
 @pytest.mark.parametrize("M,N,K,gated", [
     (20, 3072, 2048, 0), (48, 3584, 4096, 0), (72, 1024, 8192, 0), (272, 8192, 3584, 0),
     (300, 512, 640, 0), (48, 1024, 448, 1), (272, 2048, 512, 1),
+    # 65-80 rows: the packed launch takes a 5-tile row block, the unpacked one 8 tiles
+    (65, 1024, 512, 0), (72, 2048, 1024, 1),
 ])
 def test_packed_weight_gemm_is_bitwise_the_unpacked(ops, dev, M, N, K, gated, variant):
     """cs_gemm_pack + cs_gemm_bf16_packed: the same fragments reach the same MFMAs, only
