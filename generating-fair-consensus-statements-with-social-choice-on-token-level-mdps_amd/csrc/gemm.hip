@@ -544,8 +544,11 @@ __device__ __forceinline__ void ws2_store(const gf32x4 (&acc)[MT][NT], uint16_t*
 // W goes to registers through inline-asm loads, so the compiler's waits never drain the
 // DMA queue: one counted s_waitcnt vmcnt per step (this step's X and W landed, the next
 // two steps' loads still in flight) + a raw s_barrier.
+#ifndef CS_WS2_GATED4
+#define CS_WS2_GATED4 1   // variant 3 gated: 4 waves x 32 W rows (64 features) per workgroup
+#endif
 template <int MT, int NT, int GATED, int WAVES, bool PACKED = false>
-__global__ __launch_bounds__(64 * WAVES, 1) void ws2_gemm_kernel(
+__global__ __launch_bounds__(64 * WAVES, WAVES == 4 ? 2 : 1) void ws2_gemm_kernel(
     const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
     uint16_t* __restrict__ Y, int64_t ldy, float* __restrict__ P, int64_t M, int64_t n_out,
     int64_t gate_off, int nk, int n_tiles, int splits, int act, int m_blocks) {
@@ -993,7 +996,7 @@ void dispatch_sk(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t 
 // 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
 int64_t variant_bn(int variant, int gated) {
   if (variant == 1) return 128;
-  if (variant == 3 && !gated) return 128;
+  if (variant == 3) return gated && !CS_WS2_GATED4 ? 256 : 128;
   return 256;
 }
 
@@ -1019,7 +1022,7 @@ int resolve_variant(int variant, int64_t N, int gated) {
   if (variant == 0) variant = 2;
   if (thin_variant(variant)) return variant;
   if ((variant == 2 || variant == 4) && N % 256) variant = gated ? 1 : 3;
-  if (variant == 3 && gated) variant = 2;
+  if (variant == 3 && gated && (!CS_WS2_GATED4 || N % 128)) variant = 2;
   return variant;
 }
 
@@ -1132,7 +1135,14 @@ int gemm_impl(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, i
     if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
     const int b = static_cast<int>(grid);
     const int mbi = static_cast<int>(mb);
-    if (gated) {
+    if (gated && variant == 3) {
+      if (packed)
+        dispatch_ws2<2, 1, 4, true>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                    n_tiles, 1, act, mbi);
+      else
+        dispatch_ws2<2, 1, 4, false>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                     n_tiles, 1, act, mbi);
+    } else if (gated) {
       if (packed)
         dispatch_ws2<2, 1, 8, true>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
                                     n_tiles, 1, act, mbi);
@@ -1265,6 +1275,7 @@ SkPlan sk_plan(int64_t M, int64_t N, int64_t K, int gated, int variant, int32_t 
   SkPlan p{};
   p.variant = resolve_variant(variant, N, gated);
   if (p.variant == 1) p.variant = gated ? 2 : 3;     // the stream-K form is ws2's
+  if (gated && p.variant == 3) p.variant = 2;         // (8 waves: no 4-wave gated form)
   ws2_rows(M, &p.mt, &p.mb, variant_max_tiles(p.variant));
   p.n_tiles = N / variant_bn(p.variant, gated);
   p.units = p.n_tiles * p.mb * (K / kGemmBK);
