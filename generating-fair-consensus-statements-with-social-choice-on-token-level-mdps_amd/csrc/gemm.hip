@@ -992,8 +992,8 @@ void dispatch_sk(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t 
 #undef CS_SK_CASE
 }
 
-// W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16;
-// 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
+// W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16, gated
+// 4 x 32; 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
 int64_t variant_bn(int variant, int gated) {
   if (variant == 1) return 128;
   if (variant == 3) return gated && !CS_WS2_GATED4 ? 256 : 128;

@@ -435,7 +435,8 @@ int cs_gated_act(const void* gate, int64_t ld_gate, const void* up, int64_t ld_u
  * takes cs_gemm_splits; y = NULL with splits > 1 leaves the partials [splits][M][N] in the
  * workspace unfolded (cs_add_rms_norm_splitk folds them).  variant: 0 = the library's choice, 1 = 2 x 4 wave grid (128 columns x
  * up to 288 rows per workgroup), 2 = column-only wave split, 256 columns, LDS-DMA X,
- * 3 = as 2 with 128 columns, 4 = as 2 with at most 144 rows per workgroup (row blocks of a
+ * 3 = as 2 with 128 columns (gated: 4 waves, 64 features per workgroup, two workgroups per
+ * CU; N a multiple of 128), 4 = as 2 with at most 144 rows per workgroup (row blocks of a
  * column tile paired on one XCD); 5-7 = the thin form for M <= 80 (no K split: every wave
  * of a workgroup streams its own K slice into registers, no barrier until the final fold;
  * 5: 16 features x 8 waves, 6: 32 x 8, 7: 16 x 16).  N a multiple of 128, K of 64 * splits;
