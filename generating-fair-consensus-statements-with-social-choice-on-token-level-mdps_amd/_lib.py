@@ -27,9 +27,9 @@ EXPORTED = (
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
-    "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits", "cs_gemm_bf16_streamk",
-    "cs_gemm_bf16_packed", "cs_gemm_pack", "cs_prefetch", "cs_rope_place_splitk",
-    "cs_gemm_streamk_workspace_size", "cs_add_rms_norm_splitk",
+    "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits",
+    "cs_gemm_bf16_packed", "cs_gemm_pack", "cs_rope_place_splitk",
+    "cs_add_rms_norm_splitk",
 )
 
 
@@ -136,19 +136,10 @@ def load():
     L.cs_gemm_bf16_packed.restype = ctypes.c_int
     L.cs_gemm_pack.argtypes = [vp, i64, i64, i64, vp, vp]
     L.cs_gemm_pack.restype = ctypes.c_int
-    L.cs_prefetch.argtypes = [vp, i64, ctypes.c_int32, vp]
-    L.cs_prefetch.restype = ctypes.c_int
     i32 = ctypes.c_int32
     L.cs_rope_place_splitk.argtypes = [vp, i32, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp,
                                        vp, vp, i64, vp]
     L.cs_rope_place_splitk.restype = ctypes.c_int
-    L.cs_gemm_bf16_streamk.argtypes = [vp, i64, vp, i64, vp, i64, i64, i64, i64, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, ctypes.c_int32, vp,
-                                       ctypes.c_size_t, vp]
-    L.cs_gemm_bf16_streamk.restype = ctypes.c_int
-    L.cs_gemm_streamk_workspace_size.argtypes = [i64, i64, i64, ctypes.c_int, ctypes.c_int,
-                                                 ctypes.c_int32]
-    L.cs_gemm_streamk_workspace_size.restype = ctypes.c_size_t
     _lib = L
     return L
 

@@ -575,142 +575,6 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 4 ? 2 : 1) void ws2_gemm_kerne
   ws2_store<MT, NT, GATED, WAVES>(acc, Y, ldy, P, M, n_out, nt, m0, sp, act);
 }
 
-// buffer resource over the hand-off slots (raw, 32-bit byte offsets; word 3 as for gfx9)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-}
-constexpr int kCpolSc1 = 16;   // cache-policy bit sc1 (write-through store / L2-served load)
-
-constexpr uint64_t kSkSpinNs = 2000000;   // 2 ms: a piece's producer that is not resident
-
-// sk_gemm_kernel: ws2_gemm_kernel's tiles (column tile x row block) with their K steps
-// divided evenly over the grid (stream-K, one workgroup per CU): workgroup b takes the
-// units [U b / G, U (b + 1) / G) of the U = tiles x nk (tile, K step) units, tile-major, so
-// every CU has the same number of K steps -- no second, partly idle round of tiles (C5's
-// gate|up: 448 tiles of 256 columns x 272 rows on 256 CUs was 1.75 rounds).  A tile cut by
-// a workgroup boundary is finished by its HEAD piece's workgroup (the one holding K step 0,
-// which reaches the tile last, at the end of its range): every later piece's workgroup
-// (which starts its range with it) hands its fp32 accumulators over (16-byte sc1 stores in
-// the lanes' own register order, vmcnt(0), barrier, one sc1 flag: the hand-off table's row
-// 1), and the head adds them in piece order to its own -- a fixed order, so the result does
-// not depend on timing.  A head that finds a piece missing after kSkSpinNs computes it
-// itself (identical values), so the launch finishes even when the grid is not resident.
-// Workspace: flags [G] (zeroed before the launch) + slots [2 G][MT NT 4 64 WAVES] floats
-// (slot b: workgroup b's piece; slot G + b: its head accumulators while it computes a
-// missing piece).
-template <int MT, int NT, int GATED, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 1) void sk_gemm_kernel(
-    const uint16_t* __restrict__ X, int64_t ldx, const uint16_t* __restrict__ W, int64_t ldw,
-    uint16_t* __restrict__ Y, int64_t ldy, int64_t M, int64_t n_out, int64_t gate_off, int nk,
-    int n_tiles, int units, uint32_t* __restrict__ flags, float* __restrict__ slots,
-    int act) {
-  using S = Ws2Shape<MT, NT, WAVES>;
-  __shared__ __align__(16) unsigned char lds[S::kLds];
-  __shared__ int sm_ready;
-  constexpr int64_t kSlot = static_cast<int64_t>(MT) * NT * 4 * 64 * WAVES;
-  const int G = static_cast<int>(gridDim.x);
-  const int bid = blockIdx.x;
-  const int tid = threadIdx.x;
-  // unit bounds are uniform: 32-bit scalar arithmetic (units < 2^31 / G, checked on the
-  // host), read into SGPRs so none of it holds a VGPR across the pipeline
-  auto ustart = [&](int b) -> int {
-    return __builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<int64_t>(units) * b / G));
-  };
-  // slot s, element (i, j) of lane tid at byte s * kSlot * 4 + (i NT + j) 4 KB * WAVES / 2 +
-  // tid * 16: the lanes' own register order, one coalesced 16-byte sc1 access per (i, j)
-  // (buffer form: the per-(i, j) offset is a scalar, so no address is held in registers)
-  const __amdgpu_buffer_rsrc_t rs = sk_rsrc(slots);
-  const int voff = tid * 16;
-  auto soff = [&](int64_t s, int i, int j) {
-    return static_cast<int>(s * kSlot * 4 + (i * NT + j) * (4 * 64 * WAVES * 4));
-  };
-  auto save = [&](const gf32x4 (&a)[MT][NT], int64_t s) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(a[i][j], rs, voff, soff(s, i, j), kCpolSc1);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every byte past the L2 before the flag
-  };
-  // a += slot s (ADD) or a = slot s
-  auto load = [&](gf32x4 (&a)[MT][NT], int64_t s, auto add_c) {
-    constexpr bool ADD = decltype(add_c)::value;
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const gf32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff(s, i, j), kCpolSc1);
-        if constexpr (ADD) a[i][j] += v;
-        else a[i][j] = v;
-      }
-      // a few row tiles' loads in flight, not all MT * NT (their registers would spill)
-      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  constexpr std::true_type kAdd{};
-  constexpr std::false_type kSet{};
-  int u = ustart(bid);
-  const int u1 = ustart(bid + 1);
-  bool first = true;
-  while (u < u1) {
-    const int tile = __builtin_amdgcn_readfirstlane(u / nk);
-    const int k0 = u - tile * nk;
-    const int len = min(nk - k0, u1 - u);
-    // tiles row-block-major: with G a multiple of 16, workgroups b and b + G / m_blocks
-    // (the same XCD) take the same column tile's K range of two row blocks at about the
-    // same time, so W is read from HBM once and from that XCD's L2 the second time
-    const int mb = __builtin_amdgcn_readfirstlane(tile / n_tiles);
-    const int nt = tile - mb * n_tiles;
-    const int m0 = mb * S::kRows;
-    if (!first) __syncthreads();     // every wave is done with the previous segment's LDS
-    first = false;
-    gf32x4 acc[MT][NT];
-    ws2_accumulate<MT, NT, GATED, WAVES>(lds, X, ldx, W, ldw, M, gate_off, nt, m0,
-                                         static_cast<int64_t>(k0) * kGemmBK, len, acc);
-    if (k0 > 0) {                    // a later piece: hand it to the tile's head
-      save(acc, bid);
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (len < nk) {                // the head of a cut tile: add the later pieces in order
-        const int tile_end = (tile + 1) * nk;
-        for (int b = bid + 1; b < G && ustart(b) < tile_end; ++b) {
-          if (tid == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-            int ok = 0;
-            for (;;) {
-              if (__hip_atomic_load(flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 1; break; }
-              if ((__builtin_amdgcn_s_memrealtime() - t0) * 10 > kSkSpinNs) break;
-              __builtin_amdgcn_s_sleep(2);
-            }
-            sm_ready = ok;
-          }
-          __syncthreads();
-#ifndef CS_SK_FALLBACK
-#define CS_SK_FALLBACK 1
-#endif
-          if (CS_SK_FALLBACK && !sm_ready) {   // block-uniform: compute piece b here (same values)
-            save(acc, G + bid);      // the running sum waits in this block's slot
-            __syncthreads();
-            const int pb = ustart(b);
-            const int plen = min(tile_end, ustart(b + 1)) - pb;
-            ws2_accumulate<MT, NT, GATED, WAVES>(lds, X, ldx, W, ldw, M, gate_off, nt, m0,
-                                                 static_cast<int64_t>(pb - tile * nk) * kGemmBK, plen,
-                                                 acc);
-            save(acc, b);
-            __syncthreads();
-            load(acc, G + bid, kSet);
-          }
-          load(acc, b, kAdd);
-        }
-      }
-      ws2_store<MT, NT, GATED, WAVES>(acc, Y, ldy, nullptr, M, n_out, nt, m0, 0, act);
-    }
-    u += len;
-  }
-}
-
 // Y[m][n] = bf16(sum_s P[s][m][n]) in split order; 8 outputs per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splits,
                                                             int64_t M, int64_t N,
@@ -966,32 +830,6 @@ void dispatch_ws2(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t
 #undef CS_WS2_CASE
 }
 
-template <int MT, int NT, int GATED>
-void launch_sk(int blocks, hipStream_t st, const uint16_t* X, int64_t ldx, const uint16_t* W,
-               int64_t ldw, uint16_t* Y, int64_t ldy, int64_t M, int64_t n_out, int64_t gate_off,
-               int nk, int n_tiles, int units, uint32_t* flags, float* slots, int act) {
-  hipLaunchKernelGGL((sk_gemm_kernel<MT, NT, GATED, 8>), dim3(blocks), dim3(512), 0, st, X, ldx, W,
-                     ldw, Y, ldy, M, n_out, gate_off, nk, n_tiles, units, flags, slots, act);
-}
-
-template <int NT, int GATED>
-void dispatch_sk(int mt, int blocks, hipStream_t st, const uint16_t* X, int64_t ldx,
-                 const uint16_t* W, int64_t ldw, uint16_t* Y, int64_t ldy, int64_t M, int64_t n_out,
-                 int64_t gate_off, int nk, int n_tiles, int units, uint32_t* flags,
-                 float* slots, int act) {
-#define CS_SK_CASE(V)                                                                            \
-  case V:                                                                                        \
-    launch_sk<V, NT, GATED>(blocks, st, X, ldx, W, ldw, Y, ldy, M, n_out, gate_off, nk, n_tiles,  \
-                            units, flags, slots, act);                                           \
-    break;
-  switch (mt) {
-    CS_SK_CASE(2) CS_SK_CASE(4) CS_SK_CASE(8) CS_SK_CASE(9) CS_SK_CASE(12) CS_SK_CASE(17)
-    CS_SK_CASE(18)
-    default: break;
-  }
-#undef CS_SK_CASE
-}
-
 // W rows per workgroup of a variant (1: ws 128; 2: ws2 8 waves x 32; 3: ws2 8 x 16, gated
 // 4 x 32; 4: as 2 with at most 9 row tiles (144 rows) per workgroup)
 int64_t variant_bn(int variant, int gated) {
@@ -1173,27 +1011,6 @@ int gemm_impl(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, i
   return check_launch("cs_gemm_bf16");
 }
 
-// Reads [p, p + bytes) once with 16-byte loads (default cache policy, so the lines land in
-// the Infinity Cache) and keeps nothing: run on a side stream while the step's attention /
-// norm launches leave HBM idle, it turns the next GEMM's weight stream into cache hits.
-// `sink` is written only when `keep` is set (never in use), so the loads cannot be dropped.
-__global__ __launch_bounds__(256) void prefetch_kernel(const gu32x4* __restrict__ p, int64_t n_vec,
-                                                       uint32_t* __restrict__ sink, int keep) {
-  uint32_t acc = 0;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256 * 4;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 * 4 + threadIdx.x; i < n_vec; i += stride) {
-    gu32x4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t j = i + u * 256;
-      v[u] = j < n_vec ? p[j] : gu32x4{0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
-  }
-  if (keep) sink[static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x] = acc;
-}
-
 // Wp[((T * ns + s) * 2 + h) * 512 + 8 l + e] = W[16 T + l % 16][64 s + 32 h + 8 (l / 16) + e]
 __global__ __launch_bounds__(256) void gemm_pack_kernel(const uint16_t* __restrict__ W, int64_t ldw,
                                                         int64_t n_vec, int64_t ns,
@@ -1227,18 +1044,6 @@ int cs_gemm_bf16_packed(const void* x, int64_t ldx, const void* w_packed, void* 
                    stream, true);
 }
 
-int cs_prefetch(const void* p, int64_t bytes, int32_t blocks, cs_stream_t stream) {
-  if (bytes < 0 || blocks < 0) return fail(CS_ERR_INVALID, "cs_prefetch: negative size");
-  if (bytes == 0) return CS_OK;
-  if (!p || reinterpret_cast<uintptr_t>(p) & 15 || bytes % 16)
-    return fail(CS_ERR_INVALID, "cs_prefetch: p must be 16-byte aligned, bytes a multiple of 16");
-  if (blocks == 0) blocks = 256;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const gu32x4*>(p), bytes / 16,
-                     nullptr, 0);
-  return check_launch("cs_prefetch");
-}
-
 int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packed,
                  cs_stream_t stream) {
   if (!w || !w_packed) return fail(CS_ERR_INVALID, "cs_gemm_pack: NULL pointer");
@@ -1251,95 +1056,6 @@ int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packe
                      static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(w), ldw, n_vec,
                      K / kGemmBK, static_cast<uint16_t*>(w_packed));
   return check_launch("cs_gemm_pack");
-}
-
-}  // extern "C"
-
-namespace {
-struct SkPlan {
-  int variant, mt, blocks;
-  int64_t mb, n_tiles, units, slot_floats;
-  size_t flags_bytes, total;
-};
-int n_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    n = (hipGetDevice(&dev) == hipSuccess &&
-         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-            ? v : 256;
-  }
-  return n;
-}
-SkPlan sk_plan(int64_t M, int64_t N, int64_t K, int gated, int variant, int32_t blocks) {
-  SkPlan p{};
-  p.variant = resolve_variant(variant, N, gated);
-  if (p.variant == 1) p.variant = gated ? 2 : 3;     // the stream-K form is ws2's
-  if (gated && p.variant == 3) p.variant = 2;         // (8 waves: no 4-wave gated form)
-  ws2_rows(M, &p.mt, &p.mb, variant_max_tiles(p.variant));
-  p.n_tiles = N / variant_bn(p.variant, gated);
-  p.units = p.n_tiles * p.mb * (K / kGemmBK);
-  int64_t b = blocks > 0 ? blocks : n_cus();
-  if (b > p.units) b = p.units;
-  p.blocks = static_cast<int>(b < 1 ? 1 : b);
-  const int nt = (p.variant == 3 && !gated) ? 1 : 2;
-  p.slot_floats = static_cast<int64_t>(p.mt) * nt * 4 * 64 * 8;
-  p.flags_bytes = (static_cast<size_t>(p.blocks) * sizeof(uint32_t) + 255) / 256 * 256;
-  p.total = p.flags_bytes + sizeof(float) * static_cast<size_t>(2 * p.blocks) * p.slot_floats;
-  return p;
-}
-}  // namespace
-
-extern "C" {
-
-size_t cs_gemm_streamk_workspace_size(int64_t M, int64_t N, int64_t K, int gated, int variant,
-                                      int32_t blocks) {
-  if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % kGemmBK || variant < 0 || variant > 4) return 0;
-  return sk_plan(M, N, K, gated, variant, blocks).total;
-}
-
-int cs_gemm_bf16_streamk(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y,
-                         int64_t ldy, int64_t M, int64_t N, int64_t K, int gated, int act,
-                         int variant, int32_t blocks, void* workspace, size_t workspace_bytes,
-                         cs_stream_t stream) {
-  const char* e = "cs_gemm_bf16_streamk: ";
-  if (M < 0 || N <= 0 || K <= 0) return fail(CS_ERR_INVALID, std::string(e) + "bad shape");
-  if (M == 0) return CS_OK;
-  if (!x || !w || !y) return fail(CS_ERR_INVALID, std::string(e) + "NULL pointer");
-  if (variant < 0 || variant > 4) return fail(CS_ERR_INVALID, std::string(e) + "variant must be 0..4");
-  if (N % 128 || K % kGemmBK)
-    return fail(CS_ERR_INVALID, std::string(e) + "N must be a multiple of 128 and K of 64");
-  if (ldx % 8 || ldw % 8 || ldy % 4 || ldy < (gated ? N / 2 : N) || ldx < K || ldw < K)
-    return fail(CS_ERR_INVALID, std::string(e) + "leading dimensions too small or misaligned");
-  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15 ||
-      reinterpret_cast<uintptr_t>(y) & 7)
-    return fail(CS_ERR_INVALID, std::string(e) + "operands must be 16-byte aligned (y 8-byte)");
-  const SkPlan p = sk_plan(M, N, K, gated, variant, blocks);
-  if (p.units * p.blocks >= (int64_t{1} << 31))
-    return fail(CS_ERR_INVALID, std::string(e) + "too many (tile, K step) units");
-  if (!workspace || workspace_bytes < p.total || reinterpret_cast<uintptr_t>(workspace) & 255)
-    return fail(CS_ERR_WORKSPACE, std::string(e) + "workspace smaller than "
-                "cs_gemm_streamk_workspace_size() or not 256-byte aligned");
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  auto* flags = static_cast<uint32_t*>(workspace);
-  auto* slots = reinterpret_cast<float*>(static_cast<char*>(workspace) + p.flags_bytes);
-  if (hipMemsetAsync(flags, 0, p.flags_bytes, st) != hipSuccess)
-    return fail(CS_ERR_HIP, std::string(e) + "clearing the hand-off flags failed");
-  const uint16_t* X = static_cast<const uint16_t*>(x);
-  const uint16_t* Wp = static_cast<const uint16_t*>(w);
-  uint16_t* Y = static_cast<uint16_t*>(y);
-  const int nk = static_cast<int>(K / kGemmBK);
-  const int nti = static_cast<int>(p.n_tiles);
-  if (gated)
-    dispatch_sk<2, 1>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N / 2, N / 2, nk, nti,
-                      static_cast<int>(p.units), flags, slots, act);
-  else if (p.variant == 3)
-    dispatch_sk<1, 0>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N, 0, nk, nti,
-                      static_cast<int>(p.units), flags, slots, 0);
-  else
-    dispatch_sk<2, 0>(p.mt, p.blocks, st, X, ldx, Wp, ldw, Y, ldy, M, N, 0, nk, nti,
-                      static_cast<int>(p.units), flags, slots, 0);
-  return check_launch("cs_gemm_bf16_streamk");
 }
 
 }  // extern "C"

@@ -845,23 +845,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = 
     return x @ w.t()
 
 
-_SK_WS: Dict[torch.device, torch.Tensor] = {}
-
-
-def _sk_workspace(device, nbytes: int) -> int:
-    """A 256-byte aligned device address with nbytes behind it for cs_gemm_bf16_streamk: one
-    buffer per device, sized up front for the largest tile shape at one workgroup per CU
-    (2 x CUs slots of 18 x 2 x 4 x 512 floats + flags, ~151 MB), grown only by a larger
-    request (e.g. an explicit sk_blocks above the CU count)."""
-    t = _SK_WS.get(device)
-    if t is None or t.numel() < nbytes + 256:
-        n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-        need = max(nbytes, 2 * n_cu * 18 * 2 * 4 * 512 * 4 + 65536) + 256
-        t = _SK_WS[device] = torch.empty(need, dtype=torch.uint8, device=device)
-    base = t.data_ptr()
-    return base + (-base) % 256
-
-
 def gemm_ok(x: torch.Tensor, w: torch.Tensor, gated: bool = False) -> bool:
     """Whether cs_gemm_bf16 takes y = x @ w.T: bf16 2-D operands with unit column stride,
     N a multiple of 128, K of 64, 16-byte aligned rows."""
@@ -876,12 +859,10 @@ def gemm_ok(x: torch.Tensor, w: torch.Tensor, gated: bool = False) -> bool:
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "silu",
-         splits: int = 0, variant: int = 0, out: Optional[torch.Tensor] = None,
-         sk_blocks: int = 0) -> torch.Tensor:
+         splits: int = 0, variant: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w.T (cs_gemm_bf16): x [M, K], w [N, K] bf16, y [M, N] bf16, fp32 accumulation.
     gated: w is the fused gate|up weight [2F, K] and y [M, F] = act(gate) * up (the rounding
-    of cs_gated_act).  splits = -1: stream-K (cs_gemm_bf16_streamk over sk_blocks workgroups,
-    0 = one per CU).  splits: K split (0 = the library's choice); the fp32 partials are a
+    of cs_gated_act).  splits: K split (0 = the library's choice); the fp32 partials are a
     per-call tensor (inside a capture it belongs to the graph's pool)."""
     L = _lib.load()
     if not gemm_ok(x, w, gated):
@@ -894,22 +875,6 @@ def gemm(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = "s
     if out.shape != (M, n_out) or out.dtype != torch.bfloat16 or out.stride(1) != 1:
         raise CSError("out must be a bf16 [M, N] tensor with unit column stride")
     _require_cuda(x, w, out)
-    if splits < 0:
-        # stream-K (cs_gemm_bf16_streamk): the tiles' K steps spread evenly over the CUs;
-        # one workspace per device shared by every call (calls on one stream run one after
-        # another, and a captured step graph replays them in that order)
-        nbytes = int(L.cs_gemm_streamk_workspace_size(M, N, K, int(bool(gated)), variant,
-                                                      sk_blocks))
-        base = _sk_workspace(x.device, nbytes)
-        ldx = x.stride(0) if M > 1 else K
-        ldy = out.stride(0) if M > 1 else n_out
-        rc = L.cs_gemm_bf16_streamk(x.data_ptr(), ldx, w.data_ptr(), w.stride(0), out.data_ptr(),
-                                    ldy, M, N, K, int(bool(gated)),
-                                    {"silu": 0, "gelu_tanh": 1}[act], variant, sk_blocks, base,
-                                    nbytes,
-                                    _stream())
-        _lib.check(rc, "cs_gemm_bf16_streamk")
-        return out
     if gated:
         splits = 1
     elif splits <= 0:
@@ -954,16 +919,6 @@ def gemm_pack(w: torch.Tensor) -> PackedWeight:
     rc = L.cs_gemm_pack(w.data_ptr(), w.stride(0), N, K, out.data_ptr(), _stream())
     _lib.check(rc, "cs_gemm_pack")
     return PackedWeight(out, N, K)
-
-
-def prefetch(t: "torch.Tensor | PackedWeight", blocks: int = 0) -> None:
-    """Read a weight once on the current stream so it lands in the Infinity Cache
-    (cs_prefetch); meant for a side stream beside launches that leave HBM idle."""
-    L = _lib.load()
-    d = t.data if isinstance(t, PackedWeight) else t
-    _require_cuda(d)
-    rc = L.cs_prefetch(d.data_ptr(), d.numel() * d.element_size(), int(blocks), _stream())
-    _lib.check(rc, "cs_prefetch")
 
 
 def gemm_packed(x: torch.Tensor, pw: PackedWeight, *, gated: bool = False, act: str = "silu",

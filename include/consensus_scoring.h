@@ -471,43 +471,9 @@ int64_t cs_gemm_splits(int64_t M, int64_t N, int64_t K, int gated, int variant);
 int cs_gemm_pack(const void* w, int64_t ldw, int64_t N, int64_t K, void* w_packed,
                  cs_stream_t stream);
 
-/*
- * cs_prefetch — read [p, p + bytes) once (16-byte loads, default cache policy) over `blocks`
- * workgroups (0: 256) and discard it, so the bytes land in the Infinity Cache.  p 16-byte
- * aligned, bytes % 16 == 0.  An experiment aid (tools/prefetch_ab.py): a side-stream prefetch
- * of the next GEMM's weight beside a 30 us HBM-idle phase made the 8-rank decode GEMMs
- * slower, not faster (profiles/r04q_prefetch_ab.jsonl), so the decode step does not use it.
- *
- * Replaces: nothing in the reference (its forward is remote); a scheduling aid of the
- *   decode step's weight stream.
- */
-int cs_prefetch(const void* p, int64_t bytes, int32_t blocks, cs_stream_t stream);
 int cs_gemm_bf16_packed(const void* x, int64_t ldx, const void* w_packed, void* y, int64_t ldy,
                         int64_t M, int64_t N, int64_t K, int splits, int gated, int act,
                         int variant, float* workspace, cs_stream_t stream);
-
-/*
- * cs_gemm_bf16_streamk — cs_gemm_bf16 (variants 2-4, plain or gated; variant 1 maps to 3 /
- * 2) with the tiles' K steps divided evenly over `blocks` workgroups (stream-K; blocks <= 0:
- * one per CU): every CU gets the same number of K steps, with no partly idle last round of
- * tiles.  A tile cut by a workgroup boundary is finished by the workgroup holding its first
- * K step, which adds the later pieces' fp32 accumulators in piece order (a fixed order:
- * deterministic, and equal to cs_gemm_bf16 within fp32 reassociation).  workspace: at least
- * cs_gemm_streamk_workspace_size() bytes, 256-byte aligned (its hand-off flags are cleared
- * on `stream` by the call itself).  Same operand rules as cs_gemm_bf16 (y required).
- *
- * Replaces: the same projections of the remote forward as cs_gemm_bf16
- *   (src/utils.py:249-259).
- */
-int cs_gemm_bf16_streamk(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y,
-                         int64_t ldy, int64_t M, int64_t N, int64_t K, int gated, int act,
-                         int variant, int32_t blocks, void* workspace, size_t workspace_bytes,
-                         cs_stream_t stream);
-
-/* cs_gemm_streamk_workspace_size — bytes of workspace cs_gemm_bf16_streamk needs (0 on a
- * bad shape). */
-size_t cs_gemm_streamk_workspace_size(int64_t M, int64_t N, int64_t K, int gated, int variant,
-                                      int32_t blocks);
 
 #ifdef __cplusplus
 }

@@ -45,31 +45,65 @@ class Backend:
     """CPU fp32 transformers model + the product's char tokenizer."""
 
     def __init__(self, hf_model, tokenizer, softcap: float = 0.0,
-                 tail_positions: Optional[int] = None):
+                 tail_positions: Optional[int] = None, kv_cache: int = 0):
         """tail_positions: echo log-probs of the prompt's last tail_positions tokens only
         (NaN before them) -- the LM head over a few rows instead of the whole prompt, for
-        traces whose recorded calls keep only the span's tail (beam search sums [-1:])."""
+        traces whose recorded calls keep only the span's tail (beam search sums [-1:]).
+        kv_cache: keep the K/V of the last kv_cache prompts and run a new prompt's forward
+        from the longest cached token prefix (a causal prefix's K/V depend on that prefix
+        alone; the forward differs from a full one by fp32 summation order only) -- for
+        the wide-model fixtures whose thousands of calls share their long prompts."""
         self.tail = tail_positions
         self.m = hf_model.eval()
         self.tok = tokenizer
         self.softcap = softcap
         self.rng = np.random.default_rng(0)
         self.calls: List[Dict] = []
+        self.kv_cache = int(kv_cache)
+        self._kv: List = []          # [(ids tuple, DynamicCache)], most recent last
+
+    @torch.no_grad()
+    def _forward(self, ids: List[int], keep: int) -> torch.Tensor:
+        """logits of the last `keep` positions of `ids` ([keep, V] fp32)."""
+        if not self.kv_cache:
+            kw = {} if keep == len(ids) else {"logits_to_keep": keep}
+            return self.m(torch.tensor([ids]), **kw).logits[0]
+        import copy
+        from transformers import DynamicCache
+
+        best, blen = None, 0
+        for key, cache in self._kv:
+            n = 0
+            lim = min(len(key), len(ids))
+            while n < lim and key[n] == ids[n]:
+                n += 1
+            if n > blen:
+                best, blen = cache, n
+        blen = min(blen, len(ids) - keep)
+        if best is not None and blen > 0:
+            cache = copy.deepcopy(best)
+            cache.crop(blen)
+        else:
+            cache, blen = DynamicCache(), 0
+        out = self.m(torch.tensor([ids[blen:]]), past_key_values=cache, use_cache=True,
+                     logits_to_keep=keep)
+        self._kv.append((tuple(ids), out.past_key_values))
+        if len(self._kv) > self.kv_cache:
+            self._kv.pop(0)
+        return out.logits[0]
 
     @torch.no_grad()
     def logits(self, ids: List[int], last_only: bool = False) -> np.ndarray:
         """fp32 logits as float64 (softcap applied by HF); last_only: the last position's
         row alone (the LM head over one position instead of the whole prompt)."""
-        kw = {"logits_to_keep": 1} if last_only else {}
-        return self.m(torch.tensor([ids]), **kw).logits[0].double().numpy()
+        return self._forward(ids, 1 if last_only else len(ids)).double().numpy()
 
     @torch.no_grad()
     def prompt_logprobs(self, ids: List[int]) -> List[Optional[float]]:
         """log_softmax(logits)[i, ids[i + 1]] in float64 for every prompt position."""
         P = len(ids)
         K = P if self.tail is None else min(P, int(self.tail) + 1)
-        kw = {} if K == P else {"logits_to_keep": K}
-        lg = self.m(torch.tensor([ids]), **kw).logits[0].double()      # positions P-K .. P-1
+        lg = self._forward(ids, K).double()                              # positions P-K .. P-1
         nxt = torch.tensor(ids[P - K + 1:], dtype=torch.long)
         ls = lg[:-1].gather(1, nxt[:, None])[:, 0] - torch.logsumexp(lg[:-1], dim=1)
         return [None] + [float("nan")] * (P - K) + [float(v) for v in ls.tolist()]

@@ -59,7 +59,12 @@ FAMILIES = {"llama3": ("tiny-llama-fixture", "method_traces.json"),
             "fl4": ("llama-3.2-1b-shaped-fixture", "method_traces_fl4.json"),
             # Gemma-2's real head shape (C3: head_dim 256, query_pre_attn_scalar 256) with
             # both soft-caps and the fixture's 8-token sliding window, 16 agents
-            "gemma256": ("tiny-gemma-d256-fixture", "method_traces_gemma256.json")}
+            "gemma256": ("tiny-gemma-d256-fixture", "method_traces_gemma256.json"),
+            # the reference's main-body experiment (configs/main_body/scenario_1.yaml: 5
+            # agents, Best-of-N n 4 x 200 tokens, lookahead bf 2 / depth 4, beam 4) on a
+            # Llama-3.1-8B-shaped fixture: widths 4096 / 14336, 32 / 8 heads of 128, the
+            # Llama-3.1 RoPE frequency scaling, vocabulary 128,256; 2 of its 32 layers
+            "main128": ("llama-3.1-8b-shaped-fixture", "method_traces_main128.json.gz")}
 BPE_DIR = os.path.join(HERE, "bpe_fixture")
 # untied LM head: with the random tied embedding a shallow model's residual stream makes
 # the last token's own logit ~45 sigma above the rest (every draw repeats it); an
@@ -69,6 +74,7 @@ C1_OVERRIDES = {"n_layers": 2, "tie_embeddings": False}
 # dims 64 / 128 / 256), so the same trace also pins the bf16 stream-decode path
 WIDE_OVERRIDES = {"head_dim": 64, "query_pre_attn_scalar": 64.0}
 GEMMA256_OVERRIDES = {"head_dim": 256, "query_pre_attn_scalar": 256.0}
+MAIN128_OVERRIDES = {"n_layers": 2}
 
 
 def fixture_model(family: str = "llama3"):
@@ -77,6 +83,9 @@ def fixture_model(family: str = "llama3"):
     T = importlib.import_module(PKG + ".tokenizer")
     if family in ("c1", "c1long", "fl4"):
         cfg = Mm.preset("llama-3.2-1b", **C1_OVERRIDES)
+        tok = T.CharTokenizer("llama3", vocab_size=cfg.vocab)
+    elif family == "main128":
+        cfg = Mm.preset("llama-3.1-8b", **MAIN128_OVERRIDES)
         tok = T.CharTokenizer("llama3", vocab_size=cfg.vocab)
     elif family == "bpe":
         tok = T.BPETokenizer(BPE_DIR, family="llama3")
@@ -125,6 +134,24 @@ GEMMA256_RUNS = [
 ]
 
 
+# configs/main_body/scenario_1.yaml:36-59 (api_delay 0, brushup off, seeds the fixture's):
+# Best-of-N at its full 200 tokens, lookahead at bf 2 / depth 4 over 8 committed tokens,
+# beam 4 (10 sampling attempts) over 100 of its 200 tokens
+MAIN128_RUNS = [
+    ("best_of_n", {"n": 4, "max_tokens": 200, "seed": 42, "temperature": 1.0, "api_delay": 0,
+                   "log_level": "WARNING"}),
+    ("finite_lookahead", {"branching_factor": 2, "max_depth": 4, "max_tokens": 8, "seed": 42,
+                          "api_delay": 0, "log_level": "WARNING"}),
+    ("beam_search", {"beam_width": 4, "max_tokens": 100, "max_sampling_attempts": 10, "seed": 42,
+                     "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
+]
+# echo log-probs of the prompt tail only (the LM head over these rows): beam search keeps
+# the last one (beam_search.py:389-390), the lookahead the path's last <= 4
+# (finite_lookahead.py:508-520); Best-of-N / the evaluator need the user span (a <= 200-token
+# statement + the chat frame's closing tokens)
+MAIN128_TAIL = {"beam_search": 8, "best_of_n": 320, "finite_lookahead": 16, "eval": 320}
+
+
 WIDE_AGENTS = 16
 WIDE_RUNS = [
     ("beam_search", {"beam_width": 8, "max_tokens": 3, "max_sampling_attempts": 8, "seed": 21,
@@ -146,6 +173,20 @@ BPE_RUNS = [
     ("finite_lookahead", {"branching_factor": 2, "max_depth": 2, "max_tokens": 4, "seed": 11,
                           "api_delay": 0, "log_level": "WARNING"}),
 ]
+
+
+def write_traces(name: str, out) -> None:
+    """JSON (gzip-compressed for *.gz: the thousands of recorded calls of the wide traces
+    repeat the same prompts)."""
+    path = os.path.join(HERE, name)
+    if name.endswith(".gz"):
+        import gzip
+        with gzip.open(path, "wt") as f:
+            json.dump(out, f)
+    else:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    print("wrote", name)
 
 
 def install(reference: str, backend) -> None:
@@ -176,10 +217,12 @@ def main() -> None:
     cfg, model, tok = fixture_model(args.family)
     # c1long: beam search only, whose calls are recorded by their last 6 span log-probs
     backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok,
-                                    tail_positions=32 if args.family == "c1long" else None)
+                                    tail_positions=32 if args.family == "c1long" else None,
+                                    kv_cache=8 if args.family == "main128" else 0)
     install(args.reference, backend)
-    scen = yaml.safe_load(open(os.path.join(args.reference, "configs", "appendix", "llama",
-                                            "scenario_1", "beam_search.yaml")))["scenario"]
+    scen_path = (("configs", "main_body", "scenario_1.yaml") if args.family == "main128" else
+                 ("configs", "appendix", "llama", "scenario_1", "beam_search.yaml"))
+    scen = yaml.safe_load(open(os.path.join(args.reference, *scen_path)))["scenario"]
     issue, opinions = scen["issue"], dict(scen["agent_opinions"])
     if args.family in ("wide", "gemma256"):
         texts = list(opinions.values())
@@ -208,11 +251,14 @@ def main() -> None:
         mod.get_prompt_logprobs = recorder(mod.get_prompt_logprobs)
 
     out = {"model_id": MODEL_ID, "weight_seed": WEIGHT_SEED, "preset": cfg.name,
-           "family": ("llama3" if args.family in ("c1", "c1long", "fl4", "bpe")
+           "family": ("llama3" if args.family in ("c1", "c1long", "fl4", "bpe", "main128")
                       else "gemma2" if args.family in ("wide", "gemma256") else args.family),
            "vocab": cfg.vocab, "issue": issue, "agent_opinions": opinions, "runs": []}
     if args.family in ("c1", "c1long", "fl4"):
         out["preset_overrides"] = dict(C1_OVERRIDES)
+        out["tokenizer_vocab"] = cfg.vocab
+    if args.family == "main128":
+        out["preset_overrides"] = dict(MAIN128_OVERRIDES)
         out["tokenizer_vocab"] = cfg.vocab
     if args.family == "bpe":
         out["tokenizer"] = "bpe_fixture"
@@ -222,6 +268,7 @@ def main() -> None:
         out["preset_overrides"] = dict(GEMMA256_OVERRIDES)
     runs = (C1_RUNS if args.family == "c1" else C1_LONG_RUNS if args.family == "c1long"
             else FL4_RUNS if args.family == "fl4"
+            else MAIN128_RUNS if args.family == "main128"
             else GEMMA256_RUNS if args.family == "gemma256"
             else BPE_RUNS if args.family == "bpe"
             else WIDE_RUNS if args.family == "wide" else None) or [
@@ -242,6 +289,8 @@ def main() -> None:
     ]
     for method, mcfg in runs:
         calls.clear()
+        if args.family == "main128":
+            backend.tail = MAIN128_TAIL[method]
         gen = get_method_generator(method, dict(mcfg), MODEL_ID)
         extra = {}
         if method == "best_of_n":
@@ -262,7 +311,7 @@ def main() -> None:
 
             gen._calculate_candidate_rewards = rec_rewards
             gen._calculate_egalitarian_welfare = rec_welfare
-        if method == "finite_lookahead" and args.family in ("fl4", "gemma256"):
+        if method == "finite_lookahead" and args.family in ("fl4", "gemma256", "main128"):
             # the reference's tree of every step and every one-token draw, so the bf16 replay
             # can teacher-force the tree (its draws from bf16 logits could flip near-ties of
             # the Gumbel argmax): each draw keyed by (statement + path so far, seed) -- the
@@ -317,13 +366,13 @@ def main() -> None:
         import math
         assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
                    if v is not None), "a recorded tail reaches past the computed positions"
-        with open(os.path.join(HERE, out_name), "w") as f:
-            json.dump(out, f, indent=1)
-        print("wrote", out_name)
+        write_traces(out_name, out)
         return
 
     # post-hoc evaluation (src/evaluation.py:128-634) on fixed statements
     from src.evaluation import StatementEvaluator  # noqa: E402
+    if args.family == "main128":
+        backend.tail = MAIN128_TAIL["eval"]
     ev = StatementEvaluator(MODEL_ID, include_comparative_ranking=False, verbose=False)
     stmts = [out["runs"][0]["statement"],
              "Genetic information should stay private unless the person consents to research.",
@@ -335,6 +384,12 @@ def main() -> None:
                 if k != "statement_embedding" and not isinstance(v, str)}
         out["evaluations"].append({"statement": s, "result": keep})
 
+    if args.family == "main128":
+        import math
+        assert all(v is None or math.isfinite(v) for e in out["evaluations"]
+                   for v in e["result"].values()), "an evaluation reaches past the tail"
+        backend.tail = None
+
     # text-compat scoring primitive (src/utils.py:201-373), incl. marker cases
     out["prompt_logprobs"] = []
     for system, user in [("You are a judge.", "The statement is fair."),
@@ -345,9 +400,7 @@ def main() -> None:
         toks, lps = rutils.get_prompt_logprobs(MODEL_ID, system, user)
         out["prompt_logprobs"].append({"system": system, "user": user, "tokens": toks,
                                        "logprobs": lps})
-    with open(os.path.join(HERE, out_name), "w") as f:
-        json.dump(out, f, indent=1)
-    print("wrote", out_name)
+    write_traces(out_name, out)
 
 
 if __name__ == "__main__":

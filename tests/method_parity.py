@@ -46,7 +46,12 @@ GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json",
 
 
 def load_traces(name: str = "method_traces.json"):
-    with open(os.path.join(HERE, "golden", name)) as f:
+    path = os.path.join(HERE, "golden", name)
+    if name.endswith(".gz"):
+        import gzip
+        with gzip.open(path, "rt") as f:
+            return json.load(f)
+    with open(path) as f:
         return json.load(f)
 
 

@@ -92,8 +92,8 @@ def test_invalid_welfare_and_topk(pkg):
 
 
 def test_round4_entry_points_validate_before_launching(pkg):
-    """The packed-weight GEMM, the thin variants, the split-K RoPE fold and the prefetch
-    reject bad arguments with a status code (no device needed: checked before any launch)."""
+    """The packed-weight GEMM, the thin variants and the split-K RoPE fold reject bad
+    arguments with a status code (no device needed: checked before any launch)."""
     from importlib import import_module
     L = import_module(pkg.__name__ + "._lib").load()
     d = ctypes.c_void_p(256)
@@ -113,10 +113,6 @@ def test_round4_entry_points_validate_before_launching(pkg):
     assert L.cs_rope_place_splitk(d, 2, d, d, None, 1, d, 1, 32, 4, 2, 64, d, d, d, 64, None) == -1
     assert L.cs_rope_place_splitk(d, 2, d, d, None, 1, d, 1, 1, 4, 2, 40, d, d, d, 32, None) == -1
     assert L.cs_rope_place_splitk(None, 2, d, d, None, 1, d, 1, 1, 4, 2, 64, d, d, d, 32, None) == -1
-    # cs_prefetch: alignment and size
-    assert L.cs_prefetch(odd, 64, 1, None) == -1
-    assert L.cs_prefetch(d, 24, 1, None) == -1
-    assert L.cs_prefetch(d, 0, 1, None) == 0
     assert L.cs_last_error().decode()
 
 

@@ -89,9 +89,6 @@ def main() -> int:
                     help="1: keep the installed table's entries for shapes this run does not measure")
     ap.add_argument("--variants", default="2,3,4,5,6,7")
     ap.add_argument("--gemms", default="", help="only these shapes (e.g. qkv,down)")
-    ap.add_argument("--sk", type=int, default=0,
-                    help="1: also time the stream-K form (splits = -1, cs_gemm_bf16_streamk; "
-                         "slower than the split-K form on every C5 shape in r04d)")
     args = ap.parse_args()
     print("tuning:", R.use_gemm_tuning(), file=sys.stderr)
     dev = torch.device("cuda:0")
@@ -126,11 +123,10 @@ def main() -> int:
                 for var in map(int, args.variants.split(",")):
                     if var >= 5 and M > 80:
                         continue                 # the thin form takes at most 80 rows
-                    for sp in ((1,) if gated or var >= 5 else (1, 2, 4, 8, 16)) + \
-                            ((-1,) if args.sk and var < 5 else ()):
+                    for sp in ((1,) if gated or var >= 5 else (1, 2, 4, 8, 16)):
                         if var in (2, 4) and N % 256:
                             continue
-                        if sp > 0 and (K % (64 * sp) or K // (64 * sp) < 2):
+                        if (K % (64 * sp) or K // (64 * sp) < 2):
                             continue
                         if sp > 1 and name in FOLDED_BY_CONSUMER:
                             t = timed(lambda: [ops.gemm_partials(x, ws[i % nw], splits=sp,
