@@ -156,6 +156,14 @@ BEAM_CONFIGS = {
     "c5": (64, 8, 32, 128_256, 0.0, torch.bfloat16,
            "C5 beam search: B=8 beams x top-32 x A=64 agents sharded over the ranks, "
            "Llama-3.3-70B vocab 128256 bf16 logits, egalitarian welfare, RCCL MIN all-reduce"),
+    # the decode launch at the shape ONE GPU of the 8-GPU C3 / C5 runs holds: its agents'
+    # rows (C3 16 / 8 = 2 agents, C5 64 / 8 = 8) beside the replicated proposer rows
+    "r8c3": (2, 16, 50, 256_000, 30.0, torch.bfloat16,
+             "C3 per GPU at 8 ranks: B=16 beams x top-50 x A=2 local agents (of 16), Gemma-2-9B "
+             "vocab 256000 bf16 logits (soft-cap 30), the launch one rank runs per step"),
+    "r8c5": (8, 8, 32, 128_256, 0.0, torch.bfloat16,
+             "C5 per GPU at 8 ranks: B=8 beams x top-32 x A=8 local agents (of 64), "
+             "Llama-3.3-70B vocab 128256 bf16 logits, the launch one rank runs per step"),
 }
 
 
@@ -178,7 +186,7 @@ def parse():
                     help="steps of a short statement timed with the re-tokenized text semantics")
     ap.add_argument("--method-statements", type=int, default=1,
                     help="timed generate_statement calls per method config")
-    ap.add_argument("--beam", default="c1,c3,c5",
+    ap.add_argument("--beam", default="c1,c3,c5,r8c3,r8c5",
                     help="kernel-level beam decode configs on resident logits ('' disables)")
     ap.add_argument("--beam-steps", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -807,7 +815,9 @@ def cpu_baseline(seconds, V=128_256, T=150):
     call at BASELINE C1's model (Llama-3.2-1B fp32, 200 + 10 tokens; C1 names "Llama-3.2-1B
     logprobs on CPU"), and the post-LM-head arithmetic on a C2 logits sample three ways: the
     fp64 C oracle, core.log_softmax_rows restated in NumPy fp64 (single thread), and
-    torch.log_softmax(x.float()).gather."""
+    torch.log_softmax(x.float()).gather.  BASELINE C3 (Gemma-2-9B fp32, one beam candidate
+    token per call) and C4 (Llama-3.1-8B, one 4-token lookahead path per call): the same
+    per-call restatement at their shapes (``c3_per_call``, ``c4_per_call``)."""
     M = importlib.import_module(PKG_DIR + ".model")
     cores = _host_cores()
     torch.set_num_threads(cores)
@@ -823,8 +833,32 @@ def cpu_baseline(seconds, V=128_256, T=150):
                      f"log-softmax over {V} + gather at the candidate's tokens, per (agent, "
                      f"candidate) as get_prompt_logprobs re-encodes every call; torch {cores} "
                      f"threads (model init {init_s:.1f} s, not timed)")
+    # (1b) BASELINE C4's scoring call on the same 8B model (Nash welfare over the same
+    # per-call utilities): an agent prompt + statement (200 tokens) + one 4-token lookahead
+    # path, the mean of the path's log-probs (finite_lookahead.py:490-520)
+    n, el = _per_call_scoring(model, 200, 4, seconds / 2)
+    out["c4_per_call"] = {
+        "value": n / el, "unit": "scorings/s",
+        "sample": f"{n} scorings in {el:.1f} s: Llama-3.1-8B fp32 (constant weights) forward of a "
+                  f"200-token agent prompt + statement and a 4-token lookahead path, log-softmax + "
+                  f"gather at the path's tokens, per (agent, path) as finite_lookahead.py:490-520 "
+                  f"calls get_prompt_logprobs; torch {cores} threads"}
     del model
     import gc
+    gc.collect()
+    # (1c) BASELINE C3's scoring call: Gemma-2-9B fp32, the agent prompt + a 50-token beam
+    # (260 tokens) + one candidate token, its last log-prob (beam_search.py:358-390)
+    t0 = time.perf_counter()
+    model = _const_model(M, "gemma-2-9b")
+    init_s = time.perf_counter() - t0
+    n, el = _per_call_scoring(model, 260, 1, seconds / 2)
+    out["c3_per_call"] = {
+        "value": n / el, "unit": "scorings/s",
+        "sample": f"{n} scorings in {el:.1f} s: Gemma-2-9B fp32 (constant weights) forward of a "
+                  f"260-token agent prompt + beam and one candidate token, log-softmax over 256,000 + "
+                  f"the token's log-prob, per (agent, beam, token) as beam_search.py:358-390 calls "
+                  f"get_prompt_logprobs; torch {cores} threads (model init {init_s:.1f} s, not timed)"}
+    del model
     gc.collect()
     # (2) C1 config: 1B fp32, 200 + 10 tokens per call
     t0 = time.perf_counter()

@@ -599,6 +599,21 @@ void prefix_attn_lds_kernel(AttnParams a) {
   }
 }
 
+#ifdef CS_TRACE_ATTN
+// diagnostics build only (tools/attn_trace.py): wall_clock64 ticks (100 MHz) per workgroup of
+// the last decode-step launch, plain stores (no atomics: those serialise and distort):
+// attention [wg][0 start, 1 prologue loads in, 2 prefix loop done, 3 history loop done
+// (wave 0), 4 partial stored (wave 0)], merge [wg][5 start, 6 done]
+constexpr int kAttTraceWgs = 4096;
+__device__ unsigned long long g_attn_ts[kAttTraceWgs][8];
+#define ATT_T(...) __VA_ARGS__
+__device__ __forceinline__ void att_at(int i) {
+  if (blockIdx.x < kAttTraceWgs) g_attn_ts[blockIdx.x][i] = wall_clock64();
+}
+#else
+#define ATT_T(...)
+#endif
+
 // Decode steps (a plan: few (group, head) cells, key splits): the agent's PREFIX blocks
 // are shared by the workgroup's four 16-row tiles, so the split's prefix blocks (split,
 // split + n_used, ...) are staged through LDS once per workgroup and attended by every
@@ -620,6 +635,7 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
   __bf16* buf = reinterpret_cast<__bf16*>(lds);
   auto sm = reinterpret_cast<float (*)[16][LDSW]>(lds);
 
+  ATT_T(if (threadIdx.x == 0) att_at(0);)
   const int4 e = a.plan[blockIdx.x];
   const int pg = e.x, qg = e.y, split = e.z & 255, n_used = e.z >> 8, slot = e.w;
   const int gi = pg / a.Hkv, g = pg % a.Hkv;
@@ -651,6 +667,7 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
   const int nbp = (pl + kKeyBlock - 1) / kKeyBlock;
   // this split's prefix blocks: split, split + n_used, ...  (workgroup-uniform)
   const int npi = nbp > split ? (nbp - split + n_used - 1) / n_used : 0;
+  ATT_T(if (tid == 0 && npi + hb + po >= 0) att_at(1);)
 
   bf16x8 qf[NDS];
   {
@@ -727,6 +744,7 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
     __syncthreads();
   }
 
+  ATT_T(if (tid == 0) att_at(2);)
   // ---- the tile's own streams' history blocks, per wave (split * kw + ks, + nslot, ...) ----
   const int rt0 = r0 + qt * 16, rt1 = min(rt0 + 15, M - 1);
   const int b_lo = (rt0 / a.rep) / a.T, b_hi = (rt1 / a.rep) / a.T;
@@ -742,6 +760,7 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
       attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
     }
   }
+  ATT_T(if (tid == 0 && l >= 0.0f) att_at(3);)
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
 
@@ -799,6 +818,7 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
       pr[D + 1] = l;
     }
   }
+  ATT_T(if (tid == 0) { __builtin_amdgcn_s_waitcnt(0); att_at(4); })
 }
 
 // One workgroup per merge entry (kMergeRows rows of a split (group, head, query group)),
@@ -811,6 +831,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) 
   constexpr int NC = D / 4;
   __shared__ float wsm[kAttnThreads / 64][2][kMaxSplit];
   __shared__ float linv[kAttnThreads / 64][2];
+  ATT_T(if (threadIdx.x == 0) att_at(5);)
   const int4 e = a.plan[a.n_attn + blockIdx.x];
   const int pg = e.x, qg = e.y, slot0 = e.z, chunk = e.w & 255, nu = e.w >> 8;
   const int gi = pg / a.Hkv, g = pg % a.Hkv;
@@ -859,6 +880,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_merge_kernel(AttnParams a) 
     for (int i = 0; i < 4; ++i) v[i] = static_cast<__bf16>(acc[i] * inv);
     *reinterpret_cast<bf16x4*>(a.out + (tok * a.H + g * a.rep + jh) * D + 4 * c4) = v;
   }
+  ATT_T(if (threadIdx.x == 0) { __builtin_amdgcn_s_waitcnt(0); att_at(6); })
 }
 
 // RoPE (half-rotation convention) + placement.  One thread per (token, head, pair i < D/2).
@@ -1338,6 +1360,16 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
 #undef CS_ATTN_LAUNCH
   return check_launch("cs_prefix_attention");
 }
+
+#ifdef CS_TRACE_ATTN
+// diagnostics build only: copy the per-workgroup timestamps [kAttTraceWgs][8] and clear them
+int cs_attn_trace_read(unsigned long long* out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_ts), sizeof(g_attn_ts));
+  static unsigned long long zero[kAttTraceWgs][8];
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_ts), zero, sizeof(zero));
+  return 0;
+}
+#endif
 
 static int hist_gather_launch(const char* name, const void* src_k, void* dst_k, const void* src_vt,
                               void* dst_vt, const int64_t* parent, const int32_t* hist_base,

@@ -395,13 +395,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   const int32_t rows = A * B;
   const int32_t C = B * K;
   const int64_t item = blockIdx.x;
-  const int32_t row = static_cast<int32_t>(item / nsplit);
-  const int32_t split = static_cast<int32_t>(item - static_cast<int64_t>(row) * nsplit);
+  const int32_t per_row = nsplit > 1 ? split_items(nsplit, BLOCK) : 1;
+  const int32_t row = static_cast<int32_t>(item / per_row);
+  const int32_t sitem = static_cast<int32_t>(item - static_cast<int64_t>(row) * per_row);
   const int32_t ag = row / B;
   const int32_t bm = row - ag * B;
   const char* rp = logits + row * ld_bytes;
-  const int64_t v0 = static_cast<int64_t>(split) * split_len;
-  const int64_t v1 = min(vocab, v0 + split_len);
   uint32_t* Uw = reinterpret_cast<uint32_t*>(U);
   const bool order_free = kind == CS_WELFARE_MIN || kind == CS_WELFARE_MAX;
   const bool is_min = kind == CS_WELFARE_MIN;
@@ -416,17 +415,27 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
     build_cap_table<BLOCK>(ctab, cap, inv_cap);
     __syncthreads();
   }
-  const float2 ms = block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, v0, v1 - v0, cap, inv_cap,
-                                                                     sm_m, sm_s, ctab);
+  int32_t split = 0;
+  bool valid = true;
+  // split rows: the canonical split arithmetic (split_partial), BLOCK / 256 splits per block
+  const float2 ms =
+      nsplit > 1 ? split_partial<DT, CAP, FIXED, BLOCK>(rp, sitem, nsplit, split_len, vocab, cap,
+                                                        inv_cap, sm_m, sm_s, ctab, split, valid)
+                 : block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, 0, vocab, cap, inv_cap,
+                                                                    sm_m, sm_s, ctab);
 
   // 2. row finish by the row's last arriver
   if (nsplit > 1) {
-    if (tid == 0) {
+    if (valid && tid % kSplitSub == 0) {
       st_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + split,
              (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
                               __float_as_uint(ms.x));
       wait_stores();
-      sm_last = arrive(&row_cnt[row]) == static_cast<uint32_t>(nsplit - 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t nv = static_cast<uint32_t>(split_count(sitem, nsplit, BLOCK));
+      sm_last = arrive(&row_cnt[row], nv) + nv == static_cast<uint32_t>(nsplit);
     }
     __syncthreads();
     if (!sm_last) return;  // block-uniform
@@ -852,24 +861,35 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
   } else {
     // ---- agent row stream ----
     const int64_t item = rblk;
-    const int32_t row = static_cast<int32_t>(item / nsplit);
-    const int32_t split = static_cast<int32_t>(item - static_cast<int64_t>(row) * nsplit);
+    const int32_t per_row = nsplit > 1 ? split_items(nsplit, BLOCK) : 1;
+    const int32_t row = static_cast<int32_t>(item / per_row);
+    const int32_t sitem = static_cast<int32_t>(item - static_cast<int64_t>(row) * per_row);
     const char* rp = logits + row * ld_bytes;
-    const int64_t v0 = static_cast<int64_t>(split) * split_len;
-    const int64_t v1 = min(vocab, v0 + split_len);
     if constexpr (TAB) {
       build_cap_table<BLOCK>(ctab, cap, inv_cap);
       __syncthreads();
     }
-    const float2 ms = block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(
-        rp, v0, v1 - v0, cap, inv_cap, sm_m, sm_s, ctab);
+    int32_t split = 0;
+    bool valid = true;
+    // split rows: the canonical split arithmetic of cs_logsoftmax_gather / cs_beam_step
+    // (split_partial), so a 1024-thread launch (proposer chunks of 16 * 1024 elements) takes
+    // split rows four splits per block with the same bits as 256-thread splits
+    const float2 ms =
+        nsplit > 1 ? split_partial<DT, CAP, FIXED, BLOCK>(rp, sitem, nsplit, split_len, vocab, cap,
+                                                          inv_cap, sm_m, sm_s, ctab, split, valid)
+                   : block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, 0, vocab, cap, inv_cap,
+                                                                      sm_m, sm_s, ctab);
     if (nsplit > 1) {
-      if (tid == 0) {
+      if (valid && tid % kSplitSub == 0) {
         st_sc1(part + static_cast<int64_t>(row) * pad_line(nsplit, 8) + split,
                (static_cast<unsigned long long>(__float_as_uint(ms.y)) << 32) |
                                 __float_as_uint(ms.x));
         wait_stores();
-        sm_last = arrive(&row_cnt[row]) == static_cast<uint32_t>(nsplit - 1);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        const uint32_t nv = static_cast<uint32_t>(split_count(sitem, nsplit, BLOCK));
+        sm_last = arrive(&row_cnt[row], nv) + nv == static_cast<uint32_t>(nsplit);
       }
       __syncthreads();
       if (!sm_last) return;  // block-uniform
@@ -1038,23 +1058,15 @@ int cs_beam_step(const void* logits, int dtype, int32_t A, int32_t B, int64_t vo
   int32_t n2 = 2;
   while (n2 < C) n2 <<= 1;
   const char* lg = static_cast<const char*>(logits);
-  const dim3 grid(static_cast<uint32_t>(rows * plan.nsplit));
-  // the same streaming shapes as cs_logsoftmax_gather (bit-identical lse)
+  // the same streaming arithmetic as cs_logsoftmax_gather (bit-identical lse): unsplit rows
+  // one 1024-thread block x 2 vectors per lane, split rows the canonical split form
+  // (split_partial), four splits per 1024-thread block
+  const dim3 grid(static_cast<uint32_t>(rows * (plan.nsplit > 1 ? split_items(plan.nsplit, 1024) : 1)));
 #define CS_BEAM_LAUNCH(DTV, CAPV, FIXV)                                                           \
-  do {                                                                                            \
-    if (plan.nsplit > 1)                                                                          \
-      hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 256, 8>), grid, dim3(256), 0, st, lg, \
-                         vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,          \
-                         rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
-                         part, row_cnt, done_cnt, wkey, out_U, out_W, n_order, n2, out_order,     \
-                         out_order_val, out_kept);                                                \
-    else                                                                                          \
-      hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 1024, 2>), grid, dim3(1024), 0, st,   \
-                         lg, vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets,      \
-                         rewards_in, softcap, inv_cap, welfare_kind, static_cast<double>(eps),    \
-                         part, row_cnt, done_cnt, wkey, out_U, out_W, n_order, n2, out_order,     \
-                         out_order_val, out_kept);                                                \
-  } while (0)
+  hipLaunchKernelGGL((beam_step_kernel<DTV, CAPV, FIXV, 1024, 2>), grid, dim3(1024), 0, st, lg,     \
+                     vocab, ld_bytes, plan.nsplit, plan.split_len, A, B, K, targets, rewards_in,  \
+                     softcap, inv_cap, welfare_kind, static_cast<double>(eps), part, row_cnt,     \
+                     done_cnt, wkey, out_U, out_W, n_order, n2, out_order, out_order_val, out_kept)
   if (dtype == CS_F32) {
     if (fixed) CS_BEAM_LAUNCH(CS_F32, true, true);
     else if (cap) CS_BEAM_LAUNCH(CS_F32, true, false);
@@ -1090,7 +1102,11 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   DecodeLayout d;
   const int64_t rows = static_cast<int64_t>(A) * B;
   d.plan = plan_split(rows, vocab, dtype);
-  d.block = d.plan.nsplit > 1 ? 256 : 1024;
+  // 1024-thread blocks: split rows take four canonical splits per block (split_partial), so
+  // the proposer keeps its 16 * 1024-element chunks (per-rank C3: 43.98 -> 26.4 us,
+  // profiles/r05e_beam_ab_*.jsonl); 256-thread blocks (one split each) only where their
+  // wave-bound proposer selection applies (K <= 16, split rows: C1)
+  d.block = d.plan.nsplit > 1 && K <= kWaveBoundMaxK ? 256 : 1024;
   if (const char* e = getenv("CS_DECODE_BLOCK")) {   // A/B: 256 or 1024 whatever the split
     const int v = atoi(e);
     if (v == 256 || v == 1024) d.block = v;
@@ -1164,7 +1180,8 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
     return fail(CS_ERR_WORKSPACE, std::string(w) + "workspace smaller than cs_beam_decode_workspace_size()");
   if (reinterpret_cast<uintptr_t>(workspace) % 8 != 0)
     return fail(CS_ERR_WORKSPACE, std::string(w) + "workspace not 8-byte aligned");
-  const int64_t grid = static_cast<int64_t>(B) * d.nchunk_p + rows * d.plan.nsplit;
+  const int64_t row_blocks = rows * (d.plan.nsplit > 1 ? split_items(d.plan.nsplit, d.block) : 1);
+  const int64_t grid = static_cast<int64_t>(B) * d.nchunk_p + row_blocks;
   if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, std::string(w) + "grid too large");
   char* wsb = static_cast<char*>(workspace);
   auto* done_cnt = reinterpret_cast<uint32_t*>(wsb);
@@ -1185,7 +1202,7 @@ int cs_beam_decode_step(const void* ref_logits, int64_t ld_ref, const void* logi
   while (n2 < C) n2 <<= 1;
   const char* rg = static_cast<const char*>(ref_logits);
   const char* lg = static_cast<const char*>(logits);
-  const int32_t rows_first = decode_rows_first(rows * d.plan.nsplit, d.block);
+  const int32_t rows_first = decode_rows_first(row_blocks, d.block);
   // 16-byte vector loads in the proposer when every reference row starts 16-B aligned
   const int32_t ref_vec = (reinterpret_cast<uintptr_t>(ref_logits) % 16 == 0 &&
                            (ld_ref * esz) % 16 == 0) ? 1 : 0;

@@ -283,16 +283,20 @@ __device__ __forceinline__ void cap_accum(float& s, uint32_t& nanmax, const u32x
 // wave64 butterfly, then the waves merged in order through LDS.  The result is valid
 // in thread 0.  FIXED (soft-capped logits, |x'| <= cap <= 60): the sum needs no running
 // max, s = sum exp(x') with m = 0, so the inner loop has no max / rescale.
+// tid_in >= 0: the caller runs several BLOCK-thread sub-blocks side by side in one larger
+// workgroup (tid_in = thread index within the sub-block, sm_m / sm_s the sub-block's NW
+// slots; every sub-block reaches the workgroup barrier inside, so they run in lockstep).
 template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
 __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp, int64_t v0,
                                                     int64_t n, float cap, float inv_cap,
                                                     float* sm_m, float* sm_s,
-                                                    const float* __restrict__ ctab = nullptr) {
+                                                    const float* __restrict__ ctab = nullptr,
+                                                    int tid_in = -1) {
   constexpr int ESZ = Elt<DT>::kSize;
   constexpr int EPV = Elt<DT>::kPerVec;
   constexpr int NW = BLOCK / 64;
   constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
-  const int tid = threadIdx.x;
+  const int tid = tid_in >= 0 ? tid_in : static_cast<int>(threadIdx.x);
   float m = FIXED ? 0.0f : -INFINITY, s = 0.0f;
   uint32_t nanmax = 0u;
 
@@ -367,6 +371,50 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
   return make_float2(mm, ss);
 }
 
+// Split rows (plan_split: nsplit > 1), ONE arithmetic for every kernel that splits a row's
+// vocabulary (cs_logsoftmax_gather, cs_beam_step, cs_beam_decode_step), so their row lse are
+// bit-identical whatever workgroup shape streams the row: split j covers
+// [j * split_len, min(vocab, (j + 1) * split_len)) and its (m, s) is block_lse_partial over a
+// kSplitSub-thread sub-block with kSplitUnroll vectors in flight per lane; the partials are
+// merged in split order by one wave (split_merge).  A 256-thread workgroup streams one split,
+// a 1024-thread workgroup kSplitQuad consecutive splits side by side (quarter q of quad item
+// i: split kSplitQuad * i + q) -- the decode kernel's 1024-thread proposer chunks then share
+// a launch with split rows (tools/beam_ab.py; DESIGN.md "The beam decode launch (round 5)").
+constexpr int kSplitSub = 256;
+constexpr int kSplitUnroll = 2;
+constexpr int kSplitQuad = 4;
+__host__ __device__ constexpr int32_t split_items(int32_t nsplit, int block) {
+  return block >= kSplitSub * kSplitQuad ? (nsplit + kSplitQuad - 1) / kSplitQuad : nsplit;
+}
+
+// this thread's split of the row's work item `item` (0 <= item < split_items) and the
+// split's (m, s), valid in the sub-block's thread 0 when `valid`
+template <int DT, bool CAP, bool FIXED, int BLOCK>
+__device__ __forceinline__ float2 split_partial(const char* __restrict__ rp, int32_t item,
+                                               int32_t nsplit, int64_t split_len, int64_t vocab,
+                                               float cap, float inv_cap, float* sm_m, float* sm_s,
+                                               const float* __restrict__ ctab, int32_t& split,
+                                               bool& valid) {
+  static_assert(BLOCK == kSplitSub || BLOCK == kSplitSub * kSplitQuad, "split sub-blocks");
+  constexpr int SUBS = BLOCK / kSplitSub;
+  const int q = SUBS > 1 ? static_cast<int>(threadIdx.x) / kSplitSub : 0;
+  split = item * SUBS + q;
+  valid = split < nsplit;
+  const int64_t v0 = valid ? static_cast<int64_t>(split) * split_len : 0;
+  const int64_t n = valid ? min(vocab, v0 + split_len) - v0 : 0;
+  constexpr int NWS = kSplitSub / 64;
+  return block_lse_partial<DT, CAP, FIXED, kSplitSub, kSplitUnroll>(
+      rp, v0, n, cap, inv_cap, sm_m + q * NWS, sm_s + q * NWS, ctab,
+      static_cast<int>(threadIdx.x) % kSplitSub);
+}
+
+// the row's splits [0, nsplit) this work item holds (the arrival count it adds)
+__device__ __forceinline__ int32_t split_count(int32_t item, int32_t nsplit, int block) {
+  const int subs = block >= kSplitSub * kSplitQuad ? kSplitQuad : 1;
+  const int32_t left = nsplit - item * subs;
+  return left < subs ? left : subs;
+}
+
 // The fixed-offset sum is exact enough and cannot overflow for |x'| <= 60:
 // e^60 * 2^31 < FLT_MAX and e^-60 is a normal float.
 inline bool fixed_lse_ok(float cap) { return cap > 0.0f && cap <= 60.0f; }
@@ -433,13 +481,17 @@ inline int64_t target_wgs() {
   return v > 0 ? v : kTargetWgs;
 }
 
+// Fewer rows than target_wgs(): split the vocabulary so that about target_wgs() x
+// kSplitQuad 256-thread split sub-blocks (target_wgs() 1024-thread workgroups of four) stream
+// the rows -- each 1024-thread workgroup of the split kernels then has as many bytes in flight
+// as a whole unsplit row's workgroup.
 inline SplitPlan plan_split(int64_t rows, int64_t vocab, int dtype) {
   SplitPlan p{1, vocab};
   const int64_t target = target_wgs();
   if (rows <= 0 || vocab <= 0 || rows >= target) return p;
   const int64_t grain = static_cast<int64_t>(kBlock) * elt_per_vec(dtype);  // one vector per lane
   const int64_t min_len = grain * kUnroll;  // >= one full unrolled sweep per split
-  int64_t want = (target + rows - 1) / rows;
+  int64_t want = (target * kSplitQuad + rows - 1) / rows;
   int64_t max_split = vocab / min_len;
   if (max_split < 1) max_split = 1;
   if (want > max_split) want = max_split;
@@ -690,8 +742,8 @@ __device__ __forceinline__ unsigned long long ld_sc1(unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ uint32_t arrive(uint32_t* cnt) {
-  return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint32_t arrive(uint32_t* cnt, uint32_t n = 1u) {
+  return __hip_atomic_fetch_add(cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // floor(i / d) for 0 <= i < 2^24, d >= 1, with inv = 1.0f / d (uniform): the float

@@ -47,6 +47,34 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 1) void lsg_stream_kerne
   }
 }
 
+// Split rows in the canonical split arithmetic (split_partial, cs_kernels.cuh): BLOCK / 256
+// splits per workgroup, each split's (m, s) to part[row * nsplit + split] for lsg_merge_kernel.
+template <int DT, bool CAP, bool FIXED, int BLOCK>
+__global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 1) void lsg_split_kernel(
+    const char* __restrict__ logits, int64_t n_items, int64_t vocab, int64_t ld_bytes,
+    int32_t nsplit, int64_t split_len, float cap, float inv_cap, float2* __restrict__ part) {
+  __shared__ float sm_m[BLOCK / 64];
+  __shared__ float sm_s[BLOCK / 64];
+  constexpr bool TAB = CapTable<DT, CAP, FIXED>::kOn;
+  __shared__ float ctab[TAB ? kCapTab : 1];
+  if constexpr (TAB) {
+    build_cap_table<BLOCK>(ctab, cap, inv_cap);
+    __syncthreads();
+  }
+  const int32_t per_row = split_items(nsplit, BLOCK);
+  for (int64_t bid = blockIdx.x; bid < n_items; bid += gridDim.x) {
+    const int64_t row = bid / per_row;
+    const int32_t item = static_cast<int32_t>(bid - row * per_row);
+    int32_t split;
+    bool valid;
+    const float2 ms = split_partial<DT, CAP, FIXED, BLOCK>(logits + row * ld_bytes, item, nsplit,
+                                                          split_len, vocab, cap, inv_cap, sm_m,
+                                                          sm_s, ctab, split, valid);
+    if (valid && threadIdx.x % kSplitSub == 0) part[row * nsplit + split] = ms;
+    __syncthreads();  // sm_* are reused by the next work item
+  }
+}
+
 // split-V finish: merge the (m, s) partials of one row in split order, then gather.
 template <int DT, bool CAP>
 __global__ __launch_bounds__(kMergeBlock) void lsg_merge_kernel(
@@ -71,7 +99,8 @@ __global__ __launch_bounds__(kMergeBlock) void lsg_merge_kernel(
 // Streaming-kernel configurations compiled into the library.  Variant 0 (default) is
 // shape-aware, from the in-process A/B on the bench's data (profiles/r01_lsg_variants.jsonl):
 //   single pass (rows >= 2048): 1024 threads x 2 vectors in flight  (C2: 7.25 TB/s, 90.6 %)
-//   split-V (fewer rows):        256 threads x 8 vectors in flight
+//   split-V (fewer rows):        the canonical split arithmetic (split_partial, cs_kernels.cuh):
+//                                256-thread sub-blocks x 2 vectors, 4 splits per 1024 threads
 // CS_LSG_VARIANT=<n> (host environment, read per launch) forces one configuration for
 // A/B timing (tools/lsg_variants.py).  All variants compute the same values up to the
 // order of the fp32 partial merges inside a row (|diff| ~ 1e-6).
@@ -136,12 +165,27 @@ void launch_lsg(const void* logits, int64_t rows, int64_t vocab, int64_t ld_byte
                                      out_tok, out_lse, part, st);
       break;
     default:
-      if (plan.nsplit == 1)
+      if (plan.nsplit == 1) {
         launch_stream<DT, CAP, 1024, 2>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
                                         inv_cap, out_tok, out_lse, part, st);
-      else
-        launch_stream<DT, CAP, 256, 8>(logits, items, vocab, ld_bytes, plan, tgt, k, cap,
-                                       inv_cap, out_tok, out_lse, part, st);
+      } else {
+        // the canonical split arithmetic, four splits per 1024-thread workgroup
+        const int64_t n_items = rows * split_items(plan.nsplit, 1024);
+        const char* lg = static_cast<const char*>(logits);
+        bool done = false;
+        if constexpr (CAP) {
+          if (fixed_lse_ok(cap)) {
+            hipLaunchKernelGGL((lsg_split_kernel<DT, CAP, true, 1024>),
+                               dim3(static_cast<uint32_t>(n_items)), dim3(1024), 0, st, lg, n_items,
+                               vocab, ld_bytes, plan.nsplit, plan.split_len, cap, inv_cap, part);
+            done = true;
+          }
+        }
+        if (!done)
+          hipLaunchKernelGGL((lsg_split_kernel<DT, CAP, false, 1024>),
+                             dim3(static_cast<uint32_t>(n_items)), dim3(1024), 0, st, lg, n_items,
+                             vocab, ld_bytes, plan.nsplit, plan.split_len, cap, inv_cap, part);
+      }
       break;
   }
   if (plan.nsplit > 1 && finish) {
