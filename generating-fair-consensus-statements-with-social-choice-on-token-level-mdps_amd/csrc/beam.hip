@@ -1104,9 +1104,9 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   d.plan = plan_split(rows, vocab, dtype);
   // 1024-thread blocks: split rows take four canonical splits per block (split_partial), so
   // the proposer keeps its 16 * 1024-element chunks (per-rank C3: 43.98 -> 26.4 us,
-  // profiles/r05e_beam_ab_*.jsonl); 256-thread blocks (one split each) only where their
-  // wave-bound proposer selection applies (K <= 16, split rows: C1)
-  d.block = d.plan.nsplit > 1 && K <= kWaveBoundMaxK ? 256 : 1024;
+  // profiles/r05e_beam_ab_*.jsonl).  256-thread blocks (one split each, wave-bound proposer
+  // selection for K <= 16) measured slower at C1 too: 17.8 vs 16.9 us (r05f_beam_ab.jsonl)
+  d.block = 1024;
   if (const char* e = getenv("CS_DECODE_BLOCK")) {   // A/B: 256 or 1024 whatever the split
     const int v = atoi(e);
     if (v == 256 || v == 1024) d.block = v;
