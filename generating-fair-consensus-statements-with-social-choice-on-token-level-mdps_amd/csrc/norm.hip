@@ -49,7 +49,8 @@ __device__ __forceinline__ float row_sum(float ss, float* red) {
 // barrier and stored after it by the same thread.  wb != nullptr: the branch b is first
 // RMS-normalised itself with weight wb (Gemma-2's post-attention / post-MLP norm), with
 // the arithmetic and rounding of a separate add_rms launch over b alone.
-template <int VPT, bool FOLD>
+// FOLD: the K-split partials' count rounded up to a power of two (only those loads issued)
+template <int VPT, bool FOLD, int NSP = kMaxSplits>
 __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
     const uint16_t* a, int64_t lda, const uint16_t* __restrict__ b, int64_t ldb,
     const uint16_t* __restrict__ wb, uint16_t* s_out, int64_t lds,
@@ -76,16 +77,16 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
         // flight together; a select, not an added zero, skips the ones past `splits`)
         const float* q = bp + r * d + 8 * v;
         const int64_t sstride = static_cast<int64_t>(gridDim.x) * d;
-        f32x4 p0[kMaxSplits], p1[kMaxSplits];
+        f32x4 p0[NSP], p1[NSP];
 #pragma unroll
-        for (int sp = 0; sp < kMaxSplits; ++sp) {
+        for (int sp = 0; sp < NSP; ++sp) {
           const float* qs = q + (sp < splits ? sp : splits - 1) * sstride;
           p0[sp] = *reinterpret_cast<const f32x4*>(qs);
           p1[sp] = *reinterpret_cast<const f32x4*>(qs + 4);
         }
         f32x4 x0 = p0[0], x1 = p1[0];
 #pragma unroll
-        for (int sp = 1; sp < kMaxSplits; ++sp) {
+        for (int sp = 1; sp < NSP; ++sp) {
           x0 = sp < splits ? x0 + p0[sp] : x0;
           x1 = sp < splits ? x1 + p1[sp] : x1;
         }
@@ -215,11 +216,16 @@ int add_rms_launch(const char* name, const void* a, int64_t lda, const void* b, 
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int nv = static_cast<int>(d / 8);
   const dim3 grid(static_cast<uint32_t>(rows));
+#define CS_ADD_RMS_FOLD(V, NS)                                                                    \
+  hipLaunchKernelGGL((add_rms_kernel<V, true, NS>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, \
+                     WB, S, lds, W, d, eps, plus_one, Y, ldy, bp, splits)
 #define CS_ADD_RMS(V)                                                                             \
-  if (bp)                                                                                         \
-    hipLaunchKernelGGL((add_rms_kernel<V, true>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, WB, \
-                       S, lds, W, d, eps, plus_one, Y, ldy, bp, splits);                          \
-  else                                                                                            \
+  if (bp) {                                                                                       \
+    if (splits <= 2) CS_ADD_RMS_FOLD(V, 2);                                                       \
+    else if (splits <= 4) CS_ADD_RMS_FOLD(V, 4);                                                  \
+    else if (splits <= 8) CS_ADD_RMS_FOLD(V, 8);                                                  \
+    else CS_ADD_RMS_FOLD(V, 16);                                                                  \
+  } else                                                                                          \
     hipLaunchKernelGGL((add_rms_kernel<V, false>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb,   \
                        WB, S, lds, W, d, eps, plus_one, Y, ldy, bp, splits)
   if (nv <= kNormThreads) {
@@ -233,6 +239,7 @@ int add_rms_launch(const char* name, const void* a, int64_t lda, const void* b, 
                        WB, S, lds, W, d, eps, plus_one, Y, ldy, nullptr, 0);
   }
 #undef CS_ADD_RMS
+#undef CS_ADD_RMS_FOLD
   return check_launch(name);
 }
 

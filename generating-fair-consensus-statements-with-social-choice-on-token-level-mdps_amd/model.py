@@ -432,6 +432,10 @@ class Model:
             if nbytes <= budget - used:
                 wp[name] = ops.gemm_pack(w)
                 used += nbytes
+        # the copies are written on this thread's stream: finish them before publishing, so a
+        # forward or capture on another stream never reads a copy the GPU is still writing
+        if wp:
+            torch.cuda.current_stream(self.device).synchronize()
         self.wp = wp          # published whole: a concurrent forward sees all or nothing
         return used
 

@@ -457,12 +457,23 @@ def text_compat_last_stems(engine, tok, system: Optional[str], agent_users: Sequ
             j = jcache[t] = "".join(tok.tokens(ids)) if ids else ""
         return j
 
-    # one prompt per call against a full encode (a tokenizer outside the assumptions
-    # disables the incremental path for good)
-    probe = next(((a, i) for a in range(A) for i in range(n)
-                  if a not in slow_agents and i not in slow_set), None)
-    if probe is not None:
-        a, i = probe
+    # prompts checked against a full encode (a tokenizer outside the assumptions disables
+    # the incremental path for good): the first item of every call, and one item of each
+    # agent frame the first time that frame is seen -- every agent's own chat frame and cut
+    # point (its user text, e.g. non-ASCII) is verified once, at the cost of one full encode
+    # per distinct agent prompt
+    fast_i = next((i for i in range(n) if i not in slow_set), None)
+    probes = []
+    if fast_i is not None:
+        for a in range(A):
+            if a in slow_agents:
+                continue
+            pkey = ("probed", system, agent_users[a])
+            if not probes or pkey not in cache:
+                probes.append(a)
+                cache[pkey] = True
+    for a in probes:
+        i = fast_i
         base, mid, post = frames[a]
         hm, tp = split[mid + stems[stem_of[i]]]
         want = tok.encode(tok.chat_text(system or None, agent_users[a] + conts[i] + marks[i], True))

@@ -218,7 +218,7 @@ def main() -> None:
     # c1long: beam search only, whose calls are recorded by their last 6 span log-probs
     backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok,
                                     tail_positions=32 if args.family == "c1long" else None,
-                                    kv_cache=8 if args.family == "main128" else 0)
+                                    kv_cache=64 if args.family == "main128" else 0)
     install(args.reference, backend)
     scen_path = (("configs", "main_body", "scenario_1.yaml") if args.family == "main128" else
                  ("configs", "appendix", "llama", "scenario_1", "beam_search.yaml"))

@@ -99,3 +99,26 @@ def test_incremental_disables_itself_on_a_disagreeing_tokenizer(bpe):
     full = [users[0] + stems[0] + p for p in pieces]
     want = U.text_compat_last(_StubEngine(), bad, [system] * 2, full)
     assert bad._inc_disabled and got == want
+
+
+def test_every_agent_frame_is_checked_once(bpe):
+    """The full-encode check covers every agent's own chat frame and cut point:
+    a tokenizer whose cut point breaks only for the SECOND agent's prompt is caught on the
+    first call, and the result is still exact."""
+    T = importlib.import_module(PKG + ".tokenizer")
+    U = importlib.import_module(PKG + ".utils")
+    P = importlib.import_module(PKG + ".methods.prompts")
+    bad = T.BPETokenizer(os.path.join(HERE, "golden", "bpe_fixture"), "llama3", vocab_size=4096,
+                         use_config=True)
+    good_cut = bad.cut_point
+    users = [P.BEAM["agent_user"].format(issue="Parks?", opinion=o)
+             for o in ("More parks.", "Naïve café prices.")]
+    # a mid-word cut (" pr|ices", one BPE token) only inside the second agent's opinion
+    bad.cut_point = lambda text, seg: (text.index("prices") + 2 if "prices" in text[seg:] else
+                                       good_cut(text, seg))
+    stems, stem_of, pieces = ["Genetic data sho"], [0, 0], ["uld", "w"]
+    system = P.BEAM["agent_system"]
+    got = U.text_compat_last_stems(_StubEngine(), bad, system, users, stems, stem_of, pieces)
+    full = [u + stems[0] + p for u in users for p in pieces]
+    want = U.text_compat_last(_StubEngine(), bad, [system] * len(full), full)
+    assert bad._inc_disabled and got == want
