@@ -26,7 +26,7 @@ for cfg, (A, B, K, V, cap, dt, desc) in bench.BEAM_CONFIGS.items():
             for r in csv.DictReader(f):
                 if "beam_decode_kernel" not in r["Kernel_Name"]:
                     continue
-                kern = r["Kernel_Name"].split("(")[0]
+                kern = r["Kernel_Name"][r["Kernel_Name"].index("beam_decode_kernel"):].split("(")[0]
                 kb.setdefault((cfg, counter), []).append(float(r["Counter_Value"]))
                 meta[cfg] = (kern, A * B + B, V, esz)
                 rows_out.append({"config": "beam_" + cfg, "counter": counter, "kernel": kern,
