@@ -42,7 +42,12 @@ GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json",
                                   "method_traces_c1_long.json",
                                   # finite lookahead at the reference's main-body setting
                                   # (branching 2, depth 4) on the C1-shaped fixture
-                                  "method_traces_fl4.json"]
+                                  "method_traces_fl4.json",
+                                  # the reference's main-body experiment on a Llama-3.1-8B
+                                  # shape (head_dim 128, 32 / 8 heads, Llama-3.1 RoPE
+                                  # scaling, vocabulary 128,256; 2 layers): 5 agents, BoN
+                                  # 4 x 200 tokens, lookahead bf 2 / d 4, beam 4 x 100 tokens
+                                  "method_traces_main128.json.gz"]
 
 
 def load_traces(name: str = "method_traces.json"):

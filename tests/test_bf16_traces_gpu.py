@@ -51,7 +51,11 @@ BF16_TRACE_FILES = ["method_traces_c1.json", "method_traces_wide.json",
                     # C1 at 50 tokens: the bf16 step graphs over two V^T tiles of history
                     "method_traces_c1_long.json",
                     # lookahead branching 2 / depth 4, teacher-forced on the reference's trees
-                    "method_traces_fl4.json"]
+                    "method_traces_fl4.json",
+                    # head_dim 128 (Llama-3.1-8B / 3.3-70B: C2, C4, C5) and the reference's
+                    # main-body experiment: BoN 4 x 200 tokens, lookahead bf 2 / d 4, beam 4
+                    # over 100 tokens, 5 agents
+                    "method_traces_main128.json.gz"]
 _REPORT = {}
 
 
