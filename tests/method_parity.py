@@ -50,6 +50,10 @@ GPU_TRACE_FILES = TRACE_FILES + ["method_traces_c1.json",
                                   "method_traces_main128.json.gz"]
 
 
+def trace_exists(name: str) -> bool:
+    return os.path.exists(os.path.join(HERE, "golden", name))
+
+
 def load_traces(name: str = "method_traces.json"):
     path = os.path.join(HERE, "golden", name)
     if name.endswith(".gz"):

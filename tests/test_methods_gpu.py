@@ -14,6 +14,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module", params=mp.GPU_TRACE_FILES)
 def traces(request, dev):
+    if not mp.trace_exists(request.param):
+        pytest.skip(f"{request.param} not generated (tests/golden/make_method_traces.py)")
     t = mp.load_traces(request.param)
     mp.register_fixture_engine(t, dev)
     yield t
