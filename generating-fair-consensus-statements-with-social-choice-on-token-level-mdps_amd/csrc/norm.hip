@@ -31,8 +31,9 @@ __device__ __forceinline__ uint16_t to_bf(float f) {
 constexpr int kNormThreads = 256;
 constexpr int kMaxSplits = 16;      // K-split partials folded by cs_add_rms_norm_splitk
 
-// the row's sum over the workgroup: wave64 butterfly, then the 4 wave sums in wave order
-// (the same order everywhere, so a norm is bitwise the same in every kernel that uses it)
+// the row's sum over the workgroup: wave64 butterfly, then the BLOCK / 64 wave sums in wave
+// order (the same order everywhere, so a norm is bitwise the same in every kernel that uses it)
+template <int BLOCK = kNormThreads>
 __device__ __forceinline__ float row_sum(float ss, float* red) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
@@ -40,7 +41,7 @@ __device__ __forceinline__ float row_sum(float ss, float* red) {
   __syncthreads();
   float tot = 0.0f;
 #pragma unroll
-  for (int i = 0; i < kNormThreads / 64; ++i) tot += red[i];
+  for (int i = 0; i < BLOCK / 64; ++i) tot += red[i];
   return tot;
 }
 
@@ -49,16 +50,19 @@ __device__ __forceinline__ float row_sum(float ss, float* red) {
 // barrier and stored after it by the same thread.  wb != nullptr: the branch b is first
 // RMS-normalised itself with weight wb (Gemma-2's post-attention / post-MLP norm), with
 // the arithmetic and rounding of a separate add_rms launch over b alone.
-// FOLD: the K-split partials' count rounded up to a power of two (only those loads issued)
-template <int VPT, bool FOLD, int NSP = kMaxSplits>
-__global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
+// FOLD: the K-split partials' count rounded up to a power of two (only those loads issued).
+// BLOCK: threads per row -- one 16-byte vector per thread up to d = 8192 (a decode step's
+// 48-72 rows are one workgroup each, so the row's loads are spread over as many lanes as
+// its vectors: the launch is a few memory round trips, not VPT serial issue batches)
+template <int VPT, bool FOLD, int NSP = kMaxSplits, int BLOCK = kNormThreads>
+__global__ __launch_bounds__(BLOCK) void add_rms_kernel(
     const uint16_t* a, int64_t lda, const uint16_t* __restrict__ b, int64_t ldb,
     const uint16_t* __restrict__ wb, uint16_t* s_out, int64_t lds,
     const uint16_t* __restrict__ w, int64_t d, float eps, int plus_one,
     uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ bp, int splits) {
   const int64_t r = blockIdx.x;
   const int nv = static_cast<int>(d >> 3);
-  __shared__ float red[2][kNormThreads / 64];
+  __shared__ float red[2][BLOCK / 64];
   // every load of the row is issued before the first reduction: one memory round trip per
   // row instead of four (b, then wb after b's norm, then a, then w after the second norm);
   // the weights are prefetched only while the registers allow (VPT <= 4)
@@ -66,7 +70,7 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
   u16x8 bv[VPT], av[VPT], wv[kPre ? VPT : 1], wbv[kPre ? VPT : 1];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int v = threadIdx.x + k * kNormThreads;
+    const int v = threadIdx.x + k * BLOCK;
     if (v < nv) {
       av[k] = *reinterpret_cast<const u16x8*>(a + r * lda + 8 * v);
       if constexpr (FOLD) {
@@ -109,16 +113,16 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
     float sb = 0.0f;
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      const int v = threadIdx.x + k * kNormThreads;
+      const int v = threadIdx.x + k * BLOCK;
       if (v < nv) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) sb = fmaf(bf(bv[k][e]), bf(bv[k][e]), sb);
       }
     }
-    const float inv_b = 1.0f / sqrtf(row_sum(sb, red[0]) / static_cast<float>(d) + eps);
+    const float inv_b = 1.0f / sqrtf(row_sum<BLOCK>(sb, red[0]) / static_cast<float>(d) + eps);
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      const int v = threadIdx.x + k * kNormThreads;
+      const int v = threadIdx.x + k * BLOCK;
       if (v < nv) {
         u16x8 g8;
         if constexpr (kPre) g8 = wbv[k];
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
   float ss = 0.0f;
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int v = threadIdx.x + k * kNormThreads;
+    const int v = threadIdx.x + k * BLOCK;
     if (v < nv) {
       if (has_b) {
 #pragma unroll
@@ -144,10 +148,10 @@ __global__ __launch_bounds__(kNormThreads) void add_rms_kernel(
       for (int e = 0; e < 8; ++e) ss = fmaf(bf(av[k][e]), bf(av[k][e]), ss);
     }
   }
-  const float inv = 1.0f / sqrtf(row_sum(ss, red[1]) / static_cast<float>(d) + eps);
+  const float inv = 1.0f / sqrtf(row_sum<BLOCK>(ss, red[1]) / static_cast<float>(d) + eps);
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int v = threadIdx.x + k * kNormThreads;
+    const int v = threadIdx.x + k * BLOCK;
     if (v < nv) {
       if (s_out) *reinterpret_cast<u16x8*>(s_out + r * lds + 8 * v) = av[k];
       u16x8 g8;
@@ -190,6 +194,14 @@ __global__ __launch_bounds__(kNormThreads) void gated_act_kernel(
   *reinterpret_cast<u16x8*>(out + r * ldo + j) = o;
 }
 
+bool norm_vpt_form() {
+  static const bool v = [] {
+    const char* e = getenv("CS_NORM_VPT");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 int add_rms_launch(const char* name, const void* a, int64_t lda, const void* b, int64_t ldb,
                    const float* bp, int splits, const void* b_weight, void* s_out, int64_t lds,
                    const void* weight, int64_t rows, int64_t d, float eps, int plus_one, void* y,
@@ -216,24 +228,38 @@ int add_rms_launch(const char* name, const void* a, int64_t lda, const void* b, 
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int nv = static_cast<int>(d / 8);
   const dim3 grid(static_cast<uint32_t>(rows));
-#define CS_ADD_RMS_FOLD(V, NS)                                                                    \
-  hipLaunchKernelGGL((add_rms_kernel<V, true, NS>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb, \
+#define CS_ADD_RMS_FOLD(V, BL, NS)                                                                \
+  hipLaunchKernelGGL((add_rms_kernel<V, true, NS, BL>), grid, dim3(BL), 0, st, A, lda, B, ldb,     \
                      WB, S, lds, W, d, eps, plus_one, Y, ldy, bp, splits)
-#define CS_ADD_RMS(V)                                                                             \
+#define CS_ADD_RMS(V, BL)                                                                         \
   if (bp) {                                                                                       \
-    if (splits <= 2) CS_ADD_RMS_FOLD(V, 2);                                                       \
-    else if (splits <= 4) CS_ADD_RMS_FOLD(V, 4);                                                  \
-    else if (splits <= 8) CS_ADD_RMS_FOLD(V, 8);                                                  \
-    else CS_ADD_RMS_FOLD(V, 16);                                                                  \
+    if (splits <= 2) CS_ADD_RMS_FOLD(V, BL, 2);                                                   \
+    else if (splits <= 4) CS_ADD_RMS_FOLD(V, BL, 4);                                              \
+    else if (splits <= 8) CS_ADD_RMS_FOLD(V, BL, 8);                                              \
+    else CS_ADD_RMS_FOLD(V, BL, 16);                                                              \
   } else                                                                                          \
-    hipLaunchKernelGGL((add_rms_kernel<V, false>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb,   \
-                       WB, S, lds, W, d, eps, plus_one, Y, ldy, bp, splits)
-  if (nv <= kNormThreads) {
-    CS_ADD_RMS(1);
-  } else if (nv <= 2 * kNormThreads) {
-    CS_ADD_RMS(2);
-  } else if (nv <= 4 * kNormThreads) {
-    CS_ADD_RMS(4);
+    hipLaunchKernelGGL((add_rms_kernel<V, false, kMaxSplits, BL>), grid, dim3(BL), 0, st, A, lda, \
+                       B, ldb, WB, S, lds, W, d, eps, plus_one, Y, ldy, bp, splits)
+  // one vector per thread up to d = 8192 (the block size depends on d only, so a norm's
+  // rounding is the same at every row count).  CS_NORM_VPT=1 (A/B only): the round-4 form,
+  // 256 threads with up to 4 vectors each
+  if (norm_vpt_form()) {
+    if (nv <= 256) {
+      CS_ADD_RMS(1, 256);
+    } else if (nv <= 512) {
+      CS_ADD_RMS(2, 256);
+    } else if (nv <= 1024) {
+      CS_ADD_RMS(4, 256);
+    } else {
+      hipLaunchKernelGGL((add_rms_kernel<16, false>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb,
+                         WB, S, lds, W, d, eps, plus_one, Y, ldy, nullptr, 0);
+    }
+  } else if (nv <= 256) {
+    CS_ADD_RMS(1, 256);
+  } else if (nv <= 512) {
+    CS_ADD_RMS(1, 512);
+  } else if (nv <= 1024) {
+    CS_ADD_RMS(1, 1024);
   } else {       // (d > 8192: the fold is refused above)
     hipLaunchKernelGGL((add_rms_kernel<16, false>), grid, dim3(kNormThreads), 0, st, A, lda, B, ldb,
                        WB, S, lds, W, d, eps, plus_one, Y, ldy, nullptr, 0);

@@ -147,9 +147,10 @@ MAIN128_RUNS = [
 ]
 # echo log-probs of the prompt tail only (the LM head over these rows): beam search keeps
 # the last one (beam_search.py:389-390), the lookahead the path's last <= 4
-# (finite_lookahead.py:508-520); Best-of-N / the evaluator need the user span (a <= 200-token
-# statement + the chat frame's closing tokens)
-MAIN128_TAIL = {"beam_search": 8, "best_of_n": 320, "finite_lookahead": 16, "eval": 320}
+# (finite_lookahead.py:508-520); Best-of-N needs the user span (a <= 200-token candidate +
+# the chat frame's closing tokens); the evaluator every position (the reference's find() of a
+# short statement can land in the system prompt, src/utils.py:321-363)
+MAIN128_TAIL = {"beam_search": 8, "best_of_n": 320, "finite_lookahead": 16, "eval": None}
 
 
 WIDE_AGENTS = 16
@@ -208,6 +209,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--family", default="llama3", choices=sorted(FAMILIES))
+    ap.add_argument("--resume", action="store_true",
+                    help="reuse the runs a previous (killed) generation of this family finished")
     args = ap.parse_args()
     import yaml
     import fake_together
@@ -287,7 +290,17 @@ def main() -> None:
                   "max_sampling_attempts": 20, "rollout_depth": 3, "gamma": 0.5, "seed": 2,
                   "api_delay": 0, "log_level": "WARNING"}),
     ]
-    for method, mcfg in runs:
+    # --resume: the runs a killed generation finished (written after every run)
+    partial = os.path.join(tempfile.gettempdir(), f"make_method_traces_{args.family}.partial.json")
+    done = []
+    if args.resume and os.path.exists(partial):
+        with open(partial) as f:
+            done = json.load(f)
+    for ri, (method, mcfg) in enumerate(runs):
+        if ri < len(done) and done[ri]["method"] == method and done[ri]["config"] == mcfg:
+            out["runs"].append(done[ri])
+            print(f"{method}: resumed ({len(done[ri]['calls'])} scoring calls)")
+            continue
         calls.clear()
         if args.family == "main128":
             backend.tail = MAIN128_TAIL[method]
@@ -361,6 +374,8 @@ def main() -> None:
                             "pre_brushup": getattr(gen, "pre_brushup_statement", None),
                             "calls": list(calls), **extra})
         print(f"{method}: {stmt!r} ({len(calls)} scoring calls)")
+        with open(partial, "w") as f:
+            json.dump(out["runs"], f)
 
     if args.family in ("c1long", "fl4"):   # method runs only (no evaluator pass)
         import math
