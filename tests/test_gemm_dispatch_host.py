@@ -2,6 +2,7 @@
 as ops.gemm_choice reads them, the per-weight packing gain, and the merge of per-config
 tuner outputs (tools/merge_gemm_dispatch.py)."""
 import importlib
+import types
 import json
 import os
 import sys
@@ -101,7 +102,12 @@ def test_pack_decode_weights_orders_by_gain_per_byte_within_the_budget(monkeypat
     qkv = sum(v for n, v in sizes.items() if n.endswith("qkv"))
     budget = gu + qkv // 2                             # every gate|up, half the q|k|v
     monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (budget + (1 << 30), 8 << 30))
+    # the packed copies are finished on their stream before they are published (no device here)
+    synced = []
+    monkeypatch.setattr(torch.cuda, "current_stream",
+                        lambda dev=None: types.SimpleNamespace(synchronize=lambda: synced.append(1)))
     used = m.pack_decode_weights(reserve_bytes=1 << 30)
+    assert synced, "the packed copies were published without finishing their stream"
     names = set(m.wp)
     assert all(n in names for n in sizes if n.endswith("gate_up"))
     assert not any(n.endswith("w_down") for n in names)          # no gain: never packed
