@@ -29,7 +29,8 @@ EXPORTED = (
     "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
     "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits",
     "cs_gemm_bf16_packed", "cs_gemm_pack", "cs_rope_place_splitk",
-    "cs_add_rms_norm_splitk",
+    "cs_add_rms_norm_splitk", "cs_prefix_attention_rows", "cs_rope_place_rows",
+    "cs_rope_place_splitk_rows", "cs_hist_rows_update",
 )
 
 
@@ -140,6 +141,16 @@ def load():
     L.cs_rope_place_splitk.argtypes = [vp, i32, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp,
                                        vp, vp, i64, vp]
     L.cs_rope_place_splitk.restype = ctypes.c_int
+    L.cs_prefix_attention_rows.argtypes = [vp, vp, vp, i64, vp, vp, i32, vp, i32, vp, vp, vp, i64,
+                                           vp, i32, i32, i32, i32, i32, f32, f32, i32, vp, i32, i32,
+                                           vp, vp, ctypes.c_size_t, vp]
+    L.cs_prefix_attention_rows.restype = ctypes.c_int
+    L.cs_rope_place_rows.argtypes = L.cs_rope_place.argtypes
+    L.cs_rope_place_rows.restype = ctypes.c_int
+    L.cs_rope_place_splitk_rows.argtypes = L.cs_rope_place_splitk.argtypes
+    L.cs_rope_place_splitk_rows.restype = ctypes.c_int
+    L.cs_hist_rows_update.argtypes = [vp, vp, vp, vp, i64, i32, vp]
+    L.cs_hist_rows_update.restype = ctypes.c_int
     _lib = L
     return L
 

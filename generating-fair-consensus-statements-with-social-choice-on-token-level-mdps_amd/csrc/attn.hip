@@ -73,6 +73,8 @@ struct AttnParams {
   const __bf16* kh;
   const __bf16* vth;
   const int32_t* hist_base;
+  const int32_t* hrow;      // row-layout history (cs_prefix_attention_rows): [S][ldh] stream
+                            // row holding each slot; nullptr: V^T tiles, slot j of stream s in row s
   __bf16* out;
   float* part;              // [slot][kGroupRows][D + 2]: O (unnormalised), m, l
   const int4* plan;         // nullable: one workgroup per (group, head, query group), no split
@@ -622,7 +624,16 @@ __device__ __forceinline__ void att_at(int i) {
 // there.  Every key block is attended exactly once per (query row, split) as in the
 // per-wave assignment, so the split partials and the merge are unchanged.
 // two waves per SIMD at every D (D = 256: 237 VGPRs, no spills; 1 wave/SIMD before)
-template <int D>
+//
+// ROWS (cs_prefix_attention_rows): the history is row-major for K AND V ([S][Hkv][ldh][D])
+// and slot j of stream s lives in stream row hrow[s][j] -- a beam inherits its parent's
+// slots through the table (cs_hist_rows_update), no K / V is copied.  A history block's 32
+// V rows are gathered by LDS DMA into the wave's own 1 KB-per-16-d image [d/16][key][16 d]
+// (lane l loads key l / 2, 8 d of d-tile i: one table entry per lane) and read back
+// transposed (ds_read_b64_tr_b16: lane 4q + p of group h reads key 4h + q, d 16 dt + 4p) as
+// the V^T operand the V^T-tile layout gives; every 32-lane half reads 8 keys x 32 B at
+// 32-B key pitch: 64 distinct banks, conflict-free.
+template <int D, bool ROWS = false>
 __global__ __launch_bounds__(kAttnThreads, 2)
 void prefix_attn_plan_lds_kernel(AttnParams a) {
   using LT = LdsTile<D>;
@@ -631,12 +642,17 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
   constexpr int LDSW = D + 2;
   constexpr int kBufBytes = 2 * LT::ELEMS * 2;
   constexpr int kCombBytes = 3 * 16 * LDSW * 4;
+  constexpr int kVImg = kKeyBlock * D * 2;            // ROWS: one wave's V image of a block
+  static_assert(kAttnThreads / 64 * kVImg <= kBufBytes, "the V images fit the prefix buffers");
   __shared__ __attribute__((aligned(16))) char lds[kBufBytes > kCombBytes ? kBufBytes : kCombBytes];
   __bf16* buf = reinterpret_cast<__bf16*>(lds);
   auto sm = reinterpret_cast<float (*)[16][LDSW]>(lds);
 
   ATT_T(if (threadIdx.x == 0) att_at(0);)
-  const int4 e = a.plan[blockIdx.x];
+  // no plan (ROWS only): one workgroup per (group, head, query group), unsplit
+  const int4 e = a.plan ? a.plan[blockIdx.x]
+                        : int4{static_cast<int>(blockIdx.x) / a.n_qg, static_cast<int>(blockIdx.x) % a.n_qg,
+                               1 << 8, 0};
   const int pg = e.x, qg = e.y, split = e.z & 255, n_used = e.z >> 8, slot = e.w;
   const int gi = pg / a.Hkv, g = pg % a.Hkv;
   const int p = a.gpfx ? a.gpfx[gi] : gi;
@@ -752,13 +768,66 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
   const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
   const int n_hist = (b_hi - b_lo + 1) * nbh;
   const int nslot = n_used * kw;
-  if (active) {
-    for (int ih = split * kw + ks; ih < n_hist; ih += nslot) {
-      KeyBlock<D> f;
-      const ItemRef r = item_ref(a, nbp + ih, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D);
-      load_block<D>(f, r);
-      attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+  if constexpr (!ROWS) {
+    if (active) {
+      for (int ih = split * kw + ks; ih < n_hist; ih += nslot) {
+        KeyBlock<D> f;
+        const ItemRef r = item_ref(a, nbp + ih, nbp, nbh, b_lo, b, gi, g, po, pl, hv, vrow, col, h4, D);
+        load_block<D>(f, r);
+        attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+      }
     }
+  } else {
+    unsigned char* vimg = reinterpret_cast<unsigned char*>(lds) + w * kVImg;
+    // this lane's transposed-read offset in a d-tile's 1 KB: key 4 h4 + q (vlo; + 16 for
+    // vhi), d 4 p of the tile, q = (lane & 15) / 4, p = lane & 3
+    const uint32_t tr0 = static_cast<uint32_t>(32 * (4 * h4 + ((lane & 15) >> 2)) + 8 * (lane & 3));
+    typedef __attribute__((address_space(3))) bf16x4* lds_b4_ptr;
+    if (active) {
+      for (int ih = split * kw + ks; ih < n_hist; ih += nslot) {
+        const int bb = b_lo + ih / nbh;
+        const int kb = (ih % nbh) * kKeyBlock;
+        const int64_t sg = static_cast<int64_t>(gi) * a.n_str + bb;
+        const int32_t* hr = a.hrow + sg * a.ldh + kb;
+        // stream rows of keys col, 16 + col (K fragments) and lane / 2 (the V gather)
+        const int64_t rk0 = hr[col], rk1 = hr[16 + col], rv = hr[lane >> 1];
+        auto row_ptr = [&](const __bf16* base, int64_t srow, int key) {
+          return base + ((srow * a.Hkv + g) * a.ldh + kb + key) * D;
+        };
+        const __bf16* vsrc = row_ptr(a.vth, rv, lane >> 1) + 8 * (lane & 1);
+        KeyBlock<D> f;
+        const __bf16* kp0 = row_ptr(a.kh, rk0, col) + 8 * h4;
+        const __bf16* kp1 = row_ptr(a.kh, rk1, 16 + col) + 8 * h4;
+        // K first: its addresses wait for the table entries, the DMAs' issue then never waits
+#pragma unroll
+        for (int ds = 0; ds < NDS; ++ds) {
+          f.k0[ds] = *reinterpret_cast<const bf16x8*>(kp0 + ds * 32);
+          f.k1[ds] = *reinterpret_cast<const bf16x8*>(kp1 + ds * 32);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the last block's reads are done
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+          __builtin_amdgcn_global_load_lds(vsrc + 16 * dt, (__attribute__((address_space(3))) void*)(vimg + 1024 * dt),
+                                           16, 0, 0);
+        // every load of the block in flight before the first wait: one memory round trip
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the V image has landed
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          f.vlo[dt] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4_ptr)(vimg + 1024 * dt + tr0));
+          f.vhi[dt] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4_ptr)(vimg + 1024 * dt + tr0 + 512));
+        }
+        ItemRef r;
+        r.k = nullptr;
+        r.v = nullptr;
+        r.kb = kb;
+        r.lim = (vrow && bb == b) ? hv : 0;
+        r.pos0 = pl;
+        attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+      }
+    }
+    __syncthreads();   // every wave's V image read before the combine reuses the LDS
   }
   ATT_T(if (tid == 0 && l >= 0.0f) att_at(3);)
   l += __shfl_xor(l, 16, 64);
@@ -900,6 +969,7 @@ struct RopeParams {
   int64_t n_tok;
   int32_t n_str, T, H, Hkv, D;
   int32_t skip_v;           // V placed by v_tile_place_kernel instead
+  int32_t v_rows;           // V row-major like K ([S][Hkv][ldh][D], cs_rope_place_rows)
 };
 
 // n_split workgroups per token (kRopeItems (head, P-pair group) items each): the token's D/2
@@ -921,8 +991,10 @@ __device__ __forceinline__ __bf16 rope_to_bf(float f) {
 
 // FOLD: the projection arrives as a K-split GEMM's unfolded fp32 partials (r.part), summed
 // here in split order and rounded as cs_gemm_bf16's own fold would -- one launch and one
-// bf16 round trip fewer per layer, bitwise the same q / K / V.
-template <int P, bool FOLD = false>
+// bf16 round trip fewer per layer, bitwise the same q / K / V.  NSP splits' loads are issued
+// together (surplus ones re-read the last split and are not summed): one memory round trip
+// per NSP splits, not one per split.
+template <int P, bool FOLD = false, int NSP = 1>
 __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r, int32_t n_split) {
   typedef __bf16 vec_t __attribute__((ext_vector_type(P)));
   __shared__ float cs[128], sn[128];                // D / 2 <= 128
@@ -952,26 +1024,29 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r, int32_t n
       const int64_t off = tok * r.ldqkv + static_cast<int64_t>(hh) * r.D + i0;
       const int64_t sstride = r.n_tok * r.ldqkv;
       float fa[P], fb[P];
+      for (int c0 = 0; c0 < r.splits; c0 += NSP) {
+        f32x4 la[NSP][P / 4], lb[NSP][P / 4];
 #pragma unroll
-      for (int e = 0; e < P; e += 4) {
-        const f32x4 va = *reinterpret_cast<const f32x4*>(r.part + off + e);
-        const f32x4 vb = *reinterpret_cast<const f32x4*>(r.part + off + half + e);
+        for (int j = 0; j < NSP; ++j) {
+          const int sp = min(c0 + j, r.splits - 1);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          fa[e + c] = va[c];
-          fb[e + c] = vb[c];
-        }
-      }
-      for (int sp = 1; sp < r.splits; ++sp) {
-#pragma unroll
-        for (int e = 0; e < P; e += 4) {
-          const f32x4 va = *reinterpret_cast<const f32x4*>(r.part + sp * sstride + off + e);
-          const f32x4 vb = *reinterpret_cast<const f32x4*>(r.part + sp * sstride + off + half + e);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            fa[e + c] += va[c];
-            fb[e + c] += vb[c];
+          for (int e = 0; e < P; e += 4) {
+            la[j][e / 4] = *reinterpret_cast<const f32x4*>(r.part + sp * sstride + off + e);
+            lb[j][e / 4] = *reinterpret_cast<const f32x4*>(r.part + sp * sstride + off + half + e);
           }
+        }
+        __builtin_amdgcn_sched_barrier(0);   // every load of the chunk issued before the sums
+#pragma unroll
+        for (int j = 0; j < NSP; ++j) {
+          const bool first = c0 + j == 0, use = c0 + j < r.splits;
+#pragma unroll
+          for (int e = 0; e < P; e += 4)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float xa = la[j][e / 4][c], xb = lb[j][e / 4][c];
+              fa[e + c] = first ? xa : (use ? fa[e + c] + xa : fa[e + c]);
+              fb[e + c] = first ? xb : (use ? fb[e + c] + xb : fb[e + c]);
+            }
         }
       }
 #pragma unroll
@@ -987,6 +1062,12 @@ __global__ __launch_bounds__(256) void rope_place_kernel(RopeParams r, int32_t n
     if (hh >= r.H + r.Hkv) {                         // v: transposed placement, no rotation
       if (r.skip_v) continue;
       const int g = hh - r.H - r.Hkv;
+      if (r.v_rows) {
+        __bf16* dst = vth + ((s * r.Hkv + g) * r.ldh + slot) * r.D;
+        *reinterpret_cast<vec_t*>(dst + i0) = a;
+        *reinterpret_cast<vec_t*>(dst + half + i0) = b;
+        continue;
+      }
       __bf16* dst = vth + ((s * r.Hkv + g) * r.ldh + (slot & ~31)) * r.D +
                     static_cast<int64_t>(i0) * 32 + (slot & 31);
 #pragma unroll
@@ -1116,6 +1197,21 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
       }
     }
   }
+}
+
+// Row-layout beam history (cs_hist_rows_update): stream s inherits its parent's slots by
+// table, dst[s][j] = src[parent[s]][j] for j < hist_base, and owns the rest (dst[s][j] = s:
+// the slots this step and later ones write into its own row).  One thread per (s, j).
+__global__ __launch_bounds__(256) void hist_rows_kernel(const int32_t* __restrict__ src,
+                                                        int32_t* __restrict__ dst,
+                                                        const int64_t* __restrict__ parent,
+                                                        const int32_t* __restrict__ hist_base,
+                                                        int64_t S, int32_t ldh) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= S * ldh) return;
+  const int64_t s = i / ldh;
+  const int j = static_cast<int>(i - s * ldh);
+  dst[i] = j < *hist_base ? src[parent[s] * ldh + j] : static_cast<int32_t>(s);
 }
 
 // plan tunables (CS_ATTN_TARGET_WGS, CS_ATTN_MIN_ITEMS override; read once)
@@ -1273,37 +1369,41 @@ int64_t cs_prefix_attention_plan(const int32_t* prefix_len, int32_t n_prefix,
   return total;
 }
 
-int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
-                        int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
-                        int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
-                        const void* k_hist, const void* vt_hist, int64_t ld_hist,
-                        const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
-                        int32_t D, float scale, float softcap, int32_t window, const void* plan,
-                        int32_t n_attn, int32_t n_merge, void* out, void* workspace,
-                        size_t workspace_bytes, cs_stream_t stream) {
-  if (n_groups < 0 || n_str < 0 || T < 0) return fail(CS_ERR_INVALID, "cs_prefix_attention: negative size");
+}  // extern "C"
+
+namespace {
+// hist_rows == nullptr: cs_prefix_attention (V^T tiles); else cs_prefix_attention_rows
+int prefix_attention_impl(const char* name, const void* q, const void* k_prefix, const void* vt_prefix,
+                          int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
+                          int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                          const void* k_hist, const void* vt_hist, const int32_t* hist_rows,
+                          int64_t ld_hist, const int32_t* hist_base, int32_t n_str, int32_t T,
+                          int32_t H, int32_t Hkv, int32_t D, float scale, float softcap,
+                          int32_t window, const void* plan, int32_t n_attn, int32_t n_merge,
+                          void* out, void* workspace, size_t workspace_bytes, cs_stream_t stream) {
+  const std::string nm(name);
+  if (n_groups < 0 || n_str < 0 || T < 0) return fail(CS_ERR_INVALID, nm + ": negative size");
   if (n_groups == 0 || n_str == 0 || T == 0) return CS_OK;
   if (Hkv <= 0 || H <= 0 || H % Hkv != 0 || H / Hkv > 64)
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: H must be a multiple of Hkv (<= 64 per group)");
+    return fail(CS_ERR_INVALID, nm + ": H must be a multiple of Hkv (<= 64 per group)");
   if (D != 64 && D != 128 && D != 256)
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: head_dim must be 64, 128 or 256");
+    return fail(CS_ERR_INVALID, nm + ": head_dim must be 64, 128 or 256");
   if (ld_prefix <= 0 || ld_prefix % kKeyBlock != 0 || ld_hist <= 0 || ld_hist % kKeyBlock != 0)
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: ld_prefix / ld_hist must be positive multiples of 32");
+    return fail(CS_ERR_INVALID, nm + ": ld_prefix / ld_hist must be positive multiples of 32");
   if (max_prefix_len < 0 || max_prefix_len > ld_prefix)
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: max_prefix_len outside [0, ld_prefix]");
+    return fail(CS_ERR_INVALID, nm + ": max_prefix_len outside [0, ld_prefix]");
   if (!q || !k_prefix || !vt_prefix || !prefix_off || !prefix_len || !k_hist || !vt_hist ||
-      !hist_base || !out)
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: NULL pointer");
-  if (!(scale > 0.0f) || softcap < 0.0f) return fail(CS_ERR_INVALID, "cs_prefix_attention: bad scale / softcap");
+      !hist_base || !out || (hist_rows == nullptr) != (nm == "cs_prefix_attention"))
+    return fail(CS_ERR_INVALID, nm + ": NULL pointer");
+  if (!(scale > 0.0f) || softcap < 0.0f) return fail(CS_ERR_INVALID, nm + ": bad scale / softcap");
   if (plan && (n_attn <= 0 || n_merge <= 0))
-    return fail(CS_ERR_INVALID, "cs_prefix_attention: a plan needs n_attn > 0 and n_merge > 0");
+    return fail(CS_ERR_INVALID, nm + ": a plan needs n_attn > 0 and n_merge > 0");
   if (plan && !workspace)
-    return fail(CS_ERR_WORKSPACE, "cs_prefix_attention: a plan needs the workspace "
-                                  "cs_prefix_attention_plan() sized");
+    return fail(CS_ERR_WORKSPACE, nm + ": a plan needs the workspace cs_prefix_attention_plan() sized");
   const int64_t M = static_cast<int64_t>(n_str) * T * (H / Hkv);
   const int64_t n_qg = (M + kGroupRows - 1) / kGroupRows;
   const int64_t base = static_cast<int64_t>(n_groups) * Hkv * n_qg;
-  if (n_qg > 0x7fffffff || base > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_prefix_attention: too many query rows");
+  if (n_qg > 0x7fffffff || base > 0x7fffffffLL) return fail(CS_ERR_INVALID, nm + ": too many query rows");
   AttnParams a;
   a.q = static_cast<const __bf16*>(q);
   a.kp = static_cast<const __bf16*>(k_prefix);
@@ -1314,6 +1414,7 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   a.kh = static_cast<const __bf16*>(k_hist);
   a.vth = static_cast<const __bf16*>(vt_hist);
   a.hist_base = hist_base;
+  a.hrow = hist_rows;
   a.out = static_cast<__bf16*>(out);
   a.part = static_cast<float*>(workspace);
   a.plan = static_cast<const int4*>(plan);
@@ -1339,7 +1440,9 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
   const dim3 merge_grid(static_cast<uint32_t>(plan ? n_merge : 0));
 #define CS_ATTN_LAUNCH(DV)                                                              \
   do {                                                                                  \
-    if (plan && attn_plan_lds())                                                        \
+    if (hist_rows)                                                                      \
+      hipLaunchKernelGGL((prefix_attn_plan_lds_kernel<DV, true>), grid, dim3(kAttnThreads), 0, st, a); \
+    else if (plan && attn_plan_lds())                                                        \
       hipLaunchKernelGGL(prefix_attn_plan_lds_kernel<DV>, grid, dim3(kAttnThreads), 0, st, a); \
     else if (plan)                                                                      \
       hipLaunchKernelGGL((prefix_attn_kernel<DV, true>), grid, dim3(kAttnThreads), 0, st, a); \
@@ -1358,7 +1461,40 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
     CS_ATTN_LAUNCH(256);
   }
 #undef CS_ATTN_LAUNCH
-  return check_launch("cs_prefix_attention");
+  return check_launch(name);
+}
+}  // namespace
+
+extern "C" {
+
+int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_prefix,
+                        int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
+                        int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                        const void* k_hist, const void* vt_hist, int64_t ld_hist,
+                        const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
+                        int32_t D, float scale, float softcap, int32_t window, const void* plan,
+                        int32_t n_attn, int32_t n_merge, void* out, void* workspace,
+                        size_t workspace_bytes, cs_stream_t stream) {
+  return prefix_attention_impl("cs_prefix_attention", q, k_prefix, vt_prefix, ld_prefix, prefix_off,
+                               prefix_len, max_prefix_len, group_prefix, n_groups, k_hist, vt_hist,
+                               nullptr, ld_hist, hist_base, n_str, T, H, Hkv, D, scale, softcap,
+                               window, plan, n_attn, n_merge, out, workspace, workspace_bytes, stream);
+}
+
+int cs_prefix_attention_rows(const void* q, const void* k_prefix, const void* vt_prefix,
+                             int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
+                             int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                             const void* k_hist, const void* v_hist, const int32_t* hist_rows,
+                             int64_t ld_hist, const int32_t* hist_base, int32_t n_str, int32_t T,
+                             int32_t H, int32_t Hkv, int32_t D, float scale, float softcap,
+                             int32_t window, const void* plan, int32_t n_attn, int32_t n_merge,
+                             void* out, void* workspace, size_t workspace_bytes, cs_stream_t stream) {
+  if (!hist_rows) return fail(CS_ERR_INVALID, "cs_prefix_attention_rows: NULL hist_rows");
+  return prefix_attention_impl("cs_prefix_attention_rows", q, k_prefix, vt_prefix, ld_prefix,
+                               prefix_off, prefix_len, max_prefix_len, group_prefix, n_groups,
+                               k_hist, v_hist, hist_rows, ld_hist, hist_base, n_str, T, H, Hkv, D,
+                               scale, softcap, window, plan, n_attn, n_merge, out, workspace,
+                               workspace_bytes, stream);
 }
 
 #ifdef CS_TRACE_ATTN
@@ -1408,6 +1544,20 @@ int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
                             S_src, S_dst, Hkv, ld_hist, D, stream);
 }
 
+int cs_hist_rows_update(const int32_t* src_rows, int32_t* dst_rows, const int64_t* parent,
+                        const int32_t* hist_base, int64_t S, int32_t ld_hist, cs_stream_t stream) {
+  if (S < 0 || ld_hist <= 0) return fail(CS_ERR_INVALID, "cs_hist_rows_update: bad shape");
+  if (S == 0) return CS_OK;
+  if (!src_rows || !dst_rows || !parent || !hist_base)
+    return fail(CS_ERR_INVALID, "cs_hist_rows_update: NULL pointer");
+  if (src_rows == dst_rows) return fail(CS_ERR_INVALID, "cs_hist_rows_update: source and destination must differ");
+  if (S > 0x7fffffffLL || (S * ld_hist + 255) / 256 > 0x7fffffffLL)
+    return fail(CS_ERR_INVALID, "cs_hist_rows_update: table too large");
+  hipLaunchKernelGGL(hist_rows_kernel, dim3(static_cast<uint32_t>((S * ld_hist + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), src_rows, dst_rows, parent, hist_base, S, ld_hist);
+  return check_launch("cs_hist_rows_update");
+}
+
 }  // extern "C"
 
 namespace {
@@ -1415,7 +1565,7 @@ int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t 
                     const float* inv_freq, const int32_t* prefix_len, const int32_t* group_prefix,
                     int32_t n_groups, const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
                     int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
-                    int64_t ld_hist, cs_stream_t stream);
+                    int64_t ld_hist, int32_t v_rows, cs_stream_t stream);
 }  // namespace
 
 extern "C" {
@@ -1426,7 +1576,17 @@ int cs_rope_place(const void* qkv, int64_t ld_qkv, const float* inv_freq, const 
                   void* k_hist, void* vt_hist, int64_t ld_hist, cs_stream_t stream) {
   if (!qkv) return fail(CS_ERR_INVALID, "cs_rope_place: NULL pointer");
   return rope_place_impl(qkv, ld_qkv, nullptr, 1, inv_freq, prefix_len, group_prefix, n_groups,
-                         hist_base, n_str, T, H, Hkv, D, q_out, k_hist, vt_hist, ld_hist, stream);
+                         hist_base, n_str, T, H, Hkv, D, q_out, k_hist, vt_hist, ld_hist, 0, stream);
+}
+
+int cs_rope_place_rows(const void* qkv, int64_t ld_qkv, const float* inv_freq,
+                       const int32_t* prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                       const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
+                       int32_t D, void* q_out, void* k_hist, void* v_hist, int64_t ld_hist,
+                       cs_stream_t stream) {
+  if (!qkv) return fail(CS_ERR_INVALID, "cs_rope_place_rows: NULL pointer");
+  return rope_place_impl(qkv, ld_qkv, nullptr, 1, inv_freq, prefix_len, group_prefix, n_groups,
+                         hist_base, n_str, T, H, Hkv, D, q_out, k_hist, v_hist, ld_hist, 1, stream);
 }
 
 int cs_rope_place_splitk(const float* part, int32_t splits, const float* inv_freq,
@@ -1440,7 +1600,21 @@ int cs_rope_place_splitk(const float* part, int32_t splits, const float* inv_fre
     return fail(CS_ERR_INVALID, "cs_rope_place_splitk: partials 16-byte aligned, head_dim % 16 == 0");
   return rope_place_impl(nullptr, static_cast<int64_t>(H + 2 * Hkv) * D, part, splits, inv_freq,
                          prefix_len, group_prefix, n_groups, hist_base, n_str, T, H, Hkv, D, q_out,
-                         k_hist, vt_hist, ld_hist, stream);
+                         k_hist, vt_hist, ld_hist, 0, stream);
+}
+
+int cs_rope_place_splitk_rows(const float* part, int32_t splits, const float* inv_freq,
+                              const int32_t* prefix_len, const int32_t* group_prefix,
+                              int32_t n_groups, const int32_t* hist_base, int32_t n_str, int32_t T,
+                              int32_t H, int32_t Hkv, int32_t D, void* q_out, void* k_hist,
+                              void* v_hist, int64_t ld_hist, cs_stream_t stream) {
+  if (!part || splits < 1) return fail(CS_ERR_INVALID, "cs_rope_place_splitk_rows: need partials, splits >= 1");
+  if (T >= 32) return fail(CS_ERR_INVALID, "cs_rope_place_splitk_rows: T < 32 only (fold first for chunks)");
+  if (reinterpret_cast<uintptr_t>(part) % 16 || D % 16)
+    return fail(CS_ERR_INVALID, "cs_rope_place_splitk_rows: partials 16-byte aligned, head_dim % 16 == 0");
+  return rope_place_impl(nullptr, static_cast<int64_t>(H + 2 * Hkv) * D, part, splits, inv_freq,
+                         prefix_len, group_prefix, n_groups, hist_base, n_str, T, H, Hkv, D, q_out,
+                         k_hist, v_hist, ld_hist, 1, stream);
 }
 
 }  // extern "C"
@@ -1450,7 +1624,7 @@ int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t 
                     const float* inv_freq, const int32_t* prefix_len, const int32_t* group_prefix,
                     int32_t n_groups, const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
                     int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
-                    int64_t ld_hist, cs_stream_t stream) {
+                    int64_t ld_hist, int32_t v_rows, cs_stream_t stream) {
   if (n_groups < 0 || n_str < 0 || T < 0) return fail(CS_ERR_INVALID, "cs_rope_place: negative size");
   if (n_groups == 0 || n_str == 0 || T == 0) return CS_OK;
   if (H <= 0 || Hkv <= 0 || D <= 0 || D % 2 != 0 || ld_qkv < static_cast<int64_t>(H + 2 * Hkv) * D)
@@ -1471,6 +1645,7 @@ int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t 
   r.kh = static_cast<__bf16*>(k_hist);
   r.vth = static_cast<__bf16*>(vt_hist);
   r.ldh = ld_hist;
+  r.v_rows = v_rows;
   r.n_tok = static_cast<int64_t>(n_groups) * n_str * T;
   r.n_str = n_str;
   r.T = T;
@@ -1484,7 +1659,7 @@ int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t 
   const int64_t n_vwg = static_cast<int64_t>(n_groups) * n_str * Hkv * n_tiles;
   {
     const char* e = getenv("CS_ROPE_VTILE");
-    r.skip_v = (!part && T >= 32 && ld_hist % 32 == 0 && ld_qkv % 8 == 0 &&
+    r.skip_v = (!part && !v_rows && T >= 32 && ld_hist % 32 == 0 && ld_qkv % 8 == 0 &&
                 reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && n_vwg <= 0x7fffffffLL &&
                 !(e && atoi(e) == 0)) ? 1 : 0;
   }
@@ -1495,8 +1670,14 @@ int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t 
   const int64_t n_split = (n_items + kRopeItems - 1) / kRopeItems;
   if (r.n_tok * n_split > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_rope_place: too many tokens");
   const dim3 grid(static_cast<uint32_t>(r.n_tok * n_split));
-  if (part)
-    hipLaunchKernelGGL((rope_place_kernel<8, true>), grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+  if (part && splits <= 2)
+    hipLaunchKernelGGL((rope_place_kernel<8, true, 2>), grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+                       r, static_cast<int32_t>(n_split));
+  else if (part && splits <= 4)
+    hipLaunchKernelGGL((rope_place_kernel<8, true, 4>), grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+                       r, static_cast<int32_t>(n_split));
+  else if (part)
+    hipLaunchKernelGGL((rope_place_kernel<8, true, 8>), grid, dim3(256), 0, static_cast<hipStream_t>(stream),
                        r, static_cast<int32_t>(n_split));
   else if (p8)
     hipLaunchKernelGGL(rope_place_kernel<8>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), r,

@@ -713,11 +713,16 @@ class DecodeState:
 
     Streams are prefix-major, s = p * n_beams + b, always n_beams of them per prefix (the
     caller pads missing beams with copies and ignores their candidates).  Every stream's
-    generated K/V lives in a preallocated history buffer [S, Hkv, ldh, D] (V transposed),
-    slot t = the token of step t; the prefix K/V is shared by the stream's n_beams
-    siblings through cs_prefix_attention.  ``advance`` = gather the parents' histories
-    (cs_hist_gather: the filled slots only, into the other half of a ping-pong pair), forward the new
-    tokens with hist_base = t read from device memory, keep the final-norm hidden.  After
+    generated K/V lives in a preallocated history buffer [S, Hkv, ldh, D], slot t = the
+    token of step t; the prefix K/V is shared by the stream's n_beams siblings through
+    cs_prefix_attention.  ``advance`` = inherit the parents' histories, forward the new
+    tokens with hist_base = t read from device memory, keep the final-norm hidden.  The
+    history is row-layout (K and V [S, Hkv, ldh, D]) behind a [S, ldh] slot table: slot t of
+    stream s is row rows[s, t], written once by the step that made it and never moved; a
+    step's inheritance is one table update (cs_hist_rows_update, a ping-pong pair of tables)
+    and the attention gathers through it (cs_prefix_attention_rows).  copy_history=True (or
+    CS_HIST_COPY=1): the round-4 form, V in 32-key V^T tiles and the parents' filled slots
+    copied into the other half of a ping-pong pair of buffers (cs_hist_gather).  After
     the first (eager) advance each parity's step is captured once in a hipGraph and
     replayed, so a decode step costs one graph launch plus its inputs' copies; ``post``
     (optional, fixed per state) is captured with it, e.g. the LM head + the fused
@@ -728,7 +733,7 @@ class DecodeState:
     stream per step."""
 
     def __init__(self, engine: "ScoringEngine", cache, n_prefix: int, n_beams: int,
-                 max_steps: int, use_graphs: bool = True):
+                 max_steps: int, use_graphs: bool = True, copy_history: Optional[bool] = None):
         """cache: a StreamPrefix (engine.prefill_streams) or a PrefixCache (re-laid)."""
         self.e = engine
         m = engine.model
@@ -740,6 +745,10 @@ class DecodeState:
         self.ldh = _ceil32(max_steps)
         self.max_steps = int(max_steps)
 
+        if copy_history is None:
+            copy_history = os.environ.get("CS_HIST_COPY") == "1"
+        self.copy_history = bool(copy_history)
+
         def buffers():
             # all layers in one tensor each, so a step's parent gather is 2 launches, not 2L
             return (torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
@@ -747,7 +756,15 @@ class DecodeState:
                     torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh // 32, c.head_dim, 32,
                                 dtype=m.dtype, device=dev))
 
-        self.hist = [buffers(), buffers()]
+        if self.copy_history:
+            self.hist = [buffers(), buffers()]
+            self.rows = None
+        else:
+            kv = torch.zeros(2, c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
+                             dtype=m.dtype, device=dev)
+            self.hist = [(kv[0], kv[1])] * 2
+            self.rows = [torch.arange(self.S, dtype=torch.int32, device=dev)[:, None]
+                         .expand(self.S, self.ldh).contiguous() for _ in range(2)]
         self.cur = 0
         self.steps = 0                                   # tokens appended so far (host copy)
         self.hist_base = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -775,11 +792,16 @@ class DecodeState:
 
     def _body(self, post) -> None:
         m = self.e.model
-        old_k, old_v = self.hist[self.cur]
         new_k, new_v = self.hist[1 - self.cur]
-        ops.hist_gather(old_k, new_k, old_v, new_v, self.src, self.hist_base)
+        rows = None
+        if self.rows is not None:
+            rows = self.rows[1 - self.cur]
+            ops.hist_rows_update(self.rows[self.cur], rows, self.src, self.hist_base)
+        else:
+            old_k, old_v = self.hist[self.cur]
+            ops.hist_gather(old_k, new_k, old_v, new_v, self.src, self.hist_base)
         h = m.forward_streams(self.tok, self.pfx, list(new_k.unbind(0)), list(new_v.unbind(0)),
-                              self.hist_base, self.B, 1)
+                              self.hist_base, self.B, 1, hist_rows=rows)
         self.hidden.copy_(h)
         self.hist_base += 1
         if post is not None:

@@ -458,7 +458,8 @@ class Model:
     def forward_streams(self, tokens: torch.Tensor, pfx, hist_k: List[torch.Tensor],
                         hist_vt: List[torch.Tensor], hist_base: torch.Tensor, n_str: int, T: int,
                         group_prefix: Optional[torch.Tensor] = None,
-                        group_prefix_host: Optional[Sequence[int]] = None) -> torch.Tensor:
+                        group_prefix_host: Optional[Sequence[int]] = None,
+                        hist_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """T new tokens for each of S = n_groups * n_str streams (tokens [S*T], stream-major):
         stream s = i * n_str + b attends to its group's prefix (pfx: engine.FusedPrefix, the
         ragged layouts of include/consensus_scoring.h cs_prefix_attention; group i uses
@@ -468,7 +469,9 @@ class Model:
         cs_rope_place, cs_prefix_attention, output GEMM, MLP.  No host synchronisation and
         no shape depends on hist_base: a decode step is graph-capturable.  Returns the
         final-norm hidden [S*T, d].  pfx.lens_host (+ group_prefix_host) size the key splits
-        of the attention work plan."""
+        of the attention work plan.  hist_rows [S, ldh] int32: a row-layout history
+        (hist_vt[layer] is V [S, Hkv, ldh, D] like K; slot j of stream s in row hist_rows[s, j]:
+        cs_prefix_attention_rows / cs_rope_place_rows)."""
         from . import ops   # local: model.py stays importable without the library
         c = self.cfg
         H, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
@@ -495,14 +498,15 @@ class Model:
                              fold=T >= 32 or c.head_dim % 16 != 0 or not _FOLD_IN_ROPE)
             q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
             ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
-                           hist_k[i], hist_vt[i], group_prefix=group_prefix)
+                           hist_k[i], hist_vt[i], group_prefix=group_prefix,
+                           v_rows=hist_rows is not None)
             o = ops.prefix_attention(q, pfx.k[i], pfx.vt[i], pfx.off, pfx.lengths, pfx.max_len,
                                      hist_k[i], hist_vt[i], hist_base, n_str, T, scale=scale,
                                      softcap=c.attn_softcap,
                                      window=c.sliding_window if i % 2 == 0 else 0,
                                      group_prefix=group_prefix,
                                      prefix_len_host=getattr(pfx, "lens_host", None),
-                                     group_prefix_host=group_prefix_host)
+                                     group_prefix_host=group_prefix_host, hist_rows=hist_rows)
             o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"], packed=wp.get(p + "wo"),
                            fold=not _FOLD_IN_NORM)
             # Gemma-2's post-attention / post-MLP norms of the branch ride in the residual

@@ -543,9 +543,12 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
                      group_prefix: Optional[torch.Tensor] = None,
                      prefix_len_host: Optional[Sequence[int]] = None,
                      group_prefix_host: Optional[Sequence[int]] = None,
-                     out: Optional[torch.Tensor] = None, plan: Optional[AttnPlan] = None):
+                     out: Optional[torch.Tensor] = None, plan: Optional[AttnPlan] = None,
+                     hist_rows: Optional[torch.Tensor] = None):
     """Cascade attention of candidate streams over shared per-agent prefix K/V
-    (cs_prefix_attention; layouts in include/consensus_scoring.h).
+    (cs_prefix_attention; layouts in include/consensus_scoring.h).  hist_rows [S, ldh] int32:
+    the history is row-layout (vt_hist is V [S, Hkv, ldh, D] like k_hist) and slot j of
+    stream s lives in row hist_rows[s, j] (cs_prefix_attention_rows: beams without copies).
 
     q [n_groups*n_str*T, H, D] bf16; k_prefix [Hkv, Lp, D], vt_prefix [Hkv, Lp/32, D, 32]
     (ragged prefixes: prefix p's keys are rows prefix_off[p] ..; V transposed in 32-key
@@ -564,8 +567,14 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     S, Hkv2, ldh, Dh = k_hist.shape
     if Dk != D or Dh != D or Hkv2 != Hkv:
         raise CSError("head layout mismatch between q, k_prefix and k_hist")
+    if hist_rows is not None:
+        if tuple(vt_hist.shape) != (S, Hkv, ldh, D):
+            raise CSError("row-layout history: V [S, Hkv, ldh, D] like K expected")
+        if hist_rows.dtype != torch.int32 or tuple(hist_rows.shape) != (S, ldh) or \
+                not hist_rows.is_contiguous():
+            raise CSError("hist_rows must be a contiguous int32 [S, ldh] tensor")
     if tuple(vt_prefix.shape) != (Hkv, Lp // 32, D, 32) or \
-            tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32):
+            (hist_rows is None and tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32)):
         raise CSError("vt_prefix [Hkv, Lp/32, D, 32] / vt_hist [S, Hkv, ldh/32, D, 32] "
                       "(V^T in 32-key tiles) expected")
     for t in (k_prefix, vt_prefix, k_hist, vt_hist):
@@ -585,7 +594,7 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     if hist_base.dtype != torch.int32 or hist_base.numel() != 1:
         raise CSError("hist_base must be a one-element int32 device tensor")
     _require_cuda(q, k_prefix, vt_prefix, prefix_off, prefix_len, k_hist, vt_hist, hist_base,
-                  group_prefix, out)
+                  group_prefix, out, hist_rows)
     if out is None:
         out = torch.empty_like(q)
     mpl = int(max_prefix_len)
@@ -602,16 +611,25 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     else:
         _retain(plan)
     ws = plan.workspace
+    gp = group_prefix.data_ptr() if group_prefix is not None else None
+    pe = plan.entries.data_ptr() if plan.entries is not None else None
+    wsp, wsn = (ws.data_ptr(), ws.numel()) if ws is not None else (None, 0)
+    if hist_rows is not None:
+        rc = L.cs_prefix_attention_rows(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), Lp,
+                                        prefix_off.data_ptr(), prefix_len.data_ptr(), mpl, gp,
+                                        n_groups, k_hist.data_ptr(), vt_hist.data_ptr(),
+                                        hist_rows.data_ptr(), ldh, hist_base.data_ptr(), n_str, T,
+                                        H, Hkv, D, float(scale), float(softcap), int(window), pe,
+                                        plan.n_attn, plan.n_merge, out.data_ptr(), wsp, wsn,
+                                        _stream())
+        _lib.check(rc, "cs_prefix_attention_rows")
+        return out
     rc = L.cs_prefix_attention(q.data_ptr(), k_prefix.data_ptr(), vt_prefix.data_ptr(), Lp,
-                               prefix_off.data_ptr(), prefix_len.data_ptr(), mpl,
-                               group_prefix.data_ptr() if group_prefix is not None else None,
+                               prefix_off.data_ptr(), prefix_len.data_ptr(), mpl, gp,
                                n_groups, k_hist.data_ptr(), vt_hist.data_ptr(), ldh,
                                hist_base.data_ptr(), n_str, T, H, Hkv, D, float(scale),
-                               float(softcap), int(window),
-                               plan.entries.data_ptr() if plan.entries is not None else None,
-                               plan.n_attn, plan.n_merge, out.data_ptr(),
-                               ws.data_ptr() if ws is not None else None,
-                               ws.numel() if ws is not None else 0, _stream())
+                               float(softcap), int(window), pe, plan.n_attn, plan.n_merge,
+                               out.data_ptr(), wsp, wsn, _stream())
     _lib.check(rc, "cs_prefix_attention")
     return out
 
@@ -619,11 +637,14 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
 def rope_place(qkv: "torch.Tensor | SplitPartials", inv_freq: torch.Tensor, prefix_len: torch.Tensor,
                hist_base: torch.Tensor, n_str: int, T: int, H: int, Hkv: int, D: int,
                q_out: torch.Tensor, k_hist: torch.Tensor, vt_hist: torch.Tensor, *,
-               group_prefix: Optional[torch.Tensor] = None) -> torch.Tensor:
+               group_prefix: Optional[torch.Tensor] = None, v_rows: bool = False) -> torch.Tensor:
     """RoPE of the fused projection + placement of q / the new K, V (cs_rope_place).  qkv
     may be a K-split GEMM's unfolded SplitPartials (T < 32): folded inside the launch
-    (cs_rope_place_splitk), bitwise the folded projection."""
+    (cs_rope_place_splitk), bitwise the folded projection.  v_rows: vt_hist is a row-layout
+    V [S, Hkv, ldh, D] (cs_rope_place_rows, the cs_prefix_attention_rows history)."""
     L = _lib.load()
+    vshape = (lambda S, ldh: (S, Hkv, ldh, D)) if v_rows else (lambda S, ldh: (S, Hkv, ldh // 32, D, 32))
+    sfx = "_rows" if v_rows else ""
     if isinstance(qkv, SplitPartials):
         part = qkv.part
         S, Hkv2, ldh, Dk = k_hist.shape
@@ -631,26 +652,26 @@ def rope_place(qkv: "torch.Tensor | SplitPartials", inv_freq: torch.Tensor, pref
         if (part.dim() != 3 or part.dtype != torch.float32 or not part.is_contiguous()
                 or part.shape[2] != (H + 2 * Hkv) * D):
             raise CSError("qkv partials must be contiguous float32 [splits, n_tok, (H + 2 Hkv) D]")
-        if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32):
+        if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != vshape(S, ldh):
             raise CSError("k_hist [S, Hkv, ldh, D] / vt_hist [S, Hkv, ldh/32, D, 32] layout mismatch")
         if n_tok != S * T or S % n_str != 0:
             raise CSError("qkv rows must be streams x T")
         if tuple(q_out.shape) != (n_tok, H, D) or q_out.dtype != torch.bfloat16 or not q_out.is_contiguous():
             raise CSError("q_out must be a contiguous [n_tok, H, D] bfloat16 tensor")
         _require_cuda(part, inv_freq, prefix_len, hist_base, q_out, k_hist, vt_hist, group_prefix)
-        rc = L.cs_rope_place_splitk(part.data_ptr(), part.shape[0], inv_freq.data_ptr(),
+        rc = getattr(L, "cs_rope_place_splitk" + sfx)(part.data_ptr(), part.shape[0], inv_freq.data_ptr(),
                                     prefix_len.data_ptr(),
                                     group_prefix.data_ptr() if group_prefix is not None else None,
                                     S // n_str, hist_base.data_ptr(), n_str, T, H, Hkv, D,
                                     q_out.data_ptr(), k_hist.data_ptr(), vt_hist.data_ptr(), ldh,
                                     _stream())
-        _lib.check(rc, "cs_rope_place_splitk")
+        _lib.check(rc, "cs_rope_place_splitk" + sfx)
         return q_out
     if qkv.dim() != 2 or qkv.dtype != torch.bfloat16 or qkv.stride(1) != 1:
         raise CSError("qkv must be a 2-D bfloat16 tensor with unit column stride")
     n_tok = qkv.shape[0]
     S, Hkv2, ldh, Dk = k_hist.shape
-    if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32):
+    if Hkv2 != Hkv or Dk != D or tuple(vt_hist.shape) != vshape(S, ldh):
         raise CSError("k_hist [S, Hkv, ldh, D] / vt_hist [S, Hkv, ldh/32, D, 32] layout mismatch")
     if n_tok != S * T or S % n_str != 0:
         raise CSError("qkv rows must be streams x T")
@@ -660,11 +681,11 @@ def rope_place(qkv: "torch.Tensor | SplitPartials", inv_freq: torch.Tensor, pref
         raise CSError("inv_freq must be float32 [D/2]")
     _require_cuda(qkv, inv_freq, prefix_len, hist_base, q_out, k_hist, vt_hist, group_prefix)
     ld = qkv.stride(0) if n_tok > 1 else qkv.shape[1]
-    rc = L.cs_rope_place(qkv.data_ptr(), ld, inv_freq.data_ptr(), prefix_len.data_ptr(),
+    rc = getattr(L, "cs_rope_place" + sfx)(qkv.data_ptr(), ld, inv_freq.data_ptr(), prefix_len.data_ptr(),
                          group_prefix.data_ptr() if group_prefix is not None else None,
                          S // n_str, hist_base.data_ptr(), n_str, T, H, Hkv, D, q_out.data_ptr(),
                          k_hist.data_ptr(), vt_hist.data_ptr(), ldh, _stream())
-    _lib.check(rc, "cs_rope_place")
+    _lib.check(rc, "cs_rope_place" + sfx)
     return q_out
 
 
@@ -1034,6 +1055,24 @@ def tree_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
                            _stream())
     _lib.check(rc, "cs_tree_gather")
 
+
+
+def hist_rows_update(src_rows: torch.Tensor, dst_rows: torch.Tensor, parent: torch.Tensor,
+                     hist_base: torch.Tensor) -> None:
+    """dst_rows[s, j] = src_rows[parent[s], j] for j < hist_base, else s
+    (cs_hist_rows_update): a row-layout history's beam step, no K / V moved."""
+    L_ = _lib.load()
+    if src_rows.dtype != torch.int32 or dst_rows.dtype != torch.int32 or \
+            src_rows.shape != dst_rows.shape or src_rows.dim() != 2 or \
+            not src_rows.is_contiguous() or not dst_rows.is_contiguous():
+        raise CSError("slot tables must be contiguous int32 [S, ldh] tensors of one shape")
+    S, ldh = src_rows.shape
+    if parent.dtype != torch.int64 or parent.numel() != S or hist_base.dtype != torch.int32:
+        raise CSError("parent must be int64 [S], hist_base int32 [1]")
+    _require_cuda(src_rows, dst_rows, parent, hist_base)
+    rc = L_.cs_hist_rows_update(src_rows.data_ptr(), dst_rows.data_ptr(), parent.data_ptr(),
+                                hist_base.data_ptr(), S, ldh, _stream())
+    _lib.check(rc, "cs_hist_rows_update")
 
 def blocked_vt(v: torch.Tensor) -> torch.Tensor:
     """V rows [..., keys, D] (keys a multiple of 32) -> the kernels' V^T in 32-key tiles

@@ -320,6 +320,31 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
                         size_t workspace_bytes, cs_stream_t stream);
 
 /*
+ * cs_prefix_attention_rows — cs_prefix_attention over a ROW-LAYOUT history reached through a
+ * slot table, for beam decoding without history copies:
+ *     k_hist, v_hist  [S][Hkv][ld_hist][D] (V row-major like K, not in 32-key V^T tiles)
+ *     hist_rows       [S][ld_hist] int32: slot j of stream s is row hist_rows[s][j] of k_hist /
+ *                     v_hist (0 <= hist_rows[s][j] < S for every j < ld_hist)
+ * so a beam's inherited slots stay where its ancestor wrote them (cs_hist_rows_update builds
+ * the next step's table; cs_rope_place_rows writes the step's K / V into the stream's own row).
+ * Same arguments, plan and results otherwise (plan may be NULL with no workspace: one
+ * workgroup per (group, K/V head, query group)).  Every result equals cs_prefix_attention on
+ * the copied history the table describes, up to fp32 reassociation (the same block order:
+ * bitwise in practice).
+ *
+ * Replaces: as cs_prefix_attention; the beam's history is the reference's beam text
+ *   (src/methods/beam_search.py:491-538), re-encoded in full by every call there.
+ */
+int cs_prefix_attention_rows(const void* q, const void* k_prefix, const void* vt_prefix,
+                             int64_t ld_prefix, const int64_t* prefix_off, const int32_t* prefix_len,
+                             int32_t max_prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                             const void* k_hist, const void* v_hist, const int32_t* hist_rows,
+                             int64_t ld_hist, const int32_t* hist_base, int32_t n_str, int32_t T,
+                             int32_t H, int32_t Hkv, int32_t D, float scale, float softcap,
+                             int32_t window, const void* plan, int32_t n_attn, int32_t n_merge,
+                             void* out, void* workspace, size_t workspace_bytes, cs_stream_t stream);
+
+/*
  * cs_rope_place — rotary embedding (half-rotation convention, angle = position *
  * inv_freq[i]) of the fused projection qkv [(s*T + t)][ld_qkv] = [q (H*D) | k (Hkv*D) |
  * v (Hkv*D)] and placement into the cs_prefix_attention layouts: q_out [(s*T+t)][H][D],
@@ -349,6 +374,24 @@ int cs_rope_place_splitk(const float* part, int32_t splits, const float* inv_fre
                          const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H,
                          int32_t Hkv, int32_t D, void* q_out, void* k_hist, void* vt_hist,
                          int64_t ld_hist, cs_stream_t stream);
+
+/*
+ * cs_rope_place_rows / cs_rope_place_splitk_rows — cs_rope_place / cs_rope_place_splitk with
+ * V placed row-major like K: v_hist[s][g][j][:] (the cs_prefix_attention_rows layout), in the
+ * stream's own row s.
+ *
+ * Replaces: as cs_rope_place (src/utils.py:249-259).
+ */
+int cs_rope_place_rows(const void* qkv, int64_t ld_qkv, const float* inv_freq,
+                       const int32_t* prefix_len, const int32_t* group_prefix, int32_t n_groups,
+                       const int32_t* hist_base, int32_t n_str, int32_t T, int32_t H, int32_t Hkv,
+                       int32_t D, void* q_out, void* k_hist, void* v_hist, int64_t ld_hist,
+                       cs_stream_t stream);
+int cs_rope_place_splitk_rows(const float* part, int32_t splits, const float* inv_freq,
+                              const int32_t* prefix_len, const int32_t* group_prefix,
+                              int32_t n_groups, const int32_t* hist_base, int32_t n_str, int32_t T,
+                              int32_t H, int32_t Hkv, int32_t D, void* q_out, void* k_hist,
+                              void* v_hist, int64_t ld_hist, cs_stream_t stream);
 
 /*
  * cs_hist_gather — beam reordering of the per-stream K/V history (the cs_prefix_attention
@@ -383,6 +426,18 @@ int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
 int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
                    const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S_src,
                    int64_t S_dst, int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
+
+/*
+ * cs_hist_rows_update — the beam step of a row-layout history (cs_prefix_attention_rows):
+ *     dst_rows[s][j] = src_rows[parent[s]][j]   j < *hist_base   (inherited slots, by table)
+ *     dst_rows[s][j] = s                        j >= *hist_base  (written by this and later steps)
+ * [S][ld_hist] int32 tables, src and dst distinct (a ping-pong pair, so a queued step can be
+ * undone); no K / V moves.  hist_base in device memory (graph replays).
+ *
+ * Replaces: as cs_hist_gather (src/methods/beam_search.py:491-538).
+ */
+int cs_hist_rows_update(const int32_t* src_rows, int32_t* dst_rows, const int64_t* parent,
+                        const int32_t* hist_base, int64_t S, int32_t ld_hist, cs_stream_t stream);
 
 /*
  * cs_add_rms_norm — residual add + RMSNorm of bf16 rows in one pass:

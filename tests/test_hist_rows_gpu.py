@@ -1,0 +1,188 @@
+"""GPU parity of the copy-free beam history (row-layout K / V behind a slot table):
+cs_prefix_attention_rows against cs_prefix_attention on the history the table describes,
+materialised by copying (bit for bit under the same work plan), and against the fp32
+reference attention; cs_hist_rows_update against its numpy restatement; cs_rope_place_rows
+against cs_rope_place (the same K and the V rows of its V^T tiles); and a DecodeState on the
+row history against one that copies its parents' slots every step (cs_hist_gather).
+
+What it replaces: the reference's beams are strings that every scoring call re-encodes
+(src/methods/beam_search.py:491-538 through src/utils.py:249-259): a kept beam's earlier
+tokens are recomputed per call there, inherited here -- before round 5 by copying the
+parent's filled slots each step, now by a table entry per slot."""
+import importlib
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from test_stream_attention_gpu import _ceil32, _fp32_twin, _ragged, _tiny, ref_attention
+
+pytestmark = pytest.mark.gpu
+
+PKG = "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd"
+
+ROWS_CASES = [
+    # n_prefix, n_str, T, H, Hkv, D, plens, hist_base, softcap, group map, window
+    (5, 4, 1, 32, 8, 64, [180, 201, 77, 160, 230], 3, 0.0, None, 0),      # C1-like (1B)
+    (3, 16, 1, 16, 8, 256, [90, 140, 33], 20, 50.0, None, 0),             # C3-like (Gemma-2)
+    (4, 8, 1, 64, 8, 128, [300, 12, 64, 250], 47, 0.0, None, 0),          # C5-like (rep 8)
+    (3, 2, 5, 8, 2, 64, [40, 64, 1], 2, 0.0, [2, 0, 0], 0),               # T > 1, group map
+    (2, 3, 1, 4, 4, 64, [31, 33], 0, 0.0, None, 0),                       # first step
+    (3, 8, 1, 16, 8, 256, [500, 64, 250], 30, 50.0, None, 100),           # sliding window
+    (2, 16, 1, 16, 8, 256, [260, 250], 95, 50.0, None, 0),                # 3 history blocks
+    (17, 8, 1, 64, 8, 128, [600] + [250 + 7 * i for i in range(16)], 49, 0.0, None, 0),
+]
+
+
+def _case_tensors(ops, dev, case):
+    n_prefix, n_str, T, H, Hkv, D, plens, hb, cap, gmap, window = case
+    g = torch.Generator(device="cpu").manual_seed(zlib.crc32(repr(case).encode()))
+    n_grp = len(gmap) if gmap is not None else n_prefix
+    S = n_grp * n_str
+    ldh = _ceil32(hb + T)
+    bf = torch.bfloat16
+
+    def rnd(*shape):
+        return torch.randn(*shape, generator=g).to(bf).to(dev)
+
+    q = rnd(S * T, H, D)
+    kps = [rnd(Hkv, n, D) for n in plens]
+    vps = [rnd(Hkv, n, D) for n in plens]
+    kflat, off = _ragged(kps, Hkv, D)
+    vflat, _ = _ragged(vps, Hkv, D)
+    # row-layout history and a slot table: inherited slots j < hb from random rows of the
+    # same or another stream, the step's own slots j >= hb in the stream's own row
+    kh, vh = rnd(S, Hkv, ldh, D), rnd(S, Hkv, ldh, D)
+    rows = torch.arange(S, dtype=torch.int32)[:, None].repeat(1, ldh)
+    rows[:, :hb] = torch.randint(0, S, (S, hb), generator=g, dtype=torch.int32)
+    rows = rows.to(dev)
+    idx = rows.long()
+    # the copied history the table describes: slot j of stream s = row rows[s, j]'s slot j
+    jj = torch.arange(ldh, device=dev)
+    kc = kh[idx, :, jj[None, :]].permute(0, 2, 1, 3).contiguous()   # [S, Hkv, ldh, D]
+    vc = vh[idx, :, jj[None, :]].permute(0, 2, 1, 3).contiguous()
+    t = dict(q=q, kflat=kflat, vtflat=ops.blocked_vt(vflat), kps=kps, vps=vps,
+             offt=torch.tensor(off, dtype=torch.int64, device=dev),
+             plen=torch.tensor(plens, dtype=torch.int32, device=dev),
+             hbt=torch.tensor([hb], dtype=torch.int32, device=dev),
+             gp=torch.tensor(gmap, dtype=torch.int32, device=dev) if gmap is not None else None,
+             kh=kh, vh=vh, rows=rows, kc=kc, vc=vc)
+    return t
+
+
+@pytest.mark.parametrize("case", ROWS_CASES)
+def test_prefix_attention_rows_equals_copied_history(ops, dev, case):
+    n_prefix, n_str, T, H, Hkv, D, plens, hb, cap, gmap, window = case
+    t = _case_tensors(ops, dev, case)
+    scale = D ** -0.5 * (4.0 if cap else 1.0)
+
+    def run(kh, vh, rows=None, **kw):
+        return ops.prefix_attention(t["q"], t["kflat"], t["vtflat"], t["offt"], t["plen"],
+                                    max(plens), kh, vh, t["hbt"], n_str, T, scale=scale,
+                                    softcap=cap, window=window, group_prefix=t["gp"],
+                                    prefix_len_host=plens, group_prefix_host=gmap,
+                                    hist_rows=rows, **kw)
+
+    out_rows = run(t["kh"], t["vh"], t["rows"])
+    out_copy = run(t["kc"], ops.blocked_vt(t["vc"]))
+    plain = run(t["kh"], t["vh"], t["rows"], plan=ops.AttnPlan(None, 0, 0, None))
+    torch.cuda.synchronize()
+    plan = ops.attention_plan(plens, gmap, t["q"].shape[0] // (T * n_str), n_str, T, H, Hkv, D,
+                              t["kh"].shape[2], dev)
+    if plan.entries is not None:
+        # one work plan, one key-block order: the table changes only where keys come from
+        assert torch.equal(out_rows, out_copy)
+    Pm = max(plens)
+    kp = torch.zeros(n_prefix, Hkv, Pm, D, dtype=torch.bfloat16, device=dev)
+    vp = torch.zeros_like(kp)
+    for i, (k, v) in enumerate(zip(t["kps"], t["vps"])):
+        kp[i, :, :k.shape[1]] = k
+        vp[i, :, :v.shape[1]] = v
+    ref = ref_attention(t["q"], kp, vp, plens, t["kc"], t["vc"], hb, n_str, T, scale, cap, gmap,
+                        window)
+    bound = 2e-2 + 2e-2 * ref.abs()
+    for name, o in (("rows", out_rows), ("copy", out_copy), ("rows, no plan", plain)):
+        err = (o.float() - ref).abs()
+        assert bool((err <= bound).all()), f"{name}: max err {float(err.max()):.3e}"
+    assert torch.equal(out_rows, run(t["kh"], t["vh"], t["rows"]))   # deterministic relaunch
+
+
+@pytest.mark.parametrize("S,ldh,hb", [(5, 32, 7), (256, 64, 33), (512, 64, 0), (16, 32, 32)])
+def test_hist_rows_update_matches_numpy(ops, dev, S, ldh, hb):
+    g = np.random.default_rng(S + ldh + hb)
+    src = g.integers(0, S, (S, ldh)).astype(np.int32)
+    parent = g.integers(0, S, S).astype(np.int64)
+    dst = torch.full((S, ldh), -7, dtype=torch.int32, device=dev)
+    ops.hist_rows_update(torch.from_numpy(src).to(dev), dst, torch.from_numpy(parent).to(dev),
+                         torch.tensor([hb], dtype=torch.int32, device=dev))
+    want = np.repeat(np.arange(S, dtype=np.int32)[:, None], ldh, axis=1)
+    want[:, :hb] = src[parent, :hb]
+    assert np.array_equal(dst.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("D,H,Hkv,T,splits", [(64, 8, 2, 1, 0), (128, 32, 8, 1, 4),
+                                               (256, 16, 8, 2, 8), (256, 16, 8, 1, 0)])
+def test_rope_place_rows_is_rope_place_with_v_rows(ops, dev, D, H, Hkv, T, splits):
+    M = importlib.import_module(PKG + ".model")
+    cfg = M.preset("tiny-llama", head_dim=D, n_heads=H, n_kv_heads=Hkv)
+    inv = M.rope_inv_freq(cfg, dev)
+    g = torch.Generator(device="cpu").manual_seed(D + H + T)
+    n_prefix, n_str = 3, 2
+    S = n_prefix * n_str
+    hb = 37
+    ldh = _ceil32(hb + T)
+    width = (H + 2 * Hkv) * D
+    plen = torch.tensor([17, 250, 1000], dtype=torch.int32, device=dev)
+    hbt = torch.tensor([hb], dtype=torch.int32, device=dev)
+    if splits:
+        src = ops.SplitPartials(torch.randn(splits, S * T, width, generator=g).to(dev))
+    else:
+        src = torch.randn(S * T, width, generator=g).to(torch.bfloat16).to(dev)
+    q1 = torch.empty(S * T, H, D, dtype=torch.bfloat16, device=dev)
+    q2 = torch.empty_like(q1)
+    k1 = torch.zeros(S, Hkv, ldh, D, dtype=torch.bfloat16, device=dev)
+    k2 = torch.zeros_like(k1)
+    vt1 = torch.zeros(S, Hkv, ldh // 32, D, 32, dtype=torch.bfloat16, device=dev)
+    v2 = torch.zeros(S, Hkv, ldh, D, dtype=torch.bfloat16, device=dev)
+    ops.rope_place(src, inv, plen, hbt, n_str, T, H, Hkv, D, q1, k1, vt1)
+    ops.rope_place(src, inv, plen, hbt, n_str, T, H, Hkv, D, q2, k2, v2, v_rows=True)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2) and torch.equal(k1, k2)
+    assert torch.equal(ops.rows_from_blocked(vt1), v2)
+    assert v2[:, :, :hb].abs().sum() == 0 and v2[:, :, hb + T:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("family", ["llama3", "gemma2"])
+def test_decode_state_row_history_equals_copied_history(dev, family):
+    """The same beam walk (random parents, more steps than one 32-slot tile) on the row
+    history and on the copied one, both against the eager fp32 twin of the model: the row
+    history no further from fp32 than the copied one (the two may run different attention
+    work plans, so they agree to bf16 rounding, not bit for bit), and its graph replays
+    bit-identical to its eager run."""
+    E = importlib.import_module(PKG + ".engine")
+    eng = _tiny(family, dev)
+    e32 = _fp32_twin(eng)
+    g = torch.Generator().manual_seed(23)
+    prefixes = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (40, 23, 61)]
+    B, steps = 4, 36
+    cache = eng.prefill(prefixes)
+    ref = E.BeamState(e32, e32.prefill(prefixes), n_prefix=3)
+    rows = E.DecodeState(eng, cache, n_prefix=3, n_beams=B, max_steps=steps, copy_history=False)
+    rows_eager = E.DecodeState(eng, cache, n_prefix=3, n_beams=B, max_steps=steps,
+                               use_graphs=False, copy_history=False)
+    copy = E.DecodeState(eng, cache, n_prefix=3, n_beams=B, max_steps=steps, copy_history=True)
+    assert rows.rows is not None and copy.rows is None
+    V = eng.model.cfg.vocab
+    tgt = torch.randint(0, V, (3 * B, 16), generator=g).to(dev).to(torch.int32)
+    for step in range(steps):
+        parent = [0] * B if step == 0 else torch.randint(0, B, (B,), generator=g).tolist()
+        toks = torch.randint(5, 500, (B,), generator=g).tolist()
+        for st in (ref, rows, rows_eager, copy):
+            st.advance(parent, toks)
+        lp32 = e32.rows_logprobs(ref.next_hidden, tgt)
+        e_rows = float((eng.rows_logprobs(rows.hidden, tgt) - lp32).abs().max())
+        e_copy = float((eng.rows_logprobs(copy.hidden, tgt) - lp32).abs().max())
+        torch.cuda.synchronize()
+        assert e_rows <= 1.5 * e_copy + 1e-2, (step, e_rows, e_copy)
+        assert torch.equal(rows.hidden, rows_eager.hidden), step
