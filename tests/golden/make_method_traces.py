@@ -401,8 +401,11 @@ def main() -> None:
 
     if args.family == "main128":
         import math
-        assert all(v is None or math.isfinite(v) for e in out["evaluations"]
-                   for v in e["result"].values()), "an evaluation reaches past the tail"
+        # (the *_cosine welfares are NaN in every family: no embedding model here)
+        bad = [(e["statement"][:20], k, v) for e in out["evaluations"]
+               for k, v in e["result"].items()
+               if v is not None and not math.isfinite(v) and not k.endswith("_cosine")]
+        assert not bad, f"non-finite evaluation values: {bad}"
         backend.tail = None
 
     # text-compat scoring primitive (src/utils.py:201-373), incl. marker cases
