@@ -147,10 +147,12 @@ MAIN128_RUNS = [
 ]
 # echo log-probs of the prompt tail only (the LM head over these rows): beam search keeps
 # the last one (beam_search.py:389-390), the lookahead the path's last <= 4
-# (finite_lookahead.py:508-520); Best-of-N needs the user span (a <= 200-token candidate +
-# the chat frame's closing tokens); the evaluator every position (the reference's find() of a
-# short statement can land in the system prompt, src/utils.py:321-363)
-MAIN128_TAIL = {"beam_search": 8, "best_of_n": 320, "finite_lookahead": 16, "eval": None}
+# (finite_lookahead.py:508-520), and a recorded call keeps its span's last 6 -- all of them
+# before the chat frame's closing text, ~60 character tokens of the fixture's tokenizer;
+# Best-of-N needs the user span (a <= 200-token candidate + that frame); the evaluator every
+# position (the reference's find() of a short statement can land in the system prompt,
+# src/utils.py:321-363)
+MAIN128_TAIL = {"beam_search": 128, "best_of_n": 320, "finite_lookahead": 128, "eval": None}
 
 
 WIDE_AGENTS = 16
@@ -377,6 +379,10 @@ def main() -> None:
         with open(partial, "w") as f:
             json.dump(out["runs"], f)
 
+    if args.family == "main128":
+        import math
+        assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
+                   if v is not None), "a recorded tail reaches past the computed positions"
     if args.family in ("c1long", "fl4"):   # method runs only (no evaluator pass)
         import math
         assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
