@@ -149,7 +149,7 @@ def load():
     L.cs_rope_place_rows.restype = ctypes.c_int
     L.cs_rope_place_splitk_rows.argtypes = L.cs_rope_place_splitk.argtypes
     L.cs_rope_place_splitk_rows.restype = ctypes.c_int
-    L.cs_hist_rows_update.argtypes = [vp, vp, vp, vp, i64, i32, vp]
+    L.cs_hist_rows_update.argtypes = [vp, vp, vp, vp, i64, i32, i64, vp]
     L.cs_hist_rows_update.restype = ctypes.c_int
     _lib = L
     return L

@@ -95,6 +95,13 @@ __device__ __forceinline__ int logical_block(int swz) {
   return (b & 7) * per + (b >> 3);
 }
 
+// ROWS history V image: the chunk swizzle of key k (even, so 32-byte pairs stay whole; the
+// 8 keys of a half-wave's transposed read land in 8 different 8-bank groups)
+template <int D>
+__device__ __forceinline__ int vimg_swz(int k) {
+  return D == 64 ? 2 * ((k >> 1) & 3) : 2 * (k & 7);
+}
+
 // One 32-key block's operands for this lane: K rows kb + col and kb + 16 + col (8 bf16 of
 // each 32-wide d step), V^T rows (16-row d tiles) of the block's 32-key tile.
 template <int D>
@@ -684,6 +691,24 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
   // this split's prefix blocks: split, split + n_used, ...  (workgroup-uniform)
   const int npi = nbp > split ? (nbp - split + n_used - 1) / n_used : 0;
   ATT_T(if (tid == 0 && npi + hb + po >= 0) att_at(1);)
+  // the tile's own streams' history blocks, per wave (split * kw + ks, + nslot, ...)
+  const int rt0 = r0 + qt * 16, rt1 = min(rt0 + 15, M - 1);
+  const int b_lo = (rt0 / a.rep) / a.T, b_hi = (rt1 / a.rep) / a.T;
+  const int t_hi = b_lo == b_hi ? (rt1 / a.rep) % a.T : a.T - 1;
+  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
+  const int n_hist = (b_hi - b_lo + 1) * nbh;
+  const int nslot = n_used * kw;
+  // ROWS: lane l's table entry (key l % 32) of history block ih; the first block's entry is
+  // loaded here, its round trip hidden behind the prefix blocks, each later one during the
+  // block before it
+  auto hrow_of = [&](int ih) -> int32_t {
+    const int64_t sg = static_cast<int64_t>(gi) * a.n_str + b_lo + ih / nbh;
+    return a.hrow[sg * a.ldh + (ih % nbh) * kKeyBlock + (lane & 31)];
+  };
+  int32_t hcur = 0;
+  if constexpr (ROWS) {
+    if (active && split * kw + ks < n_hist) hcur = hrow_of(split * kw + ks);
+  }
 
   bf16x8 qf[NDS];
   {
@@ -761,13 +786,6 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
   }
 
   ATT_T(if (tid == 0) att_at(2);)
-  // ---- the tile's own streams' history blocks, per wave (split * kw + ks, + nslot, ...) ----
-  const int rt0 = r0 + qt * 16, rt1 = min(rt0 + 15, M - 1);
-  const int b_lo = (rt0 / a.rep) / a.T, b_hi = (rt1 / a.rep) / a.T;
-  const int t_hi = b_lo == b_hi ? (rt1 / a.rep) % a.T : a.T - 1;
-  const int nbh = (min(hb + t_hi + 1, static_cast<int>(a.ldh)) + kKeyBlock - 1) / kKeyBlock;
-  const int n_hist = (b_hi - b_lo + 1) * nbh;
-  const int nslot = n_used * kw;
   if constexpr (!ROWS) {
     if (active) {
       for (int ih = split * kw + ks; ih < n_hist; ih += nslot) {
@@ -779,26 +797,44 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
     }
   } else {
     unsigned char* vimg = reinterpret_cast<unsigned char*>(lds) + w * kVImg;
-    // this lane's transposed-read offset in a d-tile's 1 KB: key 4 h4 + q (vlo; + 16 for
-    // vhi), d 4 p of the tile, q = (lane & 15) / 4, p = lane & 3
-    const uint32_t tr0 = static_cast<uint32_t>(32 * (4 * h4 + ((lane & 15) >> 2)) + 8 * (lane & 3));
+    // the wave's V image of a block: key-major, key k's 2D bytes at 2D k, its 16-byte chunk c
+    // at chunk c ^ sw(k) (sw even: 32-byte pairs stay whole).  A transposed read (lane 4q + p
+    // of group h4: key 4 h4 + q, d 16 dt + 4 p) of one half-wave then touches 8 keys whose
+    // pairs sit in 8 different 8-bank groups: conflict-free.  A DMA instruction writes KPI
+    // whole keys, so only the keys the block's rows can see are gathered
+    constexpr int CPK = D / 8;          // 16-byte chunks per key
+    constexpr int KPI = 64 / CPK;       // keys per 1 KB DMA instruction
+    const int kq = 4 * h4 + ((lane & 15) >> 2);          // this lane's vlo key (vhi: + 16)
+    const uint32_t tr_base = static_cast<uint32_t>(kq * 2 * D + 8 * (lane & 3));
+    const int s2 = vimg_swz<D>(kq) >> 1;
+    // this lane's DMA chunk: key i KPI + lane / CPK of instruction i, chunk lane % CPK
+    const int dkey = lane / CPK, dch = lane % CPK;
     typedef __attribute__((address_space(3))) bf16x4* lds_b4_ptr;
+    if (active && split * kw + ks < n_hist) {
+      // the image starts zeroed: a key the block's rows cannot see is not gathered, and its
+      // V row must still be finite (its probability is 0; 0 x NaN is not): zeros, or an
+      // earlier block's rows
+#pragma unroll
+      for (int i = 0; i < kVImg / 1024; ++i)
+        *reinterpret_cast<u32x4*>(vimg + 1024 * i + 16 * lane) = u32x4{0u, 0u, 0u, 0u};
+    }
     if (active) {
       for (int ih = split * kw + ks; ih < n_hist; ih += nslot) {
         const int bb = b_lo + ih / nbh;
         const int kb = (ih % nbh) * kKeyBlock;
-        const int64_t sg = static_cast<int64_t>(gi) * a.n_str + bb;
-        const int32_t* hr = a.hrow + sg * a.ldh + kb;
-        // stream rows of keys col, 16 + col (K fragments) and lane / 2 (the V gather)
-        const int64_t rk0 = hr[col], rk1 = hr[16 + col], rv = hr[lane >> 1];
+        // keys the tile's rows can see (wave-uniform): only those are gathered
+        const int nvalid = min(kKeyBlock, min(hb + t_hi + 1, static_cast<int>(a.ldh)) - kb);
+        const int n_instr = (nvalid + KPI - 1) / KPI;
         auto row_ptr = [&](const __bf16* base, int64_t srow, int key) {
           return base + ((srow * a.Hkv + g) * a.ldh + kb + key) * D;
         };
-        const __bf16* vsrc = row_ptr(a.vth, rv, lane >> 1) + 8 * (lane & 1);
+        // stream rows of keys col, 16 + col (K fragments)
+        const int64_t rk0 = __shfl(hcur, col, 64), rk1 = __shfl(hcur, 16 + col, 64);
         KeyBlock<D> f;
         const __bf16* kp0 = row_ptr(a.kh, rk0, col) + 8 * h4;
         const __bf16* kp1 = row_ptr(a.kh, rk1, 16 + col) + 8 * h4;
-        // K first: its addresses wait for the table entries, the DMAs' issue then never waits
+        // K first, then the V gather (the DMA issue never waits), then the next block's
+        // table entry: every load of the block in flight before the one wait
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds) {
           f.k0[ds] = *reinterpret_cast<const bf16x8*>(kp0 + ds * 32);
@@ -806,17 +842,27 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
         }
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the last block's reads are done
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-          __builtin_amdgcn_global_load_lds(vsrc + 16 * dt, (__attribute__((address_space(3))) void*)(vimg + 1024 * dt),
+#pragma unroll 1
+        for (int i = 0; i < n_instr; ++i) {
+          const int k = i * KPI + dkey;
+          const int64_t rv = __shfl(hcur, k, 64);
+          const __bf16* vsrc = row_ptr(a.vth, rv, k) + 8 * (dch ^ vimg_swz<D>(k));
+          __builtin_amdgcn_global_load_lds(vsrc, (__attribute__((address_space(3))) void*)(vimg + 1024 * i),
                                            16, 0, 0);
-        // every load of the block in flight before the first wait: one memory round trip
+        }
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the V image has landed
+        const int ihn = ih + nslot < n_hist ? ih + nslot : ih;
+        const int32_t hnext = hrow_of(ihn);
+        __builtin_amdgcn_sched_barrier(0);
+        // the V image landed (the compiler drains every VMEM op before an LDS read that
+        // follows an LDS DMA: the next table entry, an L2 hit issued after the HBM-bound
+        // gather, is in by then too)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-          f.vlo[dt] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4_ptr)(vimg + 1024 * dt + tr0));
-          f.vhi[dt] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4_ptr)(vimg + 1024 * dt + tr0 + 512));
+          const uint32_t o2 = tr_base + 32 * (((dt & 7) ^ s2) + (dt & ~7));
+          f.vlo[dt] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4_ptr)(vimg + o2));
+          f.vhi[dt] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4_ptr)(vimg + o2 + 32 * D));
         }
         ItemRef r;
         r.k = nullptr;
@@ -825,6 +871,7 @@ void prefix_attn_plan_lds_kernel(AttnParams a) {
         r.lim = (vrow && bb == b) ? hv : 0;
         r.pos0 = pl;
         attend_block<D>(a, f, r, qf, kmin_pos, h4, o, m, l);
+        hcur = hnext;
       }
     }
     __syncthreads();   // every wave's V image read before the combine reuses the LDS
@@ -1199,19 +1246,19 @@ __global__ __launch_bounds__(256) void hist_gather_kernel(
   }
 }
 
-// Row-layout beam history (cs_hist_rows_update): stream s inherits its parent's slots by
-// table, dst[s][j] = src[parent[s]][j] for j < hist_base, and owns the rest (dst[s][j] = s:
-// the slots this step and later ones write into its own row).  One thread per (s, j).
+// Row-layout history (cs_hist_rows_update): stream s inherits its parent's slots by table,
+// dst[s][j] = src[parent[s]][j] for j < hist_base, and owns the rest (dst[s][j] = row_base +
+// s: the slots this step and later ones write into its own row).  One thread per (s, j).
 __global__ __launch_bounds__(256) void hist_rows_kernel(const int32_t* __restrict__ src,
                                                         int32_t* __restrict__ dst,
                                                         const int64_t* __restrict__ parent,
                                                         const int32_t* __restrict__ hist_base,
-                                                        int64_t S, int32_t ldh) {
+                                                        int64_t S, int32_t ldh, int64_t row_base) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= S * ldh) return;
   const int64_t s = i / ldh;
   const int j = static_cast<int>(i - s * ldh);
-  dst[i] = j < *hist_base ? src[parent[s] * ldh + j] : static_cast<int32_t>(s);
+  dst[i] = j < *hist_base ? src[parent[s] * ldh + j] : static_cast<int32_t>(row_base + s);
 }
 
 // plan tunables (CS_ATTN_TARGET_WGS, CS_ATTN_MIN_ITEMS override; read once)
@@ -1545,16 +1592,18 @@ int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
 }
 
 int cs_hist_rows_update(const int32_t* src_rows, int32_t* dst_rows, const int64_t* parent,
-                        const int32_t* hist_base, int64_t S, int32_t ld_hist, cs_stream_t stream) {
-  if (S < 0 || ld_hist <= 0) return fail(CS_ERR_INVALID, "cs_hist_rows_update: bad shape");
+                        const int32_t* hist_base, int64_t S, int32_t ld_hist, int64_t row_base,
+                        cs_stream_t stream) {
+  if (S < 0 || ld_hist <= 0 || row_base < 0) return fail(CS_ERR_INVALID, "cs_hist_rows_update: bad shape");
   if (S == 0) return CS_OK;
   if (!src_rows || !dst_rows || !parent || !hist_base)
     return fail(CS_ERR_INVALID, "cs_hist_rows_update: NULL pointer");
   if (src_rows == dst_rows) return fail(CS_ERR_INVALID, "cs_hist_rows_update: source and destination must differ");
-  if (S > 0x7fffffffLL || (S * ld_hist + 255) / 256 > 0x7fffffffLL)
+  if (S > 0x7fffffffLL || row_base + S > 0x7fffffffLL || (S * ld_hist + 255) / 256 > 0x7fffffffLL)
     return fail(CS_ERR_INVALID, "cs_hist_rows_update: table too large");
   hipLaunchKernelGGL(hist_rows_kernel, dim3(static_cast<uint32_t>((S * ld_hist + 255) / 256)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), src_rows, dst_rows, parent, hist_base, S, ld_hist);
+                     static_cast<hipStream_t>(stream), src_rows, dst_rows, parent, hist_base, S, ld_hist,
+                     row_base);
   return check_launch("cs_hist_rows_update");
 }
 

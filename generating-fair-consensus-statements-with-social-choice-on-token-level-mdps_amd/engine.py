@@ -243,10 +243,11 @@ class ScoringEngine:
     @torch.no_grad()
     def append_prefix_tokens(self, sp: StreamPrefix, hist_k: torch.Tensor, hist_vt: torch.Tensor,
                              streams: Sequence[int], slot: int, hidden: torch.Tensor,
-                             which: Optional[Sequence[int]] = None) -> None:
+                             which: Optional[Sequence[int]] = None, v_rows: bool = False) -> None:
         """Append one token to prefixes of ``sp`` in place: prefix p (every prefix, or those
-        in ``which``) takes the K/V that stream streams[i] holds in history slot ``slot`` of
-        hist_k [L, S, Hkv, ldh, D] / hist_vt [L, S, Hkv, ldh/32, D, 32] as its next key, and
+        in ``which``) takes the K/V that stream (buffer row) streams[i] holds in history slot
+        ``slot`` of hist_k [L, S, Hkv, ldh, D] / hist_vt [L, S, Hkv, ldh/32, D, 32] (v_rows: V
+        row-layout [L, S, Hkv, ldh, D], a TokenTree's buffers) as its next key, and
         hidden[i] (that stream's final-norm hidden) as its new last hidden.  The token's
         K/V were computed by the stream forward that scored it, so committing a lookahead
         token costs copies, not a forward (the reference re-encodes the grown prompt,
@@ -268,7 +269,8 @@ class ScoringEngine:
         for li in range(len(fp.k)):
             # K [Hkv, Lp, D] <- hist_k[l][s, :, slot, :]; V^T [Hkv, Lp/32, D, 32] column
             fp.k[li][:, rows, :] = hist_k[li][st, :, slot, :].transpose(0, 1)
-            v = hist_vt[li][st, :, slot // 32, :, slot % 32]                # [n, Hkv, D]
+            v = hist_vt[li][st, :, slot, :] if v_rows else \
+                hist_vt[li][st, :, slot // 32, :, slot % 32]                # [n, Hkv, D]
             fp.vt[li][:, tile, :, lane] = v          # (separated advanced indices: [n, Hkv, D])
         for p in which:
             sp.lens[p] += 1
@@ -890,9 +892,13 @@ class TokenTree:
     ``forward(parent_seg, parents, tokens)`` forwards m new nodes: under each of the P
     prefixes the segment's streams are s = p * m + j (one group of m streams per prefix, ONE
     forward_streams over all P * m), history slots 0 .. t-2 inherited from the parent
-    streams (cs_tree_gather from the parent segment's buffer), slot t-1 written by the
-    forward.  ``hidden(seg, idx)`` is the final-norm hidden predicting each listed node's
-    children under every prefix ([P, len(idx), d]; seg = -1: the prefix's last position).
+    streams, slot t-1 written by the forward.  Every segment's streams are rows of ONE
+    row-layout K / V buffer (the segment's rows ``off`` .. off + P m - 1), and a stream reaches
+    its inherited slots through its [P m, ldh] slot table (cs_hist_rows_update from the
+    parent segment's table; cs_prefix_attention_rows): a node's K / V is written once by the
+    forward that made it and never copied.  ``hidden(seg, idx)`` is the final-norm hidden
+    predicting each listed node's children under every prefix ([P, len(idx), d]; seg = -1:
+    the prefix's last position).
 
     Restates what the reference does per lookahead node and per (path, agent): re-encode
     the prompt plus the path (src/methods/finite_lookahead.py:297-399, 464-524 through
@@ -901,35 +907,52 @@ class TokenTree:
 
     def __init__(self, engine: "ScoringEngine", sp: StreamPrefix, max_depth: int,
                  pool: Optional[dict] = None):
-        """pool: reusable history buffers by segment number (kept by the caller across the
-        trees of one statement).  Buffers are zero-filled once when allocated: the
-        attention reads whole 32-slot tiles and weights the unfilled slots by 0, so they
+        """pool: the reusable K / V buffer (kept by the caller across the trees of one
+        statement; grown, never shrunk).  Buffers are zero-filled when allocated: the
+        attention reads whole 32-slot blocks and weights the unfilled slots by 0, so they
         must hold finite values (a stale earlier tree's K/V are fine, NaN garbage is not)."""
         self.e = engine
         self.sp = sp
         self.P = len(sp.lens)
         self.ldh = _ceil32(max_depth)
-        self.segs: List[dict] = []       # {t, m, k, vt, hidden}
+        self.segs: List[dict] = []       # {t, m, off, rows, hidden}
         self.pool = {} if pool is None else pool
+        self.used = 0                     # buffer rows taken by this tree's segments
 
-    def _buffers(self, n_seg: int, S: int):
+    def _reserve(self, S: int) -> int:
+        """S more buffer rows for a new segment: their first row.  A full buffer is replaced
+        by one twice as large holding the rows already written (their K / V move once)."""
         c = self.e.model.cfg
-        dt = self.e.model.dtype
-        per = c.n_layers * S * c.n_kv_heads * self.ldh * c.head_dim
-        ent = self.pool.get(n_seg)
-        if ent is None or ent[0].numel() < per:
-            ent = (torch.zeros(per, dtype=dt, device=self.e.device),
-                   torch.zeros(per, dtype=dt, device=self.e.device))
-            self.pool[n_seg] = ent
-        k = ent[0][:per].view(c.n_layers, S, c.n_kv_heads, self.ldh, c.head_dim)
-        vt = ent[1][:per].view(c.n_layers, S, c.n_kv_heads, self.ldh // 32, c.head_dim, 32)
-        return k, vt
+        need = self.used + S
+        ent = self.pool.get("kv")
+        cap = 0 if ent is None else ent[0].shape[1]
+        if ent is None or ent[0].shape[2:] != (c.n_kv_heads, self.ldh, c.head_dim) or cap < need:
+            new_cap = max(need, 2 * cap, 256)
+            shape = (c.n_layers, new_cap, c.n_kv_heads, self.ldh, c.head_dim)
+            k = torch.zeros(shape, dtype=self.e.model.dtype, device=self.e.device)
+            v = torch.zeros(shape, dtype=self.e.model.dtype, device=self.e.device)
+            if ent is not None and self.used and ent[0].shape[2:] == k.shape[2:]:
+                k[:, :self.used] = ent[0][:, :self.used]
+                v[:, :self.used] = ent[1][:, :self.used]
+            self.pool["kv"] = (k, v)
+        off = self.used
+        self.used = need
+        return off
+
+    @property
+    def k(self) -> torch.Tensor:
+        """The K buffer [L, R, Hkv, ldh, D] (a segment's stream s is row off + s)."""
+        return self.pool["kv"][0]
+
+    @property
+    def v(self) -> torch.Tensor:
+        """The V buffer [L, R, Hkv, ldh, D], row-major like K."""
+        return self.pool["kv"][1]
 
     def forward(self, parent_seg: int, parents: Sequence[int], tokens: Sequence[int]) -> int:
         """Forward m new nodes whose parents are nodes ``parents`` of segment parent_seg
         (-1: the prefix); returns the new segment's id."""
         m_ = self.e.model
-        c = m_.cfg
         dev = self.e.device
         P, m = self.P, len(tokens)
         if m == 0:
@@ -938,8 +961,9 @@ class TokenTree:
         if t > self.ldh:
             raise ValueError("tree deeper than max_depth")
         S = P * m
-        k, vt = self._buffers(len(self.segs), S)
+        off = self._reserve(S)
         hb = torch.full((1,), t - 1, dtype=torch.int32, device=dev)
+        rows = torch.empty(S, self.ldh, dtype=torch.int32, device=dev)
         if t > 1:
             prev = self.segs[parent_seg]
             mp_ = prev["m"]
@@ -947,11 +971,26 @@ class TokenTree:
             if par.numel() != m or int(par.min()) < 0 or int(par.max()) >= mp_:
                 raise ValueError("parents must index the parent segment's nodes")
             src = (torch.arange(P)[:, None] * mp_ + par[None, :]).reshape(-1).to(dev)
-            ops.tree_gather(prev["k"], k, prev["vt"], vt, src, hb)
+            ops.hist_rows_update(prev["rows"], rows, src, hb, row_base=off)
+        else:
+            rows.copy_((off + torch.arange(S, dtype=torch.int32, device=dev))[:, None]
+                       .expand(S, self.ldh))
         tok = torch.as_tensor(list(tokens), dtype=torch.long).repeat(P).to(dev)
-        h = m_.forward_streams(tok, self.sp.fused, list(k.unbind(0)), list(vt.unbind(0)), hb, m, 1)
-        self.segs.append({"t": t, "m": m, "k": k, "vt": vt, "hidden": h.view(P, m, -1)})
+        h = m_.forward_streams(tok, self.sp.fused, list(self.k.unbind(0)), list(self.v.unbind(0)),
+                               hb, m, 1, hist_rows=rows, hist_row_base=off)
+        self.segs.append({"t": t, "m": m, "off": off, "rows": rows, "hidden": h.view(P, m, -1)})
         return len(self.segs) - 1
+
+    def append_to_prefix(self, seg: int, j: int, which: Optional[Sequence[int]] = None) -> None:
+        """Commit node j of a depth-1 segment: every prefix (or those in ``which``) takes that
+        node's K / V (its slot 0, in its own row) as its next key
+        (engine.append_prefix_tokens)."""
+        sg = self.segs[seg]
+        if sg["t"] != 1:
+            raise ValueError("only a depth-1 node's token extends the prefixes")
+        ps = range(self.P) if which is None else which
+        self.e.append_prefix_tokens(self.sp, self.k, self.v, [sg["off"] + p * sg["m"] + j for p in ps],
+                                    0, sg["hidden"][list(ps), j], which=which, v_rows=True)
 
     def hidden(self, seg: int, idx: Sequence[int]) -> torch.Tensor:
         """[P, len(idx), d]: the hidden predicting the children of nodes idx of ``seg``."""

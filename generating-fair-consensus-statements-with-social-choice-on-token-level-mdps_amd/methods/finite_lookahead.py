@@ -354,7 +354,6 @@ class FiniteLookaheadGenerator(BaseGenerator):
             if first.owner is None:
                 first.owner = (tree.forward(-1, [0], [first.ids[0]]), 0)
             seg, j = first.owner
-            sg = tree.segs[seg]
             # the reference re-tokenizes the grown prompts (retokenize "text", default); with a
             # tokenizer that is not merge-free the id append can differ from that, and then the
             # prompts are encoded afresh; retokenize "ids" appends the committed token's id
@@ -362,9 +361,7 @@ class FiniteLookaheadGenerator(BaseGenerator):
             want = [i + [first.ids[0]] for i in ids] if self.retokenize == "ids" else \
                 self._prompts(tok, issue, agent_opinions, shard, current)
             if getattr(tok, "merge_free", True) or all(w == i + [first.ids[0]] for w, i in zip(want, ids)):
-                engine.append_prefix_tokens(sp, sg["k"], sg["vt"],
-                                            [p * sg["m"] + j for p in range(A_loc + 1)], 0,
-                                            sg["hidden"][:, j])
+                tree.append_to_prefix(seg, j)
                 self.stream_stats["appended"] += 1
             else:
                 # the re-tokenized prompts differ from the id append (a BPE merge across

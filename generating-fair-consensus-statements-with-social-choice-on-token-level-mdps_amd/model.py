@@ -459,7 +459,8 @@ class Model:
                         hist_vt: List[torch.Tensor], hist_base: torch.Tensor, n_str: int, T: int,
                         group_prefix: Optional[torch.Tensor] = None,
                         group_prefix_host: Optional[Sequence[int]] = None,
-                        hist_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        hist_rows: Optional[torch.Tensor] = None,
+                        hist_row_base: int = 0) -> torch.Tensor:
         """T new tokens for each of S = n_groups * n_str streams (tokens [S*T], stream-major):
         stream s = i * n_str + b attends to its group's prefix (pfx: engine.FusedPrefix, the
         ragged layouts of include/consensus_scoring.h cs_prefix_attention; group i uses
@@ -471,7 +472,9 @@ class Model:
         final-norm hidden [S*T, d].  pfx.lens_host (+ group_prefix_host) size the key splits
         of the attention work plan.  hist_rows [S, ldh] int32: a row-layout history
         (hist_vt[layer] is V [S, Hkv, ldh, D] like K; slot j of stream s in row hist_rows[s, j]:
-        cs_prefix_attention_rows / cs_rope_place_rows)."""
+        cs_prefix_attention_rows / cs_rope_place_rows); the buffers may hold more rows than
+        the S streams (a token tree's levels), the streams' own rows then start at
+        hist_row_base."""
         from . import ops   # local: model.py stays importable without the library
         c = self.cfg
         H, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
@@ -497,9 +500,12 @@ class Model:
             qkv = ops.linear(x, self.wf[p + "qkv"], packed=wp.get(p + "qkv"),
                              fold=T >= 32 or c.head_dim % 16 != 0 or not _FOLD_IN_ROPE)
             q = torch.empty(n_tok, H, D, dtype=h.dtype, device=h.device)
+            kpl, vpl = hist_k[i], hist_vt[i]
+            if hist_rows is not None and (hist_row_base or kpl.shape[0] != n_tok // T):
+                kpl = kpl[hist_row_base:hist_row_base + n_tok // T]
+                vpl = vpl[hist_row_base:hist_row_base + n_tok // T]
             ops.rope_place(qkv, self.inv_freq, pfx.lengths, hist_base, n_str, T, H, Hkv, D, q,
-                           hist_k[i], hist_vt[i], group_prefix=group_prefix,
-                           v_rows=hist_rows is not None)
+                           kpl, vpl, group_prefix=group_prefix, v_rows=hist_rows is not None)
             o = ops.prefix_attention(q, pfx.k[i], pfx.vt[i], pfx.off, pfx.lengths, pfx.max_len,
                                      hist_k[i], hist_vt[i], hist_base, n_str, T, scale=scale,
                                      softcap=c.attn_softcap,

@@ -568,11 +568,13 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
     if Dk != D or Dh != D or Hkv2 != Hkv:
         raise CSError("head layout mismatch between q, k_prefix and k_hist")
     if hist_rows is not None:
+        # the buffers may hold more rows than query streams (a token tree's earlier levels)
         if tuple(vt_hist.shape) != (S, Hkv, ldh, D):
-            raise CSError("row-layout history: V [S, Hkv, ldh, D] like K expected")
-        if hist_rows.dtype != torch.int32 or tuple(hist_rows.shape) != (S, ldh) or \
-                not hist_rows.is_contiguous():
-            raise CSError("hist_rows must be a contiguous int32 [S, ldh] tensor")
+            raise CSError("row-layout history: V [R, Hkv, ldh, D] like K expected")
+        if hist_rows.dtype != torch.int32 or hist_rows.dim() != 2 or hist_rows.shape[1] != ldh or \
+                hist_rows.shape[0] > S or not hist_rows.is_contiguous():
+            raise CSError("hist_rows must be a contiguous int32 [S, ldh] tensor (S <= buffer rows)")
+        S = hist_rows.shape[0]
     if tuple(vt_prefix.shape) != (Hkv, Lp // 32, D, 32) or \
             (hist_rows is None and tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32)):
         raise CSError("vt_prefix [Hkv, Lp/32, D, 32] / vt_hist [S, Hkv, ldh/32, D, 32] "
@@ -1058,20 +1060,21 @@ def tree_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
 
 
 def hist_rows_update(src_rows: torch.Tensor, dst_rows: torch.Tensor, parent: torch.Tensor,
-                     hist_base: torch.Tensor) -> None:
-    """dst_rows[s, j] = src_rows[parent[s], j] for j < hist_base, else s
-    (cs_hist_rows_update): a row-layout history's beam step, no K / V moved."""
+                     hist_base: torch.Tensor, row_base: int = 0) -> None:
+    """dst_rows[s, j] = src_rows[parent[s], j] for j < hist_base, else row_base + s
+    (cs_hist_rows_update): a row-layout history's beam / tree step, no K / V moved.
+    src_rows [S_src, ldh], dst_rows [S, ldh], parent [S] indexes src_rows."""
     L_ = _lib.load()
     if src_rows.dtype != torch.int32 or dst_rows.dtype != torch.int32 or \
-            src_rows.shape != dst_rows.shape or src_rows.dim() != 2 or \
+            src_rows.dim() != 2 or dst_rows.dim() != 2 or src_rows.shape[1] != dst_rows.shape[1] or \
             not src_rows.is_contiguous() or not dst_rows.is_contiguous():
-        raise CSError("slot tables must be contiguous int32 [S, ldh] tensors of one shape")
-    S, ldh = src_rows.shape
+        raise CSError("slot tables must be contiguous int32 [S, ldh] tensors of one ldh")
+    S, ldh = dst_rows.shape
     if parent.dtype != torch.int64 or parent.numel() != S or hist_base.dtype != torch.int32:
         raise CSError("parent must be int64 [S], hist_base int32 [1]")
     _require_cuda(src_rows, dst_rows, parent, hist_base)
     rc = L_.cs_hist_rows_update(src_rows.data_ptr(), dst_rows.data_ptr(), parent.data_ptr(),
-                                hist_base.data_ptr(), S, ldh, _stream())
+                                hist_base.data_ptr(), S, ldh, int(row_base), _stream())
     _lib.check(rc, "cs_hist_rows_update")
 
 def blocked_vt(v: torch.Tensor) -> torch.Tensor:

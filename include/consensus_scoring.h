@@ -324,7 +324,8 @@ int cs_prefix_attention(const void* q, const void* k_prefix, const void* vt_pref
  * slot table, for beam decoding without history copies:
  *     k_hist, v_hist  [S][Hkv][ld_hist][D] (V row-major like K, not in 32-key V^T tiles)
  *     hist_rows       [S][ld_hist] int32: slot j of stream s is row hist_rows[s][j] of k_hist /
- *                     v_hist (0 <= hist_rows[s][j] < S for every j < ld_hist)
+ *                     v_hist (every entry a row of the buffers, which may hold more than the
+ *                     S query streams: a token tree's earlier levels)
  * so a beam's inherited slots stay where its ancestor wrote them (cs_hist_rows_update builds
  * the next step's table; cs_rope_place_rows writes the step's K / V into the stream's own row).
  * Same arguments, plan and results otherwise (plan may be NULL with no workspace: one
@@ -428,16 +429,22 @@ int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
                    int64_t S_dst, int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
 
 /*
- * cs_hist_rows_update — the beam step of a row-layout history (cs_prefix_attention_rows):
+ * cs_hist_rows_update — the beam (or token-tree) step of a row-layout history
+ * (cs_prefix_attention_rows):
  *     dst_rows[s][j] = src_rows[parent[s]][j]   j < *hist_base   (inherited slots, by table)
- *     dst_rows[s][j] = s                        j >= *hist_base  (written by this and later steps)
- * [S][ld_hist] int32 tables, src and dst distinct (a ping-pong pair, so a queued step can be
- * undone); no K / V moves.  hist_base in device memory (graph replays).
+ *     dst_rows[s][j] = row_base + s             j >= *hist_base  (written by this and later steps)
+ * dst [S][ld_hist] int32; src [any][ld_hist] (the parents' table: the previous beam step's,
+ * or a token tree's parent level's), distinct from dst.  Beams: one buffer of S rows,
+ * row_base 0, a ping-pong pair of tables so a queued step can be undone; a token tree: one
+ * buffer for every level's streams, a level's streams at rows row_base .. row_base + S - 1.
+ * No K / V moves.  hist_base in device memory (graph replays).
  *
- * Replaces: as cs_hist_gather (src/methods/beam_search.py:491-538).
+ * Replaces: as cs_hist_gather / cs_tree_gather (src/methods/beam_search.py:491-538,
+ *   src/methods/finite_lookahead.py:297-399).
  */
 int cs_hist_rows_update(const int32_t* src_rows, int32_t* dst_rows, const int64_t* parent,
-                        const int32_t* hist_base, int64_t S, int32_t ld_hist, cs_stream_t stream);
+                        const int32_t* hist_base, int64_t S, int32_t ld_hist, int64_t row_base,
+                        cs_stream_t stream);
 
 /*
  * cs_add_rms_norm — residual add + RMSNorm of bf16 rows in one pass:

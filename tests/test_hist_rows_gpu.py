@@ -108,15 +108,19 @@ def test_prefix_attention_rows_equals_copied_history(ops, dev, case):
     assert torch.equal(out_rows, run(t["kh"], t["vh"], t["rows"]))   # deterministic relaunch
 
 
-@pytest.mark.parametrize("S,ldh,hb", [(5, 32, 7), (256, 64, 33), (512, 64, 0), (16, 32, 32)])
-def test_hist_rows_update_matches_numpy(ops, dev, S, ldh, hb):
+@pytest.mark.parametrize("S,S_src,ldh,hb,row_base", [(5, 5, 32, 7, 0), (256, 256, 64, 33, 0),
+                                                     (512, 512, 64, 0, 0), (16, 16, 32, 32, 0),
+                                                     # token-tree levels: another parent
+                                                     # count, the level's rows further on
+                                                     (132, 33, 32, 1, 33), (528, 132, 32, 2, 165)])
+def test_hist_rows_update_matches_numpy(ops, dev, S, S_src, ldh, hb, row_base):
     g = np.random.default_rng(S + ldh + hb)
-    src = g.integers(0, S, (S, ldh)).astype(np.int32)
-    parent = g.integers(0, S, S).astype(np.int64)
+    src = g.integers(0, S, (S_src, ldh)).astype(np.int32)
+    parent = g.integers(0, S_src, S).astype(np.int64)
     dst = torch.full((S, ldh), -7, dtype=torch.int32, device=dev)
     ops.hist_rows_update(torch.from_numpy(src).to(dev), dst, torch.from_numpy(parent).to(dev),
-                         torch.tensor([hb], dtype=torch.int32, device=dev))
-    want = np.repeat(np.arange(S, dtype=np.int32)[:, None], ldh, axis=1)
+                         torch.tensor([hb], dtype=torch.int32, device=dev), row_base=row_base)
+    want = np.repeat(row_base + np.arange(S, dtype=np.int32)[:, None], ldh, axis=1)
     want[:, :hb] = src[parent, :hb]
     assert np.array_equal(dst.cpu().numpy(), want)
 

@@ -528,10 +528,8 @@ def test_append_prefix_tokens_equals_prefill_of_the_longer_prompts(dev):
     tree = E.TokenTree(eng, sp, 2)
     toks = [77, 301, 12]
     seg = tree.forward(-1, [0, 0, 0], toks)
-    sg = tree.segs[seg]
     j = 1                                           # commit token 301
-    eng.append_prefix_tokens(sp, sg["k"], sg["vt"], [p * 3 + j for p in range(3)], 0,
-                             sg["hidden"][:, j])
+    tree.append_to_prefix(seg, j)
     assert sp.lens == [32, 65, 18]
     sp2 = eng.prefill_streams([p + [toks[j]] for p in prompts])
     torch.testing.assert_close(sp.last_hidden.float(), sp2.last_hidden.float(), atol=5e-2, rtol=5e-2)
