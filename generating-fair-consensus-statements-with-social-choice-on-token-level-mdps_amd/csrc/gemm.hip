@@ -360,6 +360,12 @@ __device__ __forceinline__ void ws2_accumulate(
     const int s = q / MT, i = q % MT;
     return *reinterpret_cast<const gbf16x8*>(base + x_swz(xr + 16 * i, s * 4 + (lane >> 4)));
   };
+#ifndef CS_WS2_THIN_RING
+// W steps in flight for row blocks of <= 80 rows: 6 measured 0-30 % SLOWER than 3 on every
+// per-rank / C1 shape (the longer prologue and tail outweigh the deeper stream;
+// profiles/r05s_gemm_{old,new}.jsonl), so 3
+#define CS_WS2_THIN_RING 3
+#endif
 #ifndef CS_GEMM_BIG_RING
 #define CS_GEMM_BIG_RING 0
 #endif
@@ -462,32 +468,33 @@ __device__ __forceinline__ void ws2_accumulate(
     for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(w[j][0]), "+v"(w[j][1]));
   };
 
-  // Step t: X(t) in LDS buffer t % 3, W(t) in register set t % 3.  It waits for X(t) (and
+  // Step t: X(t) in LDS buffer t % 3, W(t) in register set t % R.  It waits for X(t) (and
   // the older W(t)) with the loads of steps t - 2 and t - 1 after it still in flight, passes
   // the barrier (every wave done with step t - 1, so buffer (t + 2) % 3 — read in step
-  // t - 1 — is free), issues X(t + 2) into it, computes, then loads W(t + 3) into the set
-  // it used: W (HBM) three steps ahead, X (L2) two.
-  gbf16x8 w0[NT][2], w1[NT][2], w2[NT][2];
-  load_w(w0, 0);
+  // t - 1 — is free), issues X(t + 2) into it, computes, then loads W(t + R) into the set
+  // it used: W (HBM) R steps ahead, X (L2) two.  R = 3 (CS_WS2_THIN_RING for the thin row
+  // blocks; the younger loads at step t's wait are the same W(t + R - 2), X(t + 1),
+  // W(t + R - 1) for every R, so kWait holds; R % 3 == 0 keeps every step's LDS buffer a
+  // constant)
+  constexpr int R = MT <= 5 ? CS_WS2_THIN_RING : 3;
+  static_assert(R % 3 == 0 && R >= 3, "the W ring: a multiple of the 3 X buffers");
+  gbf16x8 wr[R][NT][2];
+  cs_static_for<R - 2>([&](auto rc) { load_w(wr[decltype(rc)::value], decltype(rc)::value); });
   issue_x(0, 0);
-  load_w(w1, 1);
+  load_w(wr[R - 2], R - 2);
   issue_x(1, 1);
-  load_w(w2, 2);
-#define CS_WS2_STEP(T, B, WB)        \
-  sync(WB);                          \
-  issue_x((T) + 2, ((B) + 2) % 3);   \
-  if ((T) < nk) compute(B, WB);      \
-  load_w(WB, (T) + 3);
-  for (int t = 0; t < nk; t += 3) {
-    CS_WS2_STEP(t, 0, w0)
-    CS_WS2_STEP(t + 1, 1, w1)
-    CS_WS2_STEP(t + 2, 2, w2)
+  load_w(wr[R - 1], R - 1);
+  for (int t = 0; t < nk; t += R) {
+    cs_static_for<R>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      sync(wr[r]);
+      issue_x(t + r + 2, (r + 2) % 3);
+      if (t + r < nk) compute(r % 3, wr[r]);
+      load_w(wr[r], t + r + R);
+    });
   }
-#undef CS_WS2_STEP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
-  hold(w0);
-  hold(w1);
-  hold(w2);
+  cs_static_for<R>([&](auto rc) { hold(wr[decltype(rc)::value]); });
 }
 
 // the accumulated tile to Y (bf16, or act(gate) * up) or, P != nullptr, to the fp32 partial
