@@ -222,6 +222,17 @@ static void check_rejections() {
   REJECTS(cs_tree_gather(d, d, d, d, par, i, 1, 1, 2, 1, 32, 96, nullptr));
   REJECTS(cs_rope_place(nullptr, 64, f, i, nullptr, 1, i, 1, 1, 1, 1, 64, d, d, d, 32, nullptr));
   REJECTS(cs_rope_place_splitk(f, 2, f, i, nullptr, 1, i, 1, 32, 4, 2, 64, d, d, d, 64, nullptr));
+  // the row-layout history entries
+  REJECTS(cs_prefix_attention_rows(d, d, d, 32, off, pl, 8, nullptr, 1, d, d, nullptr, 32, i, 4, 1, 8,
+                                   2, 64, 0.1f, 0.f, 0, nullptr, 0, 0, d, nullptr, 0, nullptr));
+  REJECTS(cs_prefix_attention_rows(d, d, d, 32, off, pl, 8, nullptr, 1, d, d, i, 40, i, 4, 1, 8, 2, 64,
+                                   0.1f, 0.f, 0, nullptr, 0, 0, d, nullptr, 0, nullptr));
+  REJECTS(cs_rope_place_rows(nullptr, 64, f, i, nullptr, 1, i, 1, 1, 1, 1, 64, d, d, d, 32, nullptr));
+  REJECTS(cs_rope_place_splitk_rows(f, 2, f, i, nullptr, 1, i, 1, 32, 4, 2, 64, d, d, d, 64, nullptr));
+  REJECTS(cs_hist_rows_update(i, i, par, i, 4, 32, 0, nullptr));          // source == destination
+  REJECTS(cs_hist_rows_update(i, i + 1, par, i, 4, 32, -1, nullptr));     // negative row base
+  REJECTS(cs_hist_rows_update(nullptr, i, par, i, 4, 32, 0, nullptr));
+  CHECK(cs_hist_rows_update(i, i + 1, par, i, 0, 32, 0, nullptr) == 0, "empty rows update");
 }
 
 // ---------------------------------------------------------------------------------------
