@@ -56,6 +56,10 @@ constexpr int kMaxSplit = 32;       // key splits of one (group, head, query gro
 constexpr int kPlanMinBase = 1024;  // from this many (group, head, query group) workgroups on,
                                     // the chip is full without key splits: no plan
 constexpr int kMergeRows = 8;       // query rows per merge workgroup (2 per wave)
+#ifndef CS_ATTN_LAZY
+#define CS_ATTN_LAZY 8.0f           // attend_block's lazy-rescale threshold (log2 units; 0: every block)
+#endif
+constexpr float kLazyRescale = CS_ATTN_LAZY;
 constexpr int64_t kPlanImbalance = 4;   // ... or from a longest cell 4x the mean on (T = 1)
 constexpr int kTargetWgsDefault = 512;    // plan: split cells until about this many workgroups
 constexpr int kMinItemsDefault = 3;       // ... but never below this many key blocks per wave
@@ -187,9 +191,19 @@ __device__ __forceinline__ void attend_block(const AttnParams& a, const KeyBlock
   }
   bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
   bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-  const float mn = fmaxf(m, bm);
+  // lazy rescale: the running max moves (and l, O are rescaled) only when some query column
+  // of the wave sees a block max more than kLazyRescale (log2 units) above its own — until
+  // then the stale max stands and p = 2^(s - m) stays <= 2^kLazyRescale (exact in the final
+  // O / l, which share it).  Most blocks after the first few skip the rescale's vector work.
+  float mn = m;
+  if (__ballot(bm > m + kLazyRescale) != 0) {   // wave-uniform
+    mn = fmaxf(m, bm);
+    const float alpha = mn == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) o[dt] *= alpha;
+  }
   const bool none = mn == -INFINITY;
-  const float alpha = none ? 1.0f : __builtin_amdgcn_exp2f(m - mn);
   float ps = 0.0f;
   bf16x8 pb;
 #pragma unroll
@@ -198,13 +212,12 @@ __device__ __forceinline__ void attend_block(const AttnParams& a, const KeyBlock
     ps += pv;
     pb[i] = static_cast<__bf16>(pv);
   }
-  l = fmaf(l, alpha, ps);
+  l += ps;
   m = mn;
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
     const bf16x8 va = {f.vlo[dt][0], f.vlo[dt][1], f.vlo[dt][2], f.vlo[dt][3],
                        f.vhi[dt][0], f.vhi[dt][1], f.vhi[dt][2], f.vhi[dt][3]};
-    o[dt] *= alpha;
     o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
   }
 }
