@@ -180,14 +180,37 @@ __device__ __forceinline__ void attend_block(const AttnParams& a, const KeyBlock
     y[4 + i] = s1[i];
   }
   float bm = -INFINITY;
+  if constexpr (D <= 128) {
+    // the scale into log2 units in one multiply without a soft-cap, and a key k0 + j of the
+    // lane's 8 visible iff jlo <= j < jhi: fewer vector instructions per block (the online
+    // softmax, not the MFMA, paces these kernels; D = 256 keeps the plain form, whose
+    // registers are at the two-waves-per-SIMD limit)
+    if (a.softcap > 0.0f) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int key = r.kb + (i >> 2) * 16 + 4 * h4 + (i & 3);
-    float x = y[i] * a.scale;
-    if (a.softcap > 0.0f) x = softcap_fn(x, a.softcap, a.inv_softcap);
-    x *= kLog2e;
-    y[i] = (key < r.lim && r.pos0 + key >= kmin_pos) ? x : -INFINITY;
-    bm = fmaxf(bm, y[i]);
+      for (int i = 0; i < 8; ++i) y[i] = softcap_fn(y[i] * a.scale, a.softcap, a.inv_softcap) * kLog2e;
+    } else {
+      const float sl2 = a.scale * kLog2e;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) y[i] *= sl2;
+    }
+    const int k0 = r.kb + 4 * h4;
+    const int jlo = kmin_pos == INT32_MIN ? INT32_MIN : kmin_pos - r.pos0 - k0, jhi = r.lim - k0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int j = (i >> 2) * 16 + (i & 3);
+      y[i] = (j < jhi && j >= jlo) ? y[i] : -INFINITY;
+      bm = fmaxf(bm, y[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int key = r.kb + (i >> 2) * 16 + 4 * h4 + (i & 3);
+      float x = y[i] * a.scale;
+      if (a.softcap > 0.0f) x = softcap_fn(x, a.softcap, a.inv_softcap);
+      x *= kLog2e;
+      y[i] = (key < r.lim && r.pos0 + key >= kmin_pos) ? x : -INFINITY;
+      bm = fmaxf(bm, y[i]);
+    }
   }
   bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
   bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
