@@ -45,6 +45,20 @@ TOL_BF16 = 0.06
 # around zero, so a systematic error of a few 1e-2 that TOL_BF16 alone would let through
 # moves the mean (measured means are printed and recorded in DESIGN.md)
 TOL_BF16_MEAN = 0.01
+# Both scale with the model shape's bf16 rounding floor: the mean |delta| of the same beam
+# increments on the torch bf16 path (torch matmuls + torch attention, tools/bf16_floor.py,
+# recorded in DESIGN.md) is 0.0061 / 0.0070 / 0.0088 for the c1 / wide / gemma256 traces
+# (the fused path: 0.0062 / 0.0071 / 0.0084) but 0.0122 for main128 (hidden 4096, vocab
+# 128256; fused 0.0121).  A trace whose floor exceeds 1/1.3 of TOL_BF16_MEAN gets both
+# tolerances scaled to it: per increment 6.5 x floor, mean |delta| 1.3 x floor.  The signed
+# mean (a systematic error) keeps TOL_BF16_MEAN everywhere.
+BF16_FLOOR = {"method_traces_main128.json.gz": 0.0122}
+
+
+def _tols(traces):
+    """(per-value tolerance, mean |delta| tolerance) of a trace file."""
+    floor = BF16_FLOOR.get(traces["_fname"], 0.0)
+    return max(TOL_BF16, 6.5 * floor), max(TOL_BF16_MEAN, 1.3 * floor)
 BF16_TRACE_FILES = ["method_traces_c1.json", "method_traces_wide.json",
                     # Gemma-2 head_dim 256 (C3's head shape), soft-caps, sliding window
                     "method_traces_gemma256.json",
@@ -90,6 +104,7 @@ def bf16_traces(request, dev):
         pytest.skip(f"{fname} not generated (tests/golden/make_method_traces.py)")
     ops = importlib.import_module(mp.PKG + ".ops")
     t = mp.load_traces(fname)
+    t["_fname"] = fname
     t["_file"] = fname if route == "dispatch" else (
         f"{fname} (every GEMM on cs_gemm)" if route == "cs_gemm" else
         f"{fname} (every GEMM on cs_gemm, packed weights)")
@@ -134,6 +149,7 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
         if run["method"] != "beam_search":
             continue
         ref_steps, users = mp.beam_reference_steps(traces, run, tok)
+        tol, tol_mean = _tols(traces)
         A = len(users)
         gen = methods.get_method_generator("beam_search", dict(run["config"]), traces["model_id"])
         orig_walk = gen._walk
@@ -172,7 +188,7 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
                     st["sum_err"] += e
                     st["sum_signed"] += inc[a] - ref[a]
                     st["checked"] += 1
-                    if e > TOL_BF16:
+                    if e > tol:
                         st["errs"].append(f"step {st['step']} cand {texts[i][-8:]!r} agent {a}: "
                                           f"{inc[a]:.5f} vs reference {ref[a]:.5f}")
                 U_ref.append([st["R_ref"][par[i]][a] + ref[a] for a in range(A)])
@@ -187,14 +203,14 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
             for i in range(n):
                 st["U_ref_of"][texts[i]] = U_ref[i]
             # the bf16 walk keeps the reference's beams unless the candidates it swaps are
-            # within 2 x TOL_BF16 of each other in the reference's welfare
+            # within 2 x tol of each other in the reference's welfare
             only_ref = set(idx_ref) - set(idx_mix)
             only_mix = set(idx_mix) - set(idx_ref)
             st["sel_checked"] += 1
             if only_ref or only_mix:
                 gap = min(abs(W_ref[x] - W_ref[y]) for x in only_ref for y in only_mix) \
                     if only_ref and only_mix else 0.0
-                assert gap <= 2 * TOL_BF16, (st["step"], gap, [texts[i] for i in only_ref],
+                assert gap <= 2 * tol, (st["step"], gap, [texts[i] for i in only_ref],
                                              [texts[i] for i in only_mix])
                 st["sel_waived"] += 1
             # teacher forcing: continue from the reference's kept beams
@@ -235,9 +251,9 @@ def test_beam_fused_path_teacher_forced_against_reference(bf16_traces):
         _report(tag, "selections_within_2tol_differing", st["sel_waived"])
         assert not st["errs"], "\n".join(st["errs"][:20])
         # bf16 rounding errors scatter around zero: a systematic error shows in the mean
-        assert mean_abs <= TOL_BF16_MEAN and abs(mean_signed) <= TOL_BF16_MEAN, (mean_abs, mean_signed)
+        assert mean_abs <= tol_mean and abs(mean_signed) <= TOL_BF16_MEAN, (mean_abs, mean_signed)
         # the final choice over cumulative rewards (errors add up over the steps)
-        if st["final_gap"] > 2 * TOL_BF16 * st["step"]:
+        if st["final_gap"] > 2 * tol * st["step"]:
             assert stmt == run["statement"], (stmt, run["statement"], st["final_gap"])
 
 
@@ -252,13 +268,14 @@ def test_best_of_n_scoring_fused_against_reference(bf16_traces):
         U = gen.score_candidates(traces["issue"], dict(traces["agent_opinions"]), cands)
         ref = torch.tensor([run["agent_rewards"][aid] for aid in traces["agent_opinions"]],
                            dtype=torch.float64)
+        tol, _ = _tols(traces)
         err = float((U.double().cpu() - ref).abs().max())
         _report(f"{traces['_file']} best_of_n", "max_abs_reward_err", err)
-        assert err <= TOL_BF16, err
+        assert err <= tol, err
         W = U.double().cpu().min(dim=0).values
         w_ref = torch.tensor(run["welfare"], dtype=torch.float64)
         top2 = torch.topk(w_ref, 2).values if w_ref.numel() > 1 else None
-        if top2 is None or float(top2[0] - top2[1]) > 2 * TOL_BF16:
+        if top2 is None or float(top2[0] - top2[1]) > 2 * tol:
             assert int(W.argmax()) == int(w_ref.argmax())
 
 
@@ -267,6 +284,7 @@ def test_evaluator_fused_against_reference(bf16_traces):
     ev_mod = importlib.import_module(mp.PKG + ".evaluation")
     ev = ev_mod.StatementEvaluator(traces["model_id"], include_comparative_ranking=False,
                                    verbose=False)
+    tol, _ = _tols(traces)
     worst = 0.0
     for rec in traces.get("evaluations", []):     # (absent from the beam-only c1long trace)
         got = ev.evaluate_statement(rec["statement"], traces["issue"], dict(traces["agent_opinions"]))
@@ -275,7 +293,7 @@ def test_evaluator_fused_against_reference(bf16_traces):
                 continue
             e = abs(float(got[k]) - ref)
             worst = max(worst, e)
-            assert e <= TOL_BF16, (rec["statement"][:20], k, got[k], ref)
+            assert e <= tol, (rec["statement"][:20], k, got[k], ref)
     _report(f"{traces['_file']} evaluator", "max_abs_avg_logprob_err", worst)
 
 
@@ -292,6 +310,7 @@ class _FLTeacher:
     def __init__(self, traces, run, tok, dev):
         prompts = importlib.import_module(mp.PKG + ".methods.prompts")
         self.tok, self.dev = tok, dev
+        self.tol, self.tol_mean = _tols(traces)
         self.steps = run["fl_steps"]
         self.table = {(d["suffix"], d["seed"]): d["text"] for d in run["fl_draws"]}
         self.users = [prompts.FL["agent_user"].format(issue=traces["issue"], opinion=op)
@@ -337,7 +356,7 @@ class _FLTeacher:
                 self.sum_err += e
                 self.sum_signed += float(Uc[a, p]) - ref
                 self.checked += 1
-                if e > TOL_BF16:
+                if e > self.tol:
                     self.errs.append(f"step {self.k} path {p} agent {a}: {float(Uc[a, p]):.5f} "
                                      f"vs reference {ref:.5f}")
             W_ref.append(min(u_ref))
@@ -346,7 +365,7 @@ class _FLTeacher:
         if b != b_ref:
             self.differing += 1
             gap = W_ref[b_ref] - W_ref[b]
-            assert gap <= 2 * TOL_BF16, (self.k, b, b_ref, gap)
+            assert gap <= 2 * self.tol, (self.k, b, b_ref, gap)
         self.k += 1
         return b_ref
 
@@ -375,4 +394,5 @@ def test_lookahead_stream_teacher_forced_against_reference(bf16_traces):
         _report(tag, "rewards_checked", teacher.checked)
         _report(tag, "choices_within_2tol_differing", teacher.differing)
         assert not teacher.errs, "\n".join(teacher.errs[:20])
-        assert mean_abs <= TOL_BF16_MEAN and abs(mean_signed) <= TOL_BF16_MEAN, (mean_abs, mean_signed)
+        assert mean_abs <= teacher.tol_mean and abs(mean_signed) <= TOL_BF16_MEAN, \
+            (mean_abs, mean_signed)
