@@ -30,6 +30,9 @@ SHAPES = {
     "c3": (16, 210, 1700, 16, 1, 16, 8, 256, 25, 50.0),
     "c5": (64, 210, 5500, 8, 1, 64, 8, 128, 25, 0.0),
     "c2": (8, 200, None, 64, 149, 32, 8, 128, 0, 0.0),
+    # one rank of eight (agents sharded): the per-rank decode shapes
+    "c3r8": (2, 210, 1700, 16, 1, 16, 8, 256, 25, 50.0),
+    "c5r8": (8, 210, 5500, 8, 1, 64, 8, 128, 25, 0.0),
 }
 
 
