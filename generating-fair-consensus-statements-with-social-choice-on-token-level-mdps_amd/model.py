@@ -246,19 +246,34 @@ class Model:
         if rep > 1:
             q_pos = q_pos.repeat(1, rep)
         if c.sliding_window and i % 2 == 0:
-            mask = mask & ((q_pos[:, None, :, None] - k_pos[:, None, None, :]) < c.sliding_window)
+            # q - k < W  <=>  k > q - W on integer positions: the comparison broadcasts
+            # straight to bool, never materialising an int64 [B, 1, rep*T, S] difference
+            mask = mask & (k_pos[:, None, None, :] > (q_pos - c.sliding_window)[:, None, :, None])
         return self._attend_grouped(q, k, v, mask).reshape(B, H, T, D)
 
     def _attend_grouped(self, q, k, v, mask):
         c = self.cfg
         scale = (c.query_pre_attn_scalar ** -0.5) if c.query_pre_attn_scalar else c.head_dim ** -0.5
         if c.attn_softcap > 0:
-            s = (q.float() @ k.float().transpose(-1, -2)) * scale
-            s = c.attn_softcap * torch.tanh(s / c.attn_softcap)
-            s = s.masked_fill(~mask, float("-inf"))
-            p = torch.softmax(s, dim=-1).to(v.dtype)
-            return p @ v
+            # the soft-capped scores are materialised in fp32: in query-row chunks of at most
+            # 2^27 scores (512 MB), so a batched prefill of long prompts stays bounded (each
+            # row's softmax is independent of the others)
+            B, G, R, _ = q.shape
+            rows = max(1, (1 << 27) // max(1, B * G * k.shape[2]))
+            if rows >= R or mask.shape[2] != R:
+                return self._softcap_attend(q, k, v, mask, scale)
+            return torch.cat([self._softcap_attend(q[:, :, r:r + rows], k, v,
+                                                   mask[:, :, r:r + rows], scale)
+                              for r in range(0, R, rows)], dim=2)
         return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=scale)
+
+    def _softcap_attend(self, q, k, v, mask, scale):
+        cap = self.cfg.attn_softcap
+        s = (q.float() @ k.float().transpose(-1, -2)) * scale
+        s = cap * torch.tanh(s / cap)
+        s = s.masked_fill(~mask, float("-inf"))
+        p = torch.softmax(s, dim=-1).to(v.dtype)
+        return p @ v
 
     def _layer(self, i, h, pos, ctx_k, ctx_v, ctx_mask, ctx_pos, self_mask=None, pre=None):
         """One decoder layer over new tokens h [B,T,d] at positions pos [B,T].
