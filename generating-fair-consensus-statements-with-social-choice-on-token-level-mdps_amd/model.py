@@ -113,6 +113,9 @@ _FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "0") == "1"
 class Model:
     """Decoder weights + forward.  ``dtype`` is the weight/activation dtype."""
 
+    # fp32 scores the soft-capped eager attention materialises at once (_attend_grouped)
+    softcap_chunk_scores = 1 << 27
+
     def __init__(self, cfg: ModelConfig, device, dtype=torch.bfloat16, seed: int = 0,
                  weights: Optional[Dict[str, torch.Tensor]] = None):
         self.cfg = cfg
@@ -256,10 +259,10 @@ class Model:
         scale = (c.query_pre_attn_scalar ** -0.5) if c.query_pre_attn_scalar else c.head_dim ** -0.5
         if c.attn_softcap > 0:
             # the soft-capped scores are materialised in fp32: in query-row chunks of at most
-            # 2^27 scores (512 MB), so a batched prefill of long prompts stays bounded (each
-            # row's softmax is independent of the others)
+            # softcap_chunk_scores of them, so a batched prefill of long prompts stays
+            # bounded (each row's softmax is independent of the others)
             B, G, R, _ = q.shape
-            rows = max(1, (1 << 27) // max(1, B * G * k.shape[2]))
+            rows = max(1, self.softcap_chunk_scores // max(1, B * G * k.shape[2]))
             if rows >= R or mask.shape[2] != R:
                 return self._softcap_attend(q, k, v, mask, scale)
             return torch.cat([self._softcap_attend(q[:, :, r:r + rows], k, v,

@@ -99,6 +99,25 @@ def test_grouped_query_attention_equals_repeated_kv(preset):
         torch.testing.assert_close(got, want, atol=1e-6, rtol=1e-6)
 
 
+def test_softcap_attention_in_query_chunks_equals_whole(monkeypatch):
+    """The soft-capped eager attention materialises its fp32 scores in query-row chunks of
+    at most Model.softcap_chunk_scores (a batched prefill of long prompts stays bounded);
+    chunked equals whole, ragged last chunk and one-row chunks included."""
+    cfg = M.preset("tiny-gemma", vocab=300)
+    m = M.Model(cfg, "cpu", torch.float32, seed=1)
+    g = torch.Generator().manual_seed(4)
+    B, G, R, S = 3, cfg.n_kv_heads, 13, 17
+    q = torch.randn(B, G, R, cfg.head_dim, generator=g)
+    k = torch.randn(B, G, S, cfg.head_dim, generator=g)
+    v = torch.randn(B, G, S, cfg.head_dim, generator=g)
+    mask = torch.rand(B, 1, R, S, generator=g) > 0.3
+    mask[..., 0] = True
+    whole = m._attend_grouped(q, k, v, mask)
+    for rows in (1, 4, 12):
+        monkeypatch.setattr(m, "softcap_chunk_scores", rows * B * G * S)
+        torch.testing.assert_close(m._attend_grouped(q, k, v, mask), whole, atol=1e-6, rtol=1e-6)
+
+
 def test_store_is_bounded_by_tokens():
     cfg = M.preset("tiny-llama", vocab=300)
     eng = E.ScoringEngine(M.Model(cfg, "cpu", torch.float32, seed=3), reuse_caches=4,
