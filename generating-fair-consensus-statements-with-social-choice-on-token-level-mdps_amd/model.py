@@ -414,12 +414,15 @@ class Model:
     def pack_decode_weights(self, reserve_bytes: Optional[int] = None) -> int:
         """Keep a cs_gemm_pack'ed copy (ops.gemm_pack: fragment-major, every weight load one
         contiguous 1 KB) of each decode weight the dispatch table runs packed at some row
-        count, while the device keeps ``reserve_bytes`` free (default: 1/6 of the device, at
-        least 32 GB: the first stream forward runs after its prefix caches and K/V histories
-        exist, and the reserve leaves room for a second decode state of the same shape, e.g.
-        the re-tokenized text path's, plus activations, logits and graph pools).  The weights whose
+        count, while the device keeps ``reserve_bytes`` free (default 16 GB: the first stream
+        forward runs after its prefix caches and K/V histories exist, and the reserve leaves
+        room for a second decode state of the same shape, e.g. the re-tokenized text path's,
+        plus activations, logits and graph pools -- measured enough at C5, the largest state:
+        a 70B replica with 64 agents and its text path, profiles/r05ab_bench_res16.jsonl;
+        the former 48 GB left the 70B down projection unpacked).  The weights whose
         packed form saves the most time per byte (ops.gemm_pack_gain) go first, so a partial
-        budget (a 70B replica) packs where it pays most.  CS_GEMM_PACK=0 turns packing off.
+        budget (a 70B replica) packs where it pays most.  CS_GEMM_PACK=0 turns packing off;
+        CS_GEMM_PACK_RESERVE_GB sets the reserve.
         The copies are snapshots: code that changes a weight in place after the first stream
         forward must call this again (or set ``wp = None``).  Returns the bytes packed."""
         from . import ops
@@ -429,7 +432,8 @@ class Model:
             return 0
         free, total = torch.cuda.mem_get_info(self.device)
         if reserve_bytes is None:
-            reserve_bytes = max(32 << 30, total // 6)
+            gb = os.environ.get("CS_GEMM_PACK_RESERVE_GB")
+            reserve_bytes = int(float(gb) * (1 << 30)) if gb else 16 << 30
         budget = free - reserve_bytes
         cands = []
         for name, (w, gated) in self.decode_weights().items():
