@@ -863,6 +863,17 @@ int64_t ws2_grid(int64_t cells, int64_t mblocks) {
   return mblocks > 1 ? (cells + 7) / 8 * 8 * mblocks : cells;
 }
 
+// the packed gated form at <= 80 rows (the per-rank decode steps) with 7 waves x 32 W rows
+// (112 features) per workgroup: the 70B gate|up (57,344 rows) is then 256 workgroups on
+// the 256 CUs instead of 224 (8 waves x 32 rows)
+#ifndef CS_WS2_GATED7
+#define CS_WS2_GATED7 1
+#endif
+bool ws2_gated7(int variant, int64_t M, int64_t N, int gated, bool packed) {
+  return CS_WS2_GATED7 && gated && packed && (variant == 2 || variant == 4) && M <= 80 &&
+         N % 224 == 0;
+}
+
 int resolve_variant(int variant, int64_t N, int gated) {
   if (variant == 0) variant = 2;
   if (thin_variant(variant)) return variant;
@@ -980,7 +991,18 @@ int gemm_impl(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, i
     if (grid > 0x7fffffffLL) return fail(CS_ERR_INVALID, "cs_gemm_bf16: grid too large");
     const int b = static_cast<int>(grid);
     const int mbi = static_cast<int>(mb);
-    if (gated && variant == 3) {
+    if (ws2_gated7(variant, M, N, gated, packed)) {
+      const int n7 = static_cast<int>(N / 224);     // (M <= 80: one row block, mt <= 5)
+      if (mt == 2)
+        launch_ws2<2, 2, 1, 7, true>(n7, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                     n7, 1, act, 1);
+      else if (mt == 4)
+        launch_ws2<4, 2, 1, 7, true>(n7, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                     n7, 1, act, 1);
+      else
+        launch_ws2<5, 2, 1, 7, true>(n7, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
+                                     n7, 1, act, 1);
+    } else if (gated && variant == 3) {
       if (packed)
         dispatch_ws2<2, 1, 4, true>(mt, b, st, X, ldx, Wp, ldw, Y, ldy, nullptr, M, N / 2, N / 2, nk,
                                     n_tiles, 1, act, mbi);

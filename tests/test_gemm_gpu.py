@@ -152,6 +152,9 @@ def test_thin_gemm_rejects_more_than_80_rows(ops, dev):
     (300, 512, 640, 0), (48, 1024, 448, 1), (272, 2048, 512, 1),
     # 65-80 rows: the packed launch takes a 5-tile row block, the unpacked one 8 tiles
     (65, 1024, 512, 0), (72, 2048, 1024, 1),
+    # packed gated, <= 80 rows, 2F % 224 == 0: the 7-wave form (112 features per workgroup),
+    # bitwise the unpacked 8-wave kernel -- one row block of 2, 4 and 5 tiles
+    (20, 3584, 256, 1), (48, 1792, 512, 1), (72, 1792, 1024, 1), (80, 3584, 192, 1),
 ])
 def test_packed_weight_gemm_is_bitwise_the_unpacked(ops, dev, M, N, K, gated, variant):
     """cs_gemm_pack + cs_gemm_bf16_packed: the same fragments reach the same MFMAs, only
