@@ -26,8 +26,8 @@ EXPORTED = (
     "cs_vocab_topk", "cs_vocab_sample_workspace_size", "cs_vocab_sample",
     "cs_beam_step_workspace_size", "cs_beam_step", "cs_beam_decode_workspace_size",
     "cs_beam_decode_step", "cs_beam_select", "cs_prefix_attention_plan",
-    "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act", "cs_hist_gather",
-    "cs_tree_gather", "cs_gemm_bf16", "cs_gemm_splits",
+    "cs_prefix_attention", "cs_rope_place", "cs_add_rms_norm", "cs_gated_act",
+    "cs_gemm_bf16", "cs_gemm_splits",
     "cs_gemm_bf16_packed", "cs_gemm_pack", "cs_rope_place_splitk",
     "cs_add_rms_norm_splitk", "cs_prefix_attention_rows", "cs_rope_place_rows",
     "cs_rope_place_splitk_rows", "cs_hist_rows_update",
@@ -123,10 +123,6 @@ def load():
     L.cs_add_rms_norm_splitk.restype = ctypes.c_int
     L.cs_gated_act.argtypes = [vp, i64, vp, i64, i64, i64, ctypes.c_int, vp, i64, vp]
     L.cs_gated_act.restype = ctypes.c_int
-    L.cs_hist_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, vp]
-    L.cs_hist_gather.restype = ctypes.c_int
-    L.cs_tree_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i64, i32, i32, i32, vp]
-    L.cs_tree_gather.restype = ctypes.c_int
     L.cs_gemm_bf16.argtypes = [vp, i64, vp, i64, vp, i64, i64, i64, i64, ctypes.c_int, ctypes.c_int,
                                ctypes.c_int, ctypes.c_int, vp, vp]
     L.cs_gemm_bf16.restype = ctypes.c_int
@@ -149,7 +145,7 @@ def load():
     L.cs_rope_place_rows.restype = ctypes.c_int
     L.cs_rope_place_splitk_rows.argtypes = L.cs_rope_place_splitk.argtypes
     L.cs_rope_place_splitk_rows.restype = ctypes.c_int
-    L.cs_hist_rows_update.argtypes = [vp, vp, vp, vp, i64, i32, i64, vp]
+    L.cs_hist_rows_update.argtypes = [vp, vp, vp, vp, i64, i32, i64, i64, vp]
     L.cs_hist_rows_update.restype = ctypes.c_int
     _lib = L
     return L

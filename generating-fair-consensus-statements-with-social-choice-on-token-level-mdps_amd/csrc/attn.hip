@@ -1219,69 +1219,6 @@ __global__ __launch_bounds__(256) void v_tile_place_kernel(RopeParams r, int32_t
   }
 }
 
-// Beam reordering of the per-stream history: dst[l][s] = src[l][parent[s]] for the filled
-// slots only (j < *hist_base; V tiles rounded up to 32 slots).  One workgroup per (layer,
-// stream), 16-byte vectors; the unfilled capacity is never moved.
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void hist_gather_kernel(
-    const __bf16* __restrict__ src_k, __bf16* __restrict__ dst_k, const __bf16* __restrict__ src_v,
-    __bf16* __restrict__ dst_v, const int64_t* __restrict__ parent, const int32_t* __restrict__ hist_base,
-    int64_t S_src, int64_t S, int32_t Hkv, int32_t ldh, int32_t D) {
-  // one workgroup per (layer, destination stream): all Hkv heads' K rows and V^T tiles,
-  // 16-byte vectors, 8 per thread in flight; the source buffer holds S_src streams
-  const int64_t ls = blockIdx.x;
-  const int64_t l = ls / S, s = ls % S;
-  const int hb = min(*hist_base, ldh);
-  if (hb <= 0) return;
-  const int64_t p = parent[s];
-  const int64_t per = static_cast<int64_t>(ldh) * D;                 // elements per (l, s, g)
-  const int64_t so = (l * S_src + p) * Hkv * per, dn = (l * S + s) * Hkv * per;
-  const int kv = hb * D / 8;                                          // K: hb * D contiguous
-  // V^T [ldh/32][D][32]: every 32-slot tile that holds a filled slot, whole — one
-  // contiguous span per head.  The last tile's slots >= hb come along (the parent's finite
-  // contents instead of the destination's; the attention weights them 0): copying only
-  // the 16-byte units below hb left 16-48 B holes in every 64-B row and ran at 2.4-4.5 TB/s
-  // against 6.3 with whole rows (profiles/r03i_hist_gather_tile_ab.jsonl)
-  const int vv = ((hb + 31) / 32) * D * 4;
-  const int pv = static_cast<int>(per / 8);
-  const float inv_kv = 1.0f / kv, inv_vv = 1.0f / vv;
-  const u32x4_t* sk = reinterpret_cast<const u32x4_t*>(src_k + so);
-  const u32x4_t* sv = reinterpret_cast<const u32x4_t*>(src_v + so);
-  u32x4_t* dk = reinterpret_cast<u32x4_t*>(dst_k + dn);
-  u32x4_t* dv = reinterpret_cast<u32x4_t*>(dst_v + dn);
-  const int nk = Hkv * kv, n = nk + Hkv * vv;
-  // unit i -> its offset (same in source and destination: both [Hkv][ldh*D/8] per stream)
-  auto unit = [&](int i) -> int {
-    if (i < nk) {
-      const int g = fast_div(i, kv, inv_kv);
-      return g * pv + (i - g * kv);
-    }
-    const int iv = i - nk, g = fast_div(iv, vv, inv_vv);
-    return g * pv + (iv - g * vv);
-  };
-  constexpr int U = 8;
-  for (int i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
-    u32x4_t x[U];
-    int o[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * 256;
-      if (i < n) {
-        o[u] = unit(i);
-        x[u] = (i < nk ? sk : sv)[o[u]];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * 256;
-      if (i < n) {
-        (i < nk ? dk : dv)[o[u]] = x[u];
-      }
-    }
-  }
-}
-
 // Row-layout history (cs_hist_rows_update): stream s inherits its parent's slots by table,
 // dst[s][j] = src[parent[s]][j] for j < hist_base, and owns the rest (dst[s][j] = row_base +
 // s: the slots this step and later ones write into its own row).  One thread per (s, j).
@@ -1311,13 +1248,13 @@ int attn_target_wgs() {
 }
 // scoring chunks / prompt prefill on the LDS-staged kernel (CS_ATTN_LDS=0: the per-wave one)
 bool attn_lds() {
-  const char* e = getenv("CS_ATTN_LDS");
-  return !(e && atoi(e) == 0);
+  static const bool v = env_int("CS_ATTN_LDS", 1, 0, 1) != 0;
+  return v;
 }
 // decode steps (a plan): the prefix blocks through LDS (CS_ATTN_PLAN_LDS=0: per wave)
 bool attn_plan_lds() {
-  const char* e = getenv("CS_ATTN_PLAN_LDS");
-  return !(e && atoi(e) == 0);
+  static const bool v = env_int("CS_ATTN_PLAN_LDS", 1, 0, 1) != 0;
+  return v;
 }
 int attn_min_items() {
   static const int v = env_int("CS_ATTN_MIN_ITEMS", kMinItemsDefault, 1, 4096);
@@ -1590,47 +1527,12 @@ int cs_attn_trace_read(unsigned long long* out) {
 }
 #endif
 
-static int hist_gather_launch(const char* name, const void* src_k, void* dst_k, const void* src_vt,
-                              void* dst_vt, const int64_t* parent, const int32_t* hist_base,
-                              int64_t L, int64_t S_src, int64_t S, int32_t Hkv, int32_t ld_hist,
-                              int32_t D, cs_stream_t stream) {
-  const std::string n(name);
-  if (L < 0 || S < 0 || S_src < 0 || Hkv <= 0 || D <= 0) return fail(CS_ERR_INVALID, n + ": bad shape");
-  if (L == 0 || S == 0) return CS_OK;
-  if (S_src == 0) return fail(CS_ERR_INVALID, n + ": no source streams");
-  if (!src_k || !dst_k || !src_vt || !dst_vt || !parent || !hist_base)
-    return fail(CS_ERR_INVALID, n + ": NULL pointer");
-  if (ld_hist <= 0 || ld_hist % 8 || D % 8)
-    return fail(CS_ERR_INVALID, n + ": ld_hist and D must be positive multiples of 8");
-  if (src_k == dst_k || src_vt == dst_vt)
-    return fail(CS_ERR_INVALID, n + ": source and destination must differ (ping-pong)");
-  if (L * S > 0x7fffffffLL || static_cast<int64_t>(Hkv) * ld_hist * D / 8 * 2 > 0x7fffffffLL)
-    return fail(CS_ERR_INVALID, n + ": grid too large");
-  hipLaunchKernelGGL(hist_gather_kernel, dim3(static_cast<uint32_t>(L * S)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const __bf16*>(src_k),
-                     static_cast<__bf16*>(dst_k), static_cast<const __bf16*>(src_vt),
-                     static_cast<__bf16*>(dst_vt), parent, hist_base, S_src, S, Hkv, ld_hist, D);
-  return check_launch(name);
-}
-
-int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
-                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S,
-                   int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream) {
-  return hist_gather_launch("cs_hist_gather", src_k, dst_k, src_vt, dst_vt, parent, hist_base, L,
-                            S, S, Hkv, ld_hist, D, stream);
-}
-
-int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
-                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S_src,
-                   int64_t S_dst, int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream) {
-  return hist_gather_launch("cs_tree_gather", src_k, dst_k, src_vt, dst_vt, parent, hist_base, L,
-                            S_src, S_dst, Hkv, ld_hist, D, stream);
-}
-
 int cs_hist_rows_update(const int32_t* src_rows, int32_t* dst_rows, const int64_t* parent,
                         const int32_t* hist_base, int64_t S, int32_t ld_hist, int64_t row_base,
-                        cs_stream_t stream) {
+                        int64_t n_rows, cs_stream_t stream) {
   if (S < 0 || ld_hist <= 0 || row_base < 0) return fail(CS_ERR_INVALID, "cs_hist_rows_update: bad shape");
+  if (row_base + S > n_rows)
+    return fail(CS_ERR_INVALID, "cs_hist_rows_update: rows row_base .. row_base + S - 1 exceed the buffer's n_rows");
   if (S == 0) return CS_OK;
   if (!src_rows || !dst_rows || !parent || !hist_base)
     return fail(CS_ERR_INVALID, "cs_hist_rows_update: NULL pointer");
@@ -1743,10 +1645,10 @@ int rope_place_impl(const void* qkv, int64_t ld_qkv, const float* part, int32_t 
   const int64_t n_tiles = ld_hist / 32;
   const int64_t n_vwg = static_cast<int64_t>(n_groups) * n_str * Hkv * n_tiles;
   {
-    const char* e = getenv("CS_ROPE_VTILE");
+    static const bool vtile = env_int("CS_ROPE_VTILE", 1, 0, 1) != 0;   // read once
     r.skip_v = (!part && !v_rows && T >= 32 && ld_hist % 32 == 0 && ld_qkv % 8 == 0 &&
                 reinterpret_cast<uintptr_t>(qkv) % 16 == 0 && n_vwg <= 0x7fffffffLL &&
-                !(e && atoi(e) == 0)) ? 1 : 0;
+                vtile) ? 1 : 0;
   }
   // 8-pair (16-byte) items when every head's halves are 16-byte aligned, else 4-pair
   const bool p8 = part ? true

@@ -543,10 +543,11 @@ constexpr int kp1024(int dtype) {
 // --sweep; profiles/r01f_beam_ab*.jsonl).  CS_DECODE_KP overrides (4, 8 or 16).
 int decode_kp(int32_t B, int64_t vocab, int32_t block, int32_t K, int dtype) {
   const int big = block >= 1024 ? kp1024(dtype) : 16;
-  if (const char* e = getenv("CS_DECODE_KP")) {
-    const int v = atoi(e);
-    if (v == 4 || v == big) return v;
-  }
+  static const int env_kp = [] {       // read once
+    const char* e = getenv("CS_DECODE_KP");
+    return e ? atoi(e) : 0;
+  }();
+  if (env_kp == 4 || env_kp == big) return env_kp;
   const int64_t nbig = B * ((vocab + big * block - 1) / (big * static_cast<int64_t>(block)));
   const int64_t n4c = (vocab + 4LL * block - 1) / (4LL * block);
   return (nbig < 128 && n4c * K <= 16384) ? 4 : big;
@@ -556,7 +557,11 @@ int decode_kp(int32_t B, int64_t vocab, int32_t block, int32_t K, int dtype) {
 // fill the chip (C5: 512 rows) — then the rows would starve the proposer to the end.
 // CS_DECODE_ROWS_FIRST=0/1 overrides.
 int decode_rows_first(int64_t row_blocks, int32_t block) {
-  if (const char* e = getenv("CS_DECODE_ROWS_FIRST")) return atoi(e) == 1 ? 1 : 0;
+  static const int env_rf = [] {       // read once: -1 = not set
+    const char* e = getenv("CS_DECODE_ROWS_FIRST");
+    return e ? (atoi(e) == 1 ? 1 : 0) : -1;
+  }();
+  if (env_rf >= 0) return env_rf;
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0, v = 0;
@@ -1107,10 +1112,11 @@ DecodeLayout decode_layout(int32_t A, int32_t B, int64_t vocab, int32_t K, int d
   // profiles/r05e_beam_ab_*.jsonl).  256-thread blocks (one split each, wave-bound proposer
   // selection for K <= 16) measured slower at C1 too: 17.8 vs 16.9 us (r05f_beam_ab.jsonl)
   d.block = 1024;
-  if (const char* e = getenv("CS_DECODE_BLOCK")) {   // A/B: 256 or 1024 whatever the split
-    const int v = atoi(e);
-    if (v == 256 || v == 1024) d.block = v;
-  }
+  static const int env_block = [] {    // A/B: 256 or 1024 whatever the split (read once)
+    const char* e = getenv("CS_DECODE_BLOCK");
+    return e ? atoi(e) : 0;
+  }();
+  if (env_block == 256 || env_block == 1024) d.block = env_block;
   d.kp = decode_kp(B, vocab, d.block, K, dtype);
   const int64_t ch = static_cast<int64_t>(d.kp) * d.block;
   d.nchunk_p = static_cast<int32_t>((vocab + ch - 1) / ch);

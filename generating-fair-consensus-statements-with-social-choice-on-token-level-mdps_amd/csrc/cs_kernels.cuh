@@ -476,9 +476,13 @@ struct SplitPlan {
 };
 
 inline int64_t target_wgs() {
-  const char* e = getenv("CS_TARGET_WGS");  // tuning knob (tools/beam_ab.py, split_sweep.py)
-  const int64_t v = e ? atoll(e) : 0;
-  return v > 0 ? v : kTargetWgs;
+  // tuning knob (tools/beam_ab.py, split_sweep.py), read once per translation unit
+  static const int64_t v = [] {
+    const char* e = getenv("CS_TARGET_WGS");
+    const int64_t x = e ? atoll(e) : 0;
+    return x > 0 ? x : kTargetWgs;
+  }();
+  return v;
 }
 
 // Fewer rows than target_wgs(): split the vocabulary so that about target_wgs() x
@@ -744,17 +748,6 @@ __device__ __forceinline__ unsigned long long ld_sc1(unsigned long long* p) {
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ uint32_t arrive(uint32_t* cnt, uint32_t n = 1u) {
   return __hip_atomic_fetch_add(cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// floor(i / d) for 0 <= i < 2^24, d >= 1, with inv = 1.0f / d (uniform): the float
-// estimate is off by at most one and corrected.  A runtime integer division is ~30 VALU
-// instructions; at three per 16-byte unit it held cs_hist_gather's copy below the HBM rate.
-// Exactness over the kernels' ranges: tests/test_abi.py::test_fast_div_is_floor_division.
-__host__ __device__ __forceinline__ int fast_div(int i, int d, float inv) {
-  int q = static_cast<int>(static_cast<float>(i) * inv);
-  if (q * d > i) --q;
-  else if ((q + 1) * d <= i) ++q;
-  return q;
 }
 
 }  // namespace

@@ -125,8 +125,11 @@ void launch_stream(const void* logits, int64_t items, int64_t vocab, int64_t ld_
 }
 
 int lsg_variant() {
-  const char* e = getenv("CS_LSG_VARIANT");
-  return e ? atoi(e) : 0;
+  static const int v = [] {            // A/B knob (tools/lsg_variants.py), read once
+    const char* e = getenv("CS_LSG_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <int DT, bool CAP>

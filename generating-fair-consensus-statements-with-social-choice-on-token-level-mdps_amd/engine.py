@@ -722,10 +722,7 @@ class DecodeState:
     history is row-layout (K and V [S, Hkv, ldh, D]) behind a [S, ldh] slot table: slot t of
     stream s is row rows[s, t], written once by the step that made it and never moved; a
     step's inheritance is one table update (cs_hist_rows_update, a ping-pong pair of tables)
-    and the attention gathers through it (cs_prefix_attention_rows).  copy_history=True (or
-    CS_HIST_COPY=1): the round-4 form, V in 32-key V^T tiles and the parents' filled slots
-    copied into the other half of a ping-pong pair of buffers (cs_hist_gather).  After
-    the first (eager) advance each parity's step is captured once in a hipGraph and
+    and the attention gathers through it (cs_prefix_attention_rows).  After the first (eager) advance each parity's step is captured once in a hipGraph and
     replayed, so a decode step costs one graph launch plus its inputs' copies; ``post``
     (optional, fixed per state) is captured with it, e.g. the LM head + the fused
     cs_beam_decode_step of the beam search.
@@ -735,7 +732,7 @@ class DecodeState:
     stream per step."""
 
     def __init__(self, engine: "ScoringEngine", cache, n_prefix: int, n_beams: int,
-                 max_steps: int, use_graphs: bool = True, copy_history: Optional[bool] = None):
+                 max_steps: int, use_graphs: bool = True):
         """cache: a StreamPrefix (engine.prefill_streams) or a PrefixCache (re-laid)."""
         self.e = engine
         m = engine.model
@@ -747,26 +744,14 @@ class DecodeState:
         self.ldh = _ceil32(max_steps)
         self.max_steps = int(max_steps)
 
-        if copy_history is None:
-            copy_history = os.environ.get("CS_HIST_COPY") == "1"
-        self.copy_history = bool(copy_history)
-
-        def buffers():
-            # all layers in one tensor each, so a step's parent gather is 2 launches, not 2L
-            return (torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
-                                dtype=m.dtype, device=dev),
-                    torch.zeros(c.n_layers, self.S, c.n_kv_heads, self.ldh // 32, c.head_dim, 32,
-                                dtype=m.dtype, device=dev))
-
-        if self.copy_history:
-            self.hist = [buffers(), buffers()]
-            self.rows = None
-        else:
-            kv = torch.zeros(2, c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
-                             dtype=m.dtype, device=dev)
-            self.hist = [(kv[0], kv[1])] * 2
-            self.rows = [torch.arange(self.S, dtype=torch.int32, device=dev)[:, None]
-                         .expand(self.S, self.ldh).contiguous() for _ in range(2)]
+        # K and V of every layer and stream, row-major [L, S, Hkv, ldh, D] each, written in
+        # place (never copied); a ping-pong pair of slot tables [S, ldh] so a queued step can
+        # be undone (rewind)
+        kv = torch.zeros(2, c.n_layers, self.S, c.n_kv_heads, self.ldh, c.head_dim,
+                         dtype=m.dtype, device=dev)
+        self.k_hist, self.v_hist = kv[0], kv[1]
+        self.rows = [torch.arange(self.S, dtype=torch.int32, device=dev)[:, None]
+                     .expand(self.S, self.ldh).contiguous() for _ in range(2)]
         self.cur = 0
         self.steps = 0                                   # tokens appended so far (host copy)
         self.hist_base = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -794,16 +779,11 @@ class DecodeState:
 
     def _body(self, post) -> None:
         m = self.e.model
-        new_k, new_v = self.hist[1 - self.cur]
-        rows = None
-        if self.rows is not None:
-            rows = self.rows[1 - self.cur]
-            ops.hist_rows_update(self.rows[self.cur], rows, self.src, self.hist_base)
-        else:
-            old_k, old_v = self.hist[self.cur]
-            ops.hist_gather(old_k, new_k, old_v, new_v, self.src, self.hist_base)
-        h = m.forward_streams(self.tok, self.pfx, list(new_k.unbind(0)), list(new_v.unbind(0)),
-                              self.hist_base, self.B, 1, hist_rows=rows)
+        rows = self.rows[1 - self.cur]
+        ops.hist_rows_update(self.rows[self.cur], rows, self.src, self.hist_base, n_rows=self.S)
+        h = m.forward_streams(self.tok, self.pfx, list(self.k_hist.unbind(0)),
+                              list(self.v_hist.unbind(0)), self.hist_base, self.B, 1,
+                              hist_rows=rows)
         self.hidden.copy_(h)
         self.hist_base += 1
         if post is not None:
@@ -881,6 +861,21 @@ class DecodeState:
         self._plans.clear()
 
 
+def tree_pool(engine: "ScoringEngine", n_prefix: int, bf: int, max_depth: int) -> dict:
+    """A TokenTree K / V pool sized up front for the largest tree of a lookahead statement:
+    under each of n_prefix prefixes the nodes of levels 1 .. max_depth - 1 (the expanded
+    ones; b + b^2 + ... + b^(d-1), at least the one committed node of a depth-1 tree).
+    Allocated before the first stream forward, so the packed-weight copies made there
+    (Model.pack_decode_weights) budget around it instead of leaving the tree to grow into
+    the reserve (a 70B lookahead outgrew 16 GB)."""
+    c = engine.model.cfg
+    per = max(1, sum(bf ** t for t in range(1, max(1, max_depth))))
+    rows = max(256, n_prefix * per)
+    shape = (c.n_layers, rows, c.n_kv_heads, _ceil32(max(1, max_depth)), c.head_dim)
+    return {"kv": (torch.zeros(shape, dtype=engine.model.dtype, device=engine.device),
+                   torch.zeros(shape, dtype=engine.model.dtype, device=engine.device))}
+
+
 class TokenTree:
     """One token tree decoded under every prefix of a StreamPrefix on the stream kernels
     (bf16 models), in SEGMENTS: a segment is a set of m sibling-level nodes forwarded
@@ -921,20 +916,33 @@ class TokenTree:
 
     def _reserve(self, S: int) -> int:
         """S more buffer rows for a new segment: their first row.  A full buffer is replaced
-        by one twice as large holding the rows already written (their K / V move once)."""
+        by one twice as large holding the rows already written (their K / V move once; each
+        old buffer is released as soon as it is copied, so the grow holds at most one old
+        and two new buffers)."""
         c = self.e.model.cfg
         need = self.used + S
         ent = self.pool.get("kv")
         cap = 0 if ent is None else ent[0].shape[1]
-        if ent is None or ent[0].shape[2:] != (c.n_kv_heads, self.ldh, c.head_dim) or cap < need:
+        layout = (c.n_kv_heads, self.ldh, c.head_dim)
+        if ent is not None and self.used and tuple(ent[0].shape[2:]) != layout:
+            # this tree's earlier segments live in the pool: their row tables would point
+            # into a buffer of another layout
+            raise ValueError("TokenTree: the pool's history layout changed under a tree "
+                             "with segments in it")
+        if ent is None or tuple(ent[0].shape[2:]) != layout or cap < need:
             new_cap = max(need, 2 * cap, 256)
-            shape = (c.n_layers, new_cap, c.n_kv_heads, self.ldh, c.head_dim)
-            k = torch.zeros(shape, dtype=self.e.model.dtype, device=self.e.device)
-            v = torch.zeros(shape, dtype=self.e.model.dtype, device=self.e.device)
-            if ent is not None and self.used and ent[0].shape[2:] == k.shape[2:]:
-                k[:, :self.used] = ent[0][:, :self.used]
-                v[:, :self.used] = ent[1][:, :self.used]
-            self.pool["kv"] = (k, v)
+            shape = (c.n_layers, new_cap, *layout)
+            old = list(self.pool.pop("kv", None) or (None, None))
+            keep = self.used if old[0] is not None else 0
+            ent = None
+            bufs = []
+            for j in range(2):       # K, then V: each old buffer freed once it is copied
+                t = torch.zeros(shape, dtype=self.e.model.dtype, device=self.e.device)
+                if keep:
+                    t[:, :keep] = old[j][:, :keep]
+                old[j] = None
+                bufs.append(t)
+            self.pool["kv"] = (bufs[0], bufs[1])
         off = self.used
         self.used = need
         return off
@@ -971,7 +979,8 @@ class TokenTree:
             if par.numel() != m or int(par.min()) < 0 or int(par.max()) >= mp_:
                 raise ValueError("parents must index the parent segment's nodes")
             src = (torch.arange(P)[:, None] * mp_ + par[None, :]).reshape(-1).to(dev)
-            ops.hist_rows_update(prev["rows"], rows, src, hb, row_base=off)
+            ops.hist_rows_update(prev["rows"], rows, src, hb, n_rows=self.k.shape[1],
+                                 row_base=off)
         else:
             rows.copy_((off + torch.arange(S, dtype=torch.int32, device=dev))[:, None]
                        .expand(S, self.ldh))

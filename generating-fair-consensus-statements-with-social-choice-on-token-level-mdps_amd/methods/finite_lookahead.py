@@ -36,7 +36,8 @@ the reference rows' biased seeded draws (cs_vocab_sample) give the children, the
 are gathered at those children (cs_logsoftmax_gather, bf targets per row) -- so a node's
 agent log-prob comes from its PARENT's row and the tree needs 1 + b + ... + b^(d-1) rows per
 agent, not one per node -- and the children that will be expanded are forwarded as one
-segment of streams inheriting their parents' K/V (cs_tree_gather).  The committed token's
+segment of streams inheriting their parents' K/V by slot table, without any copy
+(cs_hist_rows_update + cs_prefix_attention_rows on the tree's row-layout pool).  The committed token's
 K/V are copied from its level-1 stream into every prefix (engine.append_prefix_tokens): no
 re-prefill between steps.
 
@@ -54,7 +55,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import ops, parallel, runtime
-from ..engine import TokenTree
+from ..engine import TokenTree, tree_pool
 from .base import BaseGenerator
 from .prompts import FL, opinions_text
 
@@ -314,9 +315,11 @@ class FiniteLookaheadGenerator(BaseGenerator):
         bias = runtime.bias_token_ids(tok, FL["bias_against"])
         current, count = "", 0
         ids = self._prompts(tok, issue, agent_opinions, shard, current)
+        # the trees' history buffers, reused step to step: sized for the largest tree before
+        # the first stream forward packs the decode weights around what is left
+        pool = tree_pool(engine, A_loc + 1, bf, depth)
         sp = engine.prefill_streams(ids, reserve=max_tokens)
         self.stream_stats = {"prefills": 1, "appended": 0, "segments": 0, "rows": 0}
-        pool: dict = {}                   # the trees' history buffers, reused step to step
         while count < max_tokens:
             self.step_times.append(time.perf_counter())
             if depth <= 0 or bf <= 0:

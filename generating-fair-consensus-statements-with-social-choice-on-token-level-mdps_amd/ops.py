@@ -28,6 +28,9 @@ WELFARE = {"min": _lib.WELFARE_MIN, "egalitarian": _lib.WELFARE_MIN,
            "sumlog": _lib.WELFARE_SUMLOG, "nash": _lib.WELFARE_SUMLOG,
            "max": _lib.WELFARE_MAX}
 
+# CS_DEBUG_TABLES=1: the row-layout history's slot tables are checked on the host against
+# the K / V buffer they index before every (uncaptured) launch that reads them (read once)
+_DEBUG_TABLES = os.environ.get("CS_DEBUG_TABLES") == "1"
 _DTYPE = {torch.float32: _lib.CS_F32, torch.bfloat16: _lib.CS_BF16, torch.float16: _lib.CS_F16}
 
 
@@ -574,6 +577,9 @@ def prefix_attention(q: torch.Tensor, k_prefix: torch.Tensor, vt_prefix: torch.T
         if hist_rows.dtype != torch.int32 or hist_rows.dim() != 2 or hist_rows.shape[1] != ldh or \
                 hist_rows.shape[0] > S or not hist_rows.is_contiguous():
             raise CSError("hist_rows must be a contiguous int32 [S, ldh] tensor (S <= buffer rows)")
+        if _DEBUG_TABLES and hist_rows.numel() and not torch.cuda.is_current_stream_capturing():
+            if int(hist_rows.min()) < 0 or int(hist_rows.max()) >= S:
+                raise CSError("hist_rows names a row outside the K / V buffer")
         S = hist_rows.shape[0]
     if tuple(vt_prefix.shape) != (Hkv, Lp // 32, D, 32) or \
             (hist_rows is None and tuple(vt_hist.shape) != (S, Hkv, ldh // 32, D, 32)):
@@ -1010,60 +1016,13 @@ def gemm_partials(x: torch.Tensor, w: torch.Tensor, *, splits: int, variant: int
     return SplitPartials(part)
 
 
-def hist_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
-                dst_vt: torch.Tensor, parent: torch.Tensor, hist_base: torch.Tensor) -> None:
-    """dst[l][s] = src[l][parent[s]] over the filled history slots (cs_hist_gather);
-    K [L, S, Hkv, ldh, D], V^T [L, S, Hkv, ldh/32, D, 32] bf16, parent [S] int64."""
-    L_ = _lib.load()
-    if src_k.dim() != 5 or src_k.shape != dst_k.shape or src_vt.shape != dst_vt.shape:
-        raise CSError("history buffers must be matching [L, S, Hkv, ldh, D] / "
-                      "[L, S, Hkv, ldh/32, D, 32]")
-    Ln, S, Hkv, ldh, D = src_k.shape
-    if tuple(src_vt.shape) != (Ln, S, Hkv, ldh // 32, D, 32):
-        raise CSError("V^T history layout mismatch")
-    for t in (src_k, dst_k, src_vt, dst_vt):
-        if t.dtype != torch.bfloat16 or not t.is_contiguous():
-            raise CSError("history buffers must be contiguous bfloat16")
-    if parent.dtype != torch.int64 or parent.numel() != S or hist_base.dtype != torch.int32:
-        raise CSError("parent must be int64 [S], hist_base int32 [1]")
-    _require_cuda(src_k, dst_k, src_vt, dst_vt, parent, hist_base)
-    rc = L_.cs_hist_gather(src_k.data_ptr(), dst_k.data_ptr(), src_vt.data_ptr(), dst_vt.data_ptr(),
-                           parent.data_ptr(), hist_base.data_ptr(), Ln, S, Hkv, ldh, D, _stream())
-    _lib.check(rc, "cs_hist_gather")
-
-
-def tree_gather(src_k: torch.Tensor, dst_k: torch.Tensor, src_vt: torch.Tensor,
-                dst_vt: torch.Tensor, parent: torch.Tensor, hist_base: torch.Tensor) -> None:
-    """dst[l][s] = src[l][parent[s]] over the filled history slots between buffers of
-    different stream counts (cs_tree_gather): K [L, S_src|S_dst, Hkv, ldh, D], V^T
-    [L, S_src|S_dst, Hkv, ldh/32, D, 32] bf16, parent [S_dst] int64 in [0, S_src)."""
-    L_ = _lib.load()
-    if src_k.dim() != 5 or dst_k.dim() != 5:
-        raise CSError("history buffers must be [L, S, Hkv, ldh, D]")
-    Ln, Ss, Hkv, ldh, D = src_k.shape
-    Sd = dst_k.shape[1]
-    if tuple(dst_k.shape) != (Ln, Sd, Hkv, ldh, D) or \
-            tuple(src_vt.shape) != (Ln, Ss, Hkv, ldh // 32, D, 32) or \
-            tuple(dst_vt.shape) != (Ln, Sd, Hkv, ldh // 32, D, 32):
-        raise CSError("tree_gather: K / V^T history layouts do not match")
-    for t in (src_k, dst_k, src_vt, dst_vt):
-        if t.dtype != torch.bfloat16 or not t.is_contiguous():
-            raise CSError("history buffers must be contiguous bfloat16")
-    if parent.dtype != torch.int64 or parent.numel() != Sd or hist_base.dtype != torch.int32:
-        raise CSError("parent must be int64 [S_dst], hist_base int32 [1]")
-    _require_cuda(src_k, dst_k, src_vt, dst_vt, parent, hist_base)
-    rc = L_.cs_tree_gather(src_k.data_ptr(), dst_k.data_ptr(), src_vt.data_ptr(), dst_vt.data_ptr(),
-                           parent.data_ptr(), hist_base.data_ptr(), Ln, Ss, Sd, Hkv, ldh, D,
-                           _stream())
-    _lib.check(rc, "cs_tree_gather")
-
-
-
 def hist_rows_update(src_rows: torch.Tensor, dst_rows: torch.Tensor, parent: torch.Tensor,
-                     hist_base: torch.Tensor, row_base: int = 0) -> None:
+                     hist_base: torch.Tensor, *, n_rows: int, row_base: int = 0) -> None:
     """dst_rows[s, j] = src_rows[parent[s], j] for j < hist_base, else row_base + s
     (cs_hist_rows_update): a row-layout history's beam / tree step, no K / V moved.
-    src_rows [S_src, ldh], dst_rows [S, ldh], parent [S] indexes src_rows."""
+    src_rows [S_src, ldh], dst_rows [S, ldh], parent [S] indexes src_rows; n_rows = the
+    K / V buffer's row count (row_base + S beyond it is rejected).  With CS_DEBUG_TABLES=1
+    the parents and the source table's entries are checked on the host as well."""
     L_ = _lib.load()
     if src_rows.dtype != torch.int32 or dst_rows.dtype != torch.int32 or \
             src_rows.dim() != 2 or dst_rows.dim() != 2 or src_rows.shape[1] != dst_rows.shape[1] or \
@@ -1073,9 +1032,16 @@ def hist_rows_update(src_rows: torch.Tensor, dst_rows: torch.Tensor, parent: tor
     if parent.dtype != torch.int64 or parent.numel() != S or hist_base.dtype != torch.int32:
         raise CSError("parent must be int64 [S], hist_base int32 [1]")
     _require_cuda(src_rows, dst_rows, parent, hist_base)
+    if _DEBUG_TABLES and S and not torch.cuda.is_current_stream_capturing():
+        if int(parent.min()) < 0 or int(parent.max()) >= src_rows.shape[0]:
+            raise CSError("hist_rows_update: a parent does not index the source table")
+        if int(src_rows.min()) < 0 or int(src_rows.max()) >= int(n_rows):
+            raise CSError("hist_rows_update: the source table names a row past n_rows")
     rc = L_.cs_hist_rows_update(src_rows.data_ptr(), dst_rows.data_ptr(), parent.data_ptr(),
-                                hist_base.data_ptr(), S, ldh, int(row_base), _stream())
+                                hist_base.data_ptr(), S, ldh, int(row_base), int(n_rows),
+                                _stream())
     _lib.check(rc, "cs_hist_rows_update")
+
 
 def blocked_vt(v: torch.Tensor) -> torch.Tensor:
     """V rows [..., keys, D] (keys a multiple of 32) -> the kernels' V^T in 32-key tiles

@@ -395,40 +395,6 @@ int cs_rope_place_splitk_rows(const float* part, int32_t splits, const float* in
                               void* v_hist, int64_t ld_hist, cs_stream_t stream);
 
 /*
- * cs_hist_gather — beam reordering of the per-stream K/V history (the cs_prefix_attention
- * layouts, all L layers in one buffer): for every layer l and stream s, the filled slots
- * j < *hist_base of stream parent[s] are copied,
- *     dst_k [l][s][g][j][:] = src_k [l][parent[s]][g][j][:]     ([L][S][Hkv][ld_hist][D])
- *     dst_vt[l][s][g][..]   = src_vt[l][parent[s]][g][..]      ([L][S][Hkv][ld_hist/32][D][32],
- *                                  every 32-slot tile holding a slot j < hist_base, whole;
- *                                  later tiles keep dst's data)
- * src and dst distinct (a ping-pong pair).  hist_base in device memory (graph replays).
- *
- * Replaces: the reference's beams are strings re-encoded in full by every call
- *   (src/methods/beam_search.py:491-538 through src/utils.py:249-259); here a kept beam
- *   inherits its parent's K/V.
- */
-int cs_hist_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
-                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S,
-                   int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
-
-/*
- * cs_tree_gather — cs_hist_gather between buffers of different stream counts: the
- * source holds S_src streams ([L][S_src][Hkv][ld_hist][D] / V^T tiles), the destination
- * S_dst; destination stream s receives the filled slots j < *hist_base of source stream
- * parent[s] (0 <= parent[s] < S_src).  Used level by level for a token tree: the streams of
- * the nodes with t tokens inherit the K/V of their parent nodes' streams (t - 1 tokens).
- *
- * Replaces: every lookahead tree node re-encodes the prompt plus its whole path, once to
- *   sample its children (src/methods/finite_lookahead.py:297-399 through generate_text) and
- *   once per agent to score each path (finite_lookahead.py:464-524 through
- *   src/utils.py:249-259); here a node's K/V is computed once and its children inherit it.
- */
-int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst_vt,
-                   const int64_t* parent, const int32_t* hist_base, int64_t L, int64_t S_src,
-                   int64_t S_dst, int32_t Hkv, int32_t ld_hist, int32_t D, cs_stream_t stream);
-
-/*
  * cs_hist_rows_update — the beam (or token-tree) step of a row-layout history
  * (cs_prefix_attention_rows):
  *     dst_rows[s][j] = src_rows[parent[s]][j]   j < *hist_base   (inherited slots, by table)
@@ -437,14 +403,18 @@ int cs_tree_gather(const void* src_k, void* dst_k, const void* src_vt, void* dst
  * or a token tree's parent level's), distinct from dst.  Beams: one buffer of S rows,
  * row_base 0, a ping-pong pair of tables so a queued step can be undone; a token tree: one
  * buffer for every level's streams, a level's streams at rows row_base .. row_base + S - 1.
- * No K / V moves.  hist_base in device memory (graph replays).
+ * n_rows: the K / V buffer's row count; row_base + S > n_rows is rejected (CS_ERR_INVALID),
+ * so a table can never name a row past the buffer it indexes.  No K / V moves.  hist_base
+ * in device memory (graph replays).
  *
- * Replaces: as cs_hist_gather / cs_tree_gather (src/methods/beam_search.py:491-538,
- *   src/methods/finite_lookahead.py:297-399).
+ * Replaces: the reference's beams and lookahead paths are strings that every scoring call
+ *   re-encodes in full (src/methods/beam_search.py:491-538, src/methods/finite_lookahead.py:
+ *   297-399 through src/utils.py:249-259); here a kept beam or a tree node inherits its
+ *   parent's K / V by table, without any copy.
  */
 int cs_hist_rows_update(const int32_t* src_rows, int32_t* dst_rows, const int64_t* parent,
                         const int32_t* hist_base, int64_t S, int32_t ld_hist, int64_t row_base,
-                        cs_stream_t stream);
+                        int64_t n_rows, cs_stream_t stream);
 
 /*
  * cs_add_rms_norm — residual add + RMSNorm of bf16 rows in one pass:

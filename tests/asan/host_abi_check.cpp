@@ -217,9 +217,6 @@ static void check_rejections() {
   REJECTS(cs_gated_act(d, 64, d, 64, -1, 64, 0, d, 64, nullptr));
   REJECTS(cs_gated_act(d, 64, d, 64, 4, 60, 0, d, 64, nullptr));
   const int64_t* par = reinterpret_cast<const int64_t*>(d);
-  REJECTS(cs_hist_gather(nullptr, d, d, d, par, i, 1, 1, 1, 32, 64, nullptr));
-  REJECTS(cs_hist_gather(d, d, d, d, par, i, 1, 1, 1, 40, 64, nullptr));
-  REJECTS(cs_tree_gather(d, d, d, d, par, i, 1, 1, 2, 1, 32, 96, nullptr));
   REJECTS(cs_rope_place(nullptr, 64, f, i, nullptr, 1, i, 1, 1, 1, 1, 64, d, d, d, 32, nullptr));
   REJECTS(cs_rope_place_splitk(f, 2, f, i, nullptr, 1, i, 1, 32, 4, 2, 64, d, d, d, 64, nullptr));
   // the row-layout history entries
@@ -229,10 +226,12 @@ static void check_rejections() {
                                    0.1f, 0.f, 0, nullptr, 0, 0, d, nullptr, 0, nullptr));
   REJECTS(cs_rope_place_rows(nullptr, 64, f, i, nullptr, 1, i, 1, 1, 1, 1, 64, d, d, d, 32, nullptr));
   REJECTS(cs_rope_place_splitk_rows(f, 2, f, i, nullptr, 1, i, 1, 32, 4, 2, 64, d, d, d, 64, nullptr));
-  REJECTS(cs_hist_rows_update(i, i, par, i, 4, 32, 0, nullptr));          // source == destination
-  REJECTS(cs_hist_rows_update(i, i + 1, par, i, 4, 32, -1, nullptr));     // negative row base
-  REJECTS(cs_hist_rows_update(nullptr, i, par, i, 4, 32, 0, nullptr));
-  CHECK(cs_hist_rows_update(i, i + 1, par, i, 0, 32, 0, nullptr) == 0, "empty rows update");
+  REJECTS(cs_hist_rows_update(i, i, par, i, 4, 32, 0, 4, nullptr));       // source == destination
+  REJECTS(cs_hist_rows_update(i, i + 1, par, i, 4, 32, -1, 4, nullptr));  // negative row base
+  REJECTS(cs_hist_rows_update(nullptr, i, par, i, 4, 32, 0, 4, nullptr));
+  REJECTS(cs_hist_rows_update(i, i + 1, par, i, 4, 32, 0, 3, nullptr));   // rows past the buffer
+  REJECTS(cs_hist_rows_update(i, i + 1, par, i, 4, 32, 2, 5, nullptr));   // row_base + S > n_rows
+  CHECK(cs_hist_rows_update(i, i + 1, par, i, 0, 32, 0, 0, nullptr) == 0, "empty rows update");
 }
 
 // ---------------------------------------------------------------------------------------

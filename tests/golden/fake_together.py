@@ -61,6 +61,11 @@ class Backend:
         self.calls: List[Dict] = []
         self.kv_cache = int(kv_cache)
         self._kv: List = []          # [(ids tuple, DynamicCache)], most recent last
+        # every draw of sample(): the Gumbel-max margin (best perturbed score minus the
+        # runner-up) -- how far the draw is from a tie, so a bf16 replay that draws another
+        # token can be checked to do so only at a near-tie
+        self.draw_log: List[Dict] = []
+        self.last_margins: List[float] = []
 
     @torch.no_grad()
     def _forward(self, ids: List[int], keep: int) -> torch.Tensor:
@@ -115,6 +120,7 @@ class Backend:
             seed = int(self.rng.integers(0, 2**63))
         cur = list(ids)
         drawn, lps = [], []
+        self.last_margins = []
         for t in range(max_tokens):
             x = self.logits(cur, last_only=True)[-1].copy()
             for i, v in bias.items():
@@ -122,10 +128,20 @@ class Backend:
             i, lp = oracle.gumbel_sample(x, draw_seed(seed, t), temperature)
             drawn.append(i)
             lps.append(lp)
+            self.last_margins.append(gumbel_margin(x, draw_seed(seed, t), temperature))
             if i in self.tok.eos_ids:
                 break
             cur.append(i)
         return drawn, lps
+
+
+def gumbel_margin(x: np.ndarray, seed: int, temperature: float) -> float:
+    """Top-1 minus top-2 of the perturbed scores x/T + g(seed, v) that gumbel_sample takes
+    the argmax of."""
+    u = oracle.cs_uniform(seed, np.arange(x.shape[0])).astype(np.float64)
+    s = np.asarray(x, dtype=np.float64) / temperature - np.log(-np.log(u))
+    top2 = np.partition(s, -2)[-2:]
+    return float(top2[1] - top2[0])
 
 
 _BACKEND: Optional[Backend] = None
@@ -174,6 +190,8 @@ class _Completions:
         b = _BACKEND
         ids = b.tok.render_raw(prompt)
         drawn, lps = b.sample(ids, max_tokens, temperature, seed, _bias_map(logit_bias))
+        b.draw_log.append({"prompt": prompt, "seed": seed, "id": drawn[0] if drawn else None,
+                           "margin": b.last_margins[0] if b.last_margins else None})
         text = b.tok.decode([i for i in drawn if i not in b.tok.eos_ids])
         lp_ns = SimpleNamespace(tokens=b.tok.tokens(drawn), token_logprobs=lps)
         return SimpleNamespace(choices=[SimpleNamespace(text=text, logprobs=lp_ns)])

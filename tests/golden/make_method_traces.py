@@ -136,13 +136,13 @@ GEMMA256_RUNS = [
 
 # configs/main_body/scenario_1.yaml:36-59 (api_delay 0, brushup off, seeds the fixture's):
 # Best-of-N at its full 200 tokens, lookahead at bf 2 / depth 4 over 8 committed tokens,
-# beam 4 (10 sampling attempts) over 100 of its 200 tokens
+# beam 4 (10 sampling attempts) over its full 200 tokens
 MAIN128_RUNS = [
     ("best_of_n", {"n": 4, "max_tokens": 200, "seed": 42, "temperature": 1.0, "api_delay": 0,
                    "log_level": "WARNING"}),
     ("finite_lookahead", {"branching_factor": 2, "max_depth": 4, "max_tokens": 8, "seed": 42,
                           "api_delay": 0, "log_level": "WARNING"}),
-    ("beam_search", {"beam_width": 4, "max_tokens": 100, "max_sampling_attempts": 10, "seed": 42,
+    ("beam_search", {"beam_width": 4, "max_tokens": 200, "max_sampling_attempts": 10, "seed": 42,
                      "api_delay": 0, "brushup": False, "log_level": "WARNING"}),
 ]
 # echo log-probs of the prompt tail only (the LM head over these rows): beam search keeps
@@ -178,6 +178,14 @@ BPE_RUNS = [
 ]
 
 
+def round_weights_bf16(model) -> None:
+    """Every weight rounded to the nearest bf16 in place (stored fp32): the same rounding
+    the product applies when it loads these weights as bf16, so that rounding is exact."""
+    with torch.no_grad():
+        for v in model.w.values():
+            v.copy_(v.bfloat16().float())
+
+
 def write_traces(name: str, out) -> None:
     """JSON (gzip-compressed for *.gz: the thousands of recorded calls of the wide traces
     repeat the same prompts)."""
@@ -211,6 +219,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--family", default="llama3", choices=sorted(FAMILIES))
+    ap.add_argument("--bf16-weights", action="store_true",
+                    help="round the seeded fixture weights to bf16 once (kept as fp32), so the "
+                         "reference's fp32 run and the product's bf16 path hold IDENTICAL "
+                         "weights; recorded as weights_bf16 in the trace")
     ap.add_argument("--resume", action="store_true",
                     help="reuse the runs a previous (killed) generation of this family finished")
     args = ap.parse_args()
@@ -220,6 +232,8 @@ def main() -> None:
     global MODEL_ID
     MODEL_ID, out_name = FAMILIES[args.family]
     cfg, model, tok = fixture_model(args.family)
+    if args.bf16_weights:
+        round_weights_bf16(model)
     # c1long: beam search only, whose calls are recorded by their last 6 span log-probs
     backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok,
                                     tail_positions=32 if args.family == "c1long" else None,
@@ -265,6 +279,8 @@ def main() -> None:
     if args.family == "main128":
         out["preset_overrides"] = dict(MAIN128_OVERRIDES)
         out["tokenizer_vocab"] = cfg.vocab
+    if args.bf16_weights:
+        out["weights_bf16"] = True
     if args.family == "bpe":
         out["tokenizer"] = "bpe_fixture"
     if args.family == "wide":
@@ -352,12 +368,21 @@ def main() -> None:
                 up = k.get("user_prompt")
                 assert up is not None and up.startswith(static) and k.get("max_tokens") == 1
                 extra["fl_draws"].append({"suffix": up[len(static):], "seed": k.get("seed"),
-                                          "text": out_text})
+                                          "text": out_text,
+                                          "margin": (backend.last_margins[0]
+                                                     if backend.last_margins else None)})
                 return out_text
 
             gen._generate_tree_paths = rec_tree
             gen._get_first_token_of_best_path = rec_first
             finite_lookahead.generate_text = rec_gen_text
+        if method == "beam_search" and args.bf16_weights:
+            # every proposal draw (beam_search.py:251-266) with its Gumbel-max margin, keyed
+            # by (statement so far, seed): a free-running bf16 replay that draws another
+            # token must do so only where the reference's draw was a near-tie
+            rs, ru = gen._create_reference_prompt(issue, opinions, "")
+            beam_static = f"{rs}\n\n{ru}" if rs else ru
+            backend.draw_log = []
         if method == "mcts":
             extra["steps"] = []
             orig_best = gen._select_best_child
@@ -370,6 +395,10 @@ def main() -> None:
 
             gen._select_best_child = rec_best
         stmt = gen.generate_statement(issue, opinions)
+        if method == "beam_search" and args.bf16_weights:
+            assert all(d["prompt"].startswith(beam_static) for d in backend.draw_log)
+            extra["draws"] = [{"suffix": d["prompt"][len(beam_static):], "seed": d["seed"],
+                               "id": d["id"], "margin": d["margin"]} for d in backend.draw_log]
         if method == "finite_lookahead" and "fl_draws" in extra:
             finite_lookahead.generate_text = orig_gen_text
         out["runs"].append({"method": method, "config": mcfg, "statement": stmt,

@@ -79,6 +79,13 @@ def register_fixture_engine(traces, device, dtype=torch.float32, model_id=None):
     cpu = Mm.Model(cfg, "cpu", torch.float32, seed=traces["weight_seed"])
     if "embed_scale" in traces:          # the C1-shaped fixture (make_method_traces.py)
         cpu.w["embed"].mul_(traces["embed_scale"])
+    if traces.get("weights_bf16"):
+        # the reference ran on the seeded weights rounded to bf16 (make_method_traces.py
+        # --bf16-weights): the fp32 replay holds the same values, and the bf16 replay's
+        # rounding below is exact -- both sides of every comparison hold IDENTICAL weights
+        with torch.no_grad():
+            for v in cpu.w.values():
+                v.copy_(v.bfloat16().float())
     # dtype=bfloat16: the same seeded fp32 weights rounded once to bf16 (the shipped path
     # for bf16 checkpoints: stream kernels, DecodeState, _score_fused)
     w = {k: v.to(device=device, dtype=dtype) for k, v in cpu.w.items()}

@@ -264,33 +264,6 @@ def _hipcc_or_skip():
     return hipcc
 
 
-def test_fast_div_is_floor_division(pkg, tmp_path):
-    """cs_kernels.cuh fast_div (cs_hist_gather's index math: float reciprocal + one
-    correction) equals integer floor division for every numerator below 2^20 and every
-    divisor the copy uses (units per head: hb * D / 8 and its V^T counterpart, 1..4
-    16-byte units per row), compiled as host code with the library's flags."""
-    import subprocess
-    from importlib import import_module
-    build = import_module(pkg.__name__ + ".build")
-    hipcc = _hipcc_or_skip()
-    src = tmp_path / "fast_div.hip"
-    src.write_text('#include "cs_kernels.cuh"\n'
-                   'int main() {\n'
-                   '  long bad = 0;\n'
-                   '  for (int d = 1; d <= 20000; d += (d < 64 ? 1 : 7)) {\n'
-                   '    const float inv = 1.0f / d;\n'
-                   '    for (int i = 0; i < (1 << 20); i += (d < 64 ? 1 : 3)) bad += fast_div(i, d, inv) != i / d;\n'
-                   '  }\n'
-                   '  printf("%ld\\n", bad);\n'
-                   '  return bad != 0;\n'
-                   '}\n')
-    exe = tmp_path / "fast_div"
-    flags = [f for f in build._flags() if f != "-fPIC"]
-    subprocess.run([hipcc] + flags + ["-O2", str(src), "-o", str(exe)], check=True, capture_output=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout
-
-
 def test_gemm_fragment_reads_are_hand_counted(pkg, tmp_path):
     """cs_gemm_bf16's 2-waves-per-SIMD kernels at 17 row tiles (C3's 272 rows, C5's 2 x 272)
     keep their LDS fragment reads in flight with counted waits (inline-asm ds_read_b128 +

@@ -245,3 +245,46 @@ def test_split_partials_folded_by_add_rms_norm_is_bitwise(ops, dev, M, d, K, spl
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
     assert torch.equal(a_got, a_ref)
+
+
+def _table_keys():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "generating-fair-consensus-statements-with-social-choice-on-token-level-mdps_amd",
+                        "tuned", "gemm_dispatch_mi355x.json")
+    with open(path) as f:
+        return sorted(json.load(f)["table"], key=lambda k: [int(v) for v in k.split(",")])
+
+
+@pytest.mark.parametrize("key", _table_keys())
+def test_every_dispatched_production_shape_matches_fp32_product(ops, dev, key):
+    """Every shape the committed dispatch table routes onto cs_gemm (the production decode
+    GEMMs of C1-C5 at 1 GPU and per rank at 8: e.g. the 70B per-rank gate|up 72 x 57,344 x
+    8,192 in the 7-wave packed gated form, its down 72 x 8,192 x 28,672, Gemma-2's per-rank
+    gate|up 48 x 28,672 x 3,584, the 520-row C5 shapes, the LM heads), through ops.linear as
+    the model calls it -- with and without the packed copy -- against the fp32 product of
+    the same bf16 operands.  Plain: |y - ref| <= 2^-7 |ref| + 1e-3 max|ref| (one bf16
+    rounding + accumulation order, _tol); gated: act(gate) * up of the ROUNDED halves, so
+    three bf16 roundings (gate, up, product): 2^-6 |ref| + 2e-3 max|ref|."""
+    M, N, K, gated = (int(v) for v in key.split(","))
+    gated = bool(gated)
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    if gated:
+        F_ = N // 2
+        ref = torch.nn.functional.silu(ref[:, :F_]) * ref[:, F_:]
+        tol = ref.abs() * 2.0 ** -6 + 2e-3 * ref.abs().max()
+    else:
+        tol = _tol(ref)
+    pw = ops.gemm_pack(w) if ops.gemm_choice(M, N, K, gated, packed=True) is not None else None
+    routes = {"unpacked": ops.linear(x, w, gated=gated, act="silu")}
+    if pw is not None:
+        routes["packed"] = ops.linear(x, w, gated=gated, act="silu", packed=pw)
+    del w
+    for name, y in routes.items():
+        assert y.shape == ref.shape, name
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (name, float(err.max()), float(ref.abs().max()))

@@ -406,24 +406,6 @@ def test_gated_act_matches_torch(ops, dev, act):
     assert float(diff.max()) <= 2 ** -6 * float(ref.float().abs().max())
 
 
-@pytest.mark.parametrize("L,S,Hkv,ldh,D,hb", [(2, 5, 2, 32, 64, 7), (3, 16, 8, 64, 256, 33),
-                                             (1, 4, 8, 96, 128, 96), (2, 3, 1, 32, 64, 0),
-                                             (2, 6, 4, 64, 128, 41), (1, 3, 2, 64, 64, 64)])
-def test_hist_gather_copies_filled_slots_of_the_parents(ops, dev, L, S, Hkv, ldh, D, hb):
-    """cs_hist_gather: dst[l][s] = src[l][parent[s]] for the filled slots (K rows j < hb,
-    the V^T 32-slot tiles holding a slot j < hb, whole); the rest of dst is left as it was."""
-    g = torch.Generator(device="cpu").manual_seed(L * 100 + S + hb)
-    bf = torch.bfloat16
-    sk = torch.randn(L, S, Hkv, ldh, D, generator=g).to(bf).to(dev)
-    sv = torch.randn(L, S, Hkv, ldh // 32, D, 32, generator=g).to(bf).to(dev)
-    dk = torch.full_like(sk, 7.0)
-    dv = torch.full_like(sv, 7.0)
-    parent = torch.randint(0, S, (S,), generator=g).to(dev)
-    ops.hist_gather(sk, dk, sv, dv, parent, torch.tensor([hb], dtype=torch.int32, device=dev))
-    torch.cuda.synchronize()
-    _check_gathered(sk, sv, dk, dv, parent, hb, ldh)
-
-
 def test_captured_decode_state_is_freed_by_refcount_and_plans_survive_eviction(dev):
     """A DecodeState whose ``post`` closure references it is freed as soon as its last
     reference goes (no reference cycle through the graph keys), so the cyclic collector
@@ -483,36 +465,6 @@ def test_captured_decode_state_is_freed_by_refcount_and_plans_survive_eviction(d
     _, want = run(False)
     for a, b in zip(got, want):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("L,Ss,Sd,Hkv,ldh,D,hb", [(2, 5, 12, 2, 32, 64, 3), (3, 33, 132, 8, 32, 128, 1),
-                                                 (1, 7, 2, 4, 64, 256, 40), (2, 4, 9, 1, 32, 64, 0)])
-def test_tree_gather_copies_parent_streams_between_levels(ops, dev, L, Ss, Sd, Hkv, ldh, D, hb):
-    """cs_tree_gather: dst[l][s] = src[l][parent[s]] (filled slots) with source and
-    destination buffers of different stream counts (one lookahead tree level to the next)."""
-    g = torch.Generator(device="cpu").manual_seed(L * 1000 + Ss * 10 + Sd + hb)
-    bf = torch.bfloat16
-    sk = torch.randn(L, Ss, Hkv, ldh, D, generator=g).to(bf).to(dev)
-    sv = torch.randn(L, Ss, Hkv, ldh // 32, D, 32, generator=g).to(bf).to(dev)
-    dk = torch.full((L, Sd, Hkv, ldh, D), 7.0, dtype=bf, device=dev)
-    dv = torch.full((L, Sd, Hkv, ldh // 32, D, 32), 7.0, dtype=bf, device=dev)
-    parent = torch.randint(0, Ss, (Sd,), generator=g).to(dev)
-    ops.tree_gather(sk, dk, sv, dv, parent, torch.tensor([hb], dtype=torch.int32, device=dev))
-    torch.cuda.synchronize()
-    _check_gathered(sk, sv, dk, dv, parent, hb, ldh)
-
-
-def _check_gathered(sk, sv, dk, dv, parent, hb, ldh):
-    """K rows j < hb and the V^T tiles holding a slot j < hb (whole 32-slot tiles) are the
-    parent's; K rows from hb and the later V^T tiles are untouched (7.0)."""
-    ek = torch.full_like(dk, 7.0)
-    if hb > 0:
-        ek[:, :, :, :hb] = sk[:, parent][:, :, :, :hb]
-    assert torch.equal(dk, ek)
-    slot = torch.arange(ldh, device=dv.device).view(ldh // 32, 1, 32)     # [tile, 1, lane]
-    copied = slot < ((hb + 31) // 32) * 32
-    want = torch.where(copied, sv[:, parent], torch.full_like(dv, 7.0))
-    assert torch.equal(dv, want)
 
 
 def test_append_prefix_tokens_equals_prefill_of_the_longer_prompts(dev):

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """A/B timing of the beam-step pieces on resident logits (HIP events, GPU kept busy so the
-host never gaps the queue).  python tools/beam_ab.py"""
+host never gaps the queue).  python tools/beam_ab.py [--only c3,c5] [--lib alt.so]
+
+The library reads its planning knobs (CS_DECODE_BLOCK, CS_DECODE_KP, CS_DECODE_ROWS_FIRST,
+CS_TARGET_WGS) once per process: sweep them by running this tool once per setting, e.g.
+CS_DECODE_KP=4 python tools/beam_ab.py --only c5."""
 import importlib
 import json
 import os
@@ -70,57 +74,6 @@ def main():
         wd = ops.Workspace(zeroed=True)
         r["decode_us"] = timed(lambda: ops.beam_decode_step(ref, x, R, K, "min", n_order=B,
                                                             softcap=cap, workspace=wd))
-        if "--blocks" in sys.argv:
-            for blk in (256, 1024):
-                for kp in ("", "4"):
-                    os.environ["CS_DECODE_BLOCK"] = str(blk)
-                    if kp:
-                        os.environ["CS_DECODE_KP"] = kp
-                    wd2 = ops.Workspace(zeroed=True)
-                    r[f"decode_block{blk}{'_kp' + kp if kp else ''}_us"] = timed(
-                        lambda: ops.beam_decode_step(ref, x, R, K, "min", n_order=B, softcap=cap,
-                                                     workspace=wd2))
-                    os.environ.pop("CS_DECODE_KP", None)
-            os.environ.pop("CS_DECODE_BLOCK")
-        if "--knobs" in sys.argv:
-            # --knobs "CS_TARGET_WGS=512,CS_DECODE_BLOCK=1024;CS_TARGET_WGS=768" : each ';' group
-            # is one setting of the host planning knobs, timed on the fused decode launch
-            for grp in sys.argv[sys.argv.index("--knobs") + 1].split(";"):
-                kv = dict(x.split("=") for x in grp.split(",") if x)
-                old_env = {k: os.environ.get(k) for k in kv}
-                os.environ.update(kv)
-                wdk = ops.Workspace(zeroed=True)
-                try:
-                    r["decode[" + grp + "]_us"] = timed(lambda: ops.beam_decode_step(
-                        ref, x, R, K, "min", n_order=B, softcap=cap, workspace=wdk))
-                finally:
-                    for k, v in old_env.items():
-                        if v is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = v
-        if "--sweep" in sys.argv:
-            for kp in (4, 8, 16):
-                for rf in (0, 1):
-                    os.environ["CS_DECODE_KP"] = str(kp)
-                    os.environ["CS_DECODE_ROWS_FIRST"] = str(rf)
-                    try:
-                        r[f"decode_kp{kp}_rf{rf}_us"] = timed(lambda: ops.beam_decode_step(
-                            ref, x, R, K, "min", n_order=B, softcap=cap, workspace=wd))
-                    except Exception:   # a KP the block size does not build
-                        pass
-            os.environ.pop("CS_DECODE_KP")
-            os.environ.pop("CS_DECODE_ROWS_FIRST")
-        if "--twsweep" in sys.argv:   # split-V target grid (block shape) x grid order
-            for tw in (512, 1024, 2048):
-                for rf in (0, 1):
-                    os.environ["CS_TARGET_WGS"] = str(tw)
-                    os.environ["CS_DECODE_ROWS_FIRST"] = str(rf)
-                    wt = ops.Workspace(zeroed=True)
-                    r[f"decode_tw{tw}_rf{rf}_us"] = timed(lambda: ops.beam_decode_step(
-                        ref, x, R, K, "min", n_order=B, softcap=cap, workspace=wt))
-            os.environ.pop("CS_TARGET_WGS")
-            os.environ.pop("CS_DECODE_ROWS_FIRST")
         r["bytes"] = A * B * V * x.element_size()
         r["ideal_us"] = r["bytes"] / 8e12 * 1e6
         print(json.dumps(r), flush=True)
