@@ -419,9 +419,9 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_step_kernel
   bool valid = true;
   // split rows: the canonical split arithmetic (split_partial), BLOCK / 256 splits per block
   const float2 ms =
-      nsplit > 1 ? split_partial<DT, CAP, FIXED, BLOCK>(rp, sitem, nsplit, split_len, vocab, cap,
+      nsplit > 1 ? split_partial<DT, CAP, FIXED, BLOCK, true>(rp, sitem, nsplit, split_len, vocab, cap,
                                                         inv_cap, sm_m, sm_s, ctab, split, valid)
-                 : block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, 0, vocab, cap, inv_cap,
+                 : block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL, true>(rp, 0, vocab, cap, inv_cap,
                                                                     sm_m, sm_s, ctab);
 
   // 2. row finish by the row's last arriver
@@ -880,9 +880,9 @@ __global__ __launch_bounds__(BLOCK, BLOCK >= 1024 ? 8 : 4) void beam_decode_kern
     // (split_partial), so a 1024-thread launch (proposer chunks of 16 * 1024 elements) takes
     // split rows four splits per block with the same bits as 256-thread splits
     const float2 ms =
-        nsplit > 1 ? split_partial<DT, CAP, FIXED, BLOCK>(rp, sitem, nsplit, split_len, vocab, cap,
+        nsplit > 1 ? split_partial<DT, CAP, FIXED, BLOCK, true>(rp, sitem, nsplit, split_len, vocab, cap,
                                                           inv_cap, sm_m, sm_s, ctab, split, valid)
-                   : block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL>(rp, 0, vocab, cap, inv_cap,
+                   : block_lse_partial<DT, CAP, FIXED, BLOCK, UNROLL, true>(rp, 0, vocab, cap, inv_cap,
                                                                       sm_m, sm_s, ctab);
     if (nsplit > 1) {
       if (valid && tid % kSplitSub == 0) {

@@ -286,7 +286,7 @@ __device__ __forceinline__ void cap_accum(float& s, uint32_t& nanmax, const u32x
 // tid_in >= 0: the caller runs several BLOCK-thread sub-blocks side by side in one larger
 // workgroup (tid_in = thread index within the sub-block, sm_m / sm_s the sub-block's NW
 // slots; every sub-block reaches the workgroup barrier inside, so they run in lockstep).
-template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL>
+template <int DT, bool CAP, bool FIXED, int BLOCK, int UNROLL, bool PIPE = false>
 __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp, int64_t v0,
                                                     int64_t n, float cap, float inv_cap,
                                                     float* sm_m, float* sm_s,
@@ -331,10 +331,7 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
   const u32x4* vp = reinterpret_cast<const u32x4*>(rp + (v0 + head) * ESZ);
   int64_t i = tid;
   constexpr int STEP = UNROLL * BLOCK;
-  for (; i + (UNROLL - 1) * BLOCK < nvec; i += STEP) {
-    u32x4 q[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * BLOCK);
+  auto consume = [&](u32x4* q) {
     if constexpr (TAB) {
       cap_accum<UNROLL>(s, nanmax, q, ctab);
     } else {
@@ -342,6 +339,35 @@ __device__ __forceinline__ float2 block_lse_partial(const char* __restrict__ rp,
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) unpack_vec<DT>(q[u], v + u * EPV);
       accum_elems<UNROLL * EPV, CAP, FIXED>(m, s, v, cap, inv_cap);
+    }
+  };
+  // PIPE (the beam kernels' soft-capped bf16 rows: the LDS exp-table path, <= 2 vectors
+  // per lane): software-pipelined, the next UNROLL vectors issued before this batch is
+  // consumed, so a wave keeps its loads in flight through its table lookups and the
+  // proposer / tail work beside it (same elements, same order: bit-identical to the plain
+  // loop).  The C3 decode launch 42.7 -> 40.0 us, the C3 cs_beam_step 33.9 -> 31.7 us;
+  // measured slower in cs_logsoftmax_gather's own launches (C3 split rows 28.0 -> 33.5 us,
+  // C2's plain rows 2.725 -> 2.75 ms) and past 2 vectors (VGPRs cost occupancy), so those
+  // keep the plain loop (profiles/r06_ab_lsg.jsonl, r06_ab_beam.jsonl, r06b_beam_ab.jsonl)
+  if (PIPE && TAB && UNROLL <= 2 && i + (UNROLL - 1) * BLOCK < nvec) {
+    u32x4 q[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * BLOCK);
+    for (i += STEP; i + (UNROLL - 1) * BLOCK < nvec; i += STEP) {
+      u32x4 nx[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) nx[u] = __builtin_nontemporal_load(vp + i + u * BLOCK);
+      consume(q);
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) q[u] = nx[u];
+    }
+    consume(q);
+  } else {
+    for (; i + (UNROLL - 1) * BLOCK < nvec; i += STEP) {
+      u32x4 q[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) q[u] = __builtin_nontemporal_load(vp + i + u * BLOCK);
+      consume(q);
     }
   }
   for (; i < nvec; i += BLOCK) {
@@ -389,7 +415,7 @@ __host__ __device__ constexpr int32_t split_items(int32_t nsplit, int block) {
 
 // this thread's split of the row's work item `item` (0 <= item < split_items) and the
 // split's (m, s), valid in the sub-block's thread 0 when `valid`
-template <int DT, bool CAP, bool FIXED, int BLOCK>
+template <int DT, bool CAP, bool FIXED, int BLOCK, bool PIPE = false>
 __device__ __forceinline__ float2 split_partial(const char* __restrict__ rp, int32_t item,
                                                int32_t nsplit, int64_t split_len, int64_t vocab,
                                                float cap, float inv_cap, float* sm_m, float* sm_s,
@@ -403,7 +429,7 @@ __device__ __forceinline__ float2 split_partial(const char* __restrict__ rp, int
   const int64_t v0 = valid ? static_cast<int64_t>(split) * split_len : 0;
   const int64_t n = valid ? min(vocab, v0 + split_len) - v0 : 0;
   constexpr int NWS = kSplitSub / 64;
-  return block_lse_partial<DT, CAP, FIXED, kSplitSub, kSplitUnroll>(
+  return block_lse_partial<DT, CAP, FIXED, kSplitSub, kSplitUnroll, PIPE>(
       rp, v0, n, cap, inv_cap, sm_m + q * NWS, sm_s + q * NWS, ctab,
       static_cast<int>(threadIdx.x) % kSplitSub);
 }

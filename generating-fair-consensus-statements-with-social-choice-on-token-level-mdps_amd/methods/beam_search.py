@@ -459,7 +459,9 @@ class BeamSearchGenerator(BaseGenerator):
         step graph (advance + LM head + cs_vocab_topk), rank 0's proposals broadcast, a
         scoring graph (cs_beam_step, no order), the MIN all-reduce of the welfare and a
         selection graph (cs_beam_select: stable order of every candidate) -- the two
-        exchanges on the stream between graph replays.  One device->host copy per step."""
+        exchanges on the stream between graph replays -- or, when the direct RCCL
+        communicator's collectives are capturable (parallel.StepComm.capturable), all of it
+        inside the step graph.  One device->host copy per step."""
         dev = engine.device
         m = engine.model
         B, K = st.B, int(self.top_k)
@@ -582,16 +584,42 @@ class BeamSearchGenerator(BaseGenerator):
                 comm.min_(Wx)                  # welfare over every agent
                 replay("select", select)
 
-            def first_step():
-                propose()
-                exchange_and_select()
+            if comm.capturable:
+                # the collectives record into the step graph: a sharded step (forward, LM
+                # head, proposer, broadcast, scoring, MIN all-reduce, selection) is ONE
+                # replay, no host call between its parts
+                def exchange_in_graph():
+                    comm.bcast0(ids_buf)
+                    score_w()
+                    comm.min_(Wx)
+                    select()
 
-            def launch(host=None):
-                if host is None:
-                    st.advance_device(post=post)
-                else:
-                    st.advance(*host, post=post)
-                exchange_and_select()
+                def post():
+                    torch.index_select(U_buf, 1, kidx, out=rewards)
+                    propose()
+                    exchange_in_graph()
+
+                def first_step():
+                    propose()
+                    exchange_in_graph()
+
+                def launch(host=None):
+                    if host is None:
+                        st.advance_device(post=post)
+                    else:
+                        st.advance(*host, post=post)
+                self.decode_path = "fused-topk-sharded-graph"
+            else:
+                def first_step():
+                    propose()
+                    exchange_and_select()
+
+                def launch(host=None):
+                    if host is None:
+                        st.advance_device(post=post)
+                    else:
+                        st.advance(*host, post=post)
+                    exchange_and_select()
 
         # speculative steps: the next step is queued from the device-side order before the
         # host has walked this one, and redone (rewind + host inputs) when the walk differs

@@ -221,18 +221,34 @@ class StepComm:
     ``min_(W)`` (all-reduce MIN of the per-candidate welfare) and ``bcast0(ids)`` (rank 0's
     proposals).  Over RCCL (the default process group's backend is nccl) they go through
     one process-wide direct communicator (RcclComm: a few us of host time per call; built
-    once, CS_DIRECT_RCCL=0 disables), otherwise through the ProcessGroup (gloo rehearsals)."""
+    once, CS_DIRECT_RCCL=0 disables), otherwise through the ProcessGroup (gloo rehearsals).
+
+    ``capturable``: the direct communicator's collectives can be recorded in a hipGraph, so
+    a sharded decode step (forward, LM head, proposer, broadcast, scoring, MIN all-reduce,
+    selection) is ONE graph replay.  Decided once per communicator by a probe -- a captured
+    broadcast + all-reduce replayed and checked on every rank, the verdict agreed over the
+    process group (every rank takes the same path) -- and CS_RCCL_IN_GRAPH=0 turns it off."""
 
     _direct: Optional[RcclComm] = None
+    _capturable: Optional[bool] = None
 
     def __init__(self, shard: AgentShard):
         self.shard = shard
         self.comm = None
         if (shard.world > 1 and dist.get_backend() == "nccl"
                 and os.environ.get("CS_DIRECT_RCCL", "1") != "0"):
-            if StepComm._direct is None or StepComm._direct.world != shard.world:
+            if StepComm._direct is None or StepComm._direct.world != dist.get_world_size():
                 StepComm._direct = RcclComm()
+                StepComm._capturable = None
             self.comm = StepComm._direct
+
+    @property
+    def capturable(self) -> bool:
+        if self.comm is None or os.environ.get("CS_RCCL_IN_GRAPH", "1") == "0":
+            return False
+        if StepComm._capturable is None:
+            StepComm._capturable = _probe_capture(self.comm)
+        return StepComm._capturable
 
     def min_(self, t: torch.Tensor) -> None:
         if self.shard.world == 1:
@@ -249,3 +265,42 @@ class StepComm:
             self.comm.broadcast(t, 0)
         else:
             dist.broadcast(t, src=0)
+
+
+def _probe_capture(comm: RcclComm) -> bool:
+    """Whether ``comm``'s collectives record into and replay from a hipGraph on this
+    system: a graph of (broadcast from rank 0, kernel, all-reduce MIN) captured, replayed
+    twice with new inputs and checked; every rank's verdict MIN-reduced over the process
+    group so all ranks agree."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ok = 1
+    try:
+        x = torch.zeros(64, dtype=torch.float32, device=dev)
+        ids = torch.zeros(16, dtype=torch.int32, device=dev)
+        # warm the communicator's channels outside the capture
+        comm.broadcast(ids, 0)
+        comm.all_reduce(x, RcclComm.MIN)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                comm.broadcast(ids, 0)
+                x.copy_(ids[:1].float().expand(64) + torch.arange(64, device=dev) * 0
+                        + float(comm.rank))
+                comm.all_reduce(x, RcclComm.MIN)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        for v in (5, 9):
+            ids.fill_(v if comm.rank == 0 else -1)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            # every rank: rank 0's ids, then the MIN over ranks of ids + rank = v
+            if int(ids[0]) != v or float(x.min()) != v or float(x.max()) != v:
+                ok = 0
+        del g
+    except Exception:          # capture refused by the runtime: take the uncaptured path
+        ok = 0
+        torch.cuda.synchronize(dev)
+    verdict = torch.tensor([ok], dtype=torch.int64, device=dev)
+    dist.all_reduce(verdict, op=dist.ReduceOp.MIN)
+    return bool(int(verdict.item()))

@@ -148,11 +148,16 @@ MAIN128_RUNS = [
 # echo log-probs of the prompt tail only (the LM head over these rows): beam search keeps
 # the last one (beam_search.py:389-390), the lookahead the path's last <= 4
 # (finite_lookahead.py:508-520), and a recorded call keeps its span's last 6 -- all of them
-# before the chat frame's closing text, ~60 character tokens of the fixture's tokenizer;
-# Best-of-N needs the user span (a <= 200-token candidate + that frame); the evaluator every
-# position (the reference's find() of a short statement can land in the system prompt,
-# src/utils.py:321-363)
-MAIN128_TAIL = {"beam_search": 128, "best_of_n": 320, "finite_lookahead": 128, "eval": None}
+# within the last ~20 positions (the chat frame after the user text is 14 tokens of the
+# fixture's tokenizer, tokenizer.render_chat; every recorded tail is checked finite as it is
+# recorded); Best-of-N needs the user span (a <= 200-token candidate + that frame); the
+# evaluator every position (the reference's find() of a short statement can land in the
+# system prompt, src/utils.py:321-363)
+MAIN128_TAIL = {"beam_search": 32, "best_of_n": 320, "finite_lookahead": 32, "eval": None}
+# the same for the short-candidate traces regenerated on bf16-representable weights (C1:
+# Best-of-N candidates <= 16 tokens, gemma256: <= 8)
+SHORT_TAIL = {"beam_search": 32, "best_of_n": 96, "finite_lookahead": 32, "eval": None}
+TAILS = {"main128": MAIN128_TAIL, "c1": SHORT_TAIL, "gemma256": SHORT_TAIL}
 
 
 WIDE_AGENTS = 16
@@ -237,7 +242,9 @@ def main() -> None:
     # c1long: beam search only, whose calls are recorded by their last 6 span log-probs
     backend = fake_together.Backend(fake_together.hf_model_for(model, cfg), tok,
                                     tail_positions=32 if args.family == "c1long" else None,
-                                    kv_cache=64 if args.family == "main128" else 0)
+                                    kv_cache=64 if (args.family == "main128" or
+                                                    (args.bf16_weights and args.family in TAILS))
+                                    else 0)
     install(args.reference, backend)
     scen_path = (("configs", "main_body", "scenario_1.yaml") if args.family == "main128" else
                  ("configs", "appendix", "llama", "scenario_1", "beam_search.yaml"))
@@ -257,6 +264,10 @@ def main() -> None:
     def recorder(fn):
         def wrapped(model, system_prompt, user_prompt, *a, **k):
             toks, lps = fn(model, system_prompt, user_prompt, *a, **k)
+            if backend.tail is not None:     # fail fast: a tail past the computed rows
+                import math
+                assert all(v is None or math.isfinite(v) for v in lps[-6:]), \
+                    "a recorded tail reaches past the computed positions"
             calls.append({"system": system_prompt, "user": user_prompt, "n": len(lps),
                           "tail": lps[-6:]})
             return toks, lps
@@ -320,8 +331,8 @@ def main() -> None:
             print(f"{method}: resumed ({len(done[ri]['calls'])} scoring calls)")
             continue
         calls.clear()
-        if args.family == "main128":
-            backend.tail = MAIN128_TAIL[method]
+        if args.family in TAILS and (args.family == "main128" or args.bf16_weights):
+            backend.tail = TAILS[args.family][method]
         gen = get_method_generator(method, dict(mcfg), MODEL_ID)
         extra = {}
         if method == "best_of_n":
@@ -421,8 +432,8 @@ def main() -> None:
 
     # post-hoc evaluation (src/evaluation.py:128-634) on fixed statements
     from src.evaluation import StatementEvaluator  # noqa: E402
-    if args.family == "main128":
-        backend.tail = MAIN128_TAIL["eval"]
+    if args.family in TAILS and (args.family == "main128" or args.bf16_weights):
+        backend.tail = TAILS[args.family]["eval"]
     ev = StatementEvaluator(MODEL_ID, include_comparative_ranking=False, verbose=False)
     stmts = [out["runs"][0]["statement"],
              "Genetic information should stay private unless the person consents to research.",
