@@ -710,7 +710,42 @@ def method_leg(name, args, world, rank, dev):
                     "text by a batched prefill; random-init proposals are mostly byte fragments"}
     del eng
     _free()
+    if name == "c1":
+        out["fp32"] = _method_leg_c1_fp32(mc, gcfg, opinions, world, dev)
     return out
+
+
+def _method_leg_c1_fp32(mc, gcfg, opinions, world, dev):
+    """C1 at its stated precision (BASELINE configs[0]: Llama-3.2-1B fp32 log-probs): the same
+    generator on an fp32 random-init model.  The stream kernels serve bf16 models, so an fp32
+    model runs the eager decode (engine.BeamState: torch fp32 forward, cs_beam_step scoring)
+    with host proposals -- the path the fp32 method-trace replays pin to the reference at
+    |delta| <= 5e-5."""
+    R = importlib.import_module(PKG_DIR + ".runtime")
+    methods = importlib.import_module(PKG_DIR + ".methods")
+    eng, tok = R.random_engine(mc["preset"], dev, dtype=torch.float32, reuse_caches=0,
+                               tokenizer_dir=BPE_FIXTURE)
+    model_id = "random-fp32:" + mc["preset"]
+    R.register_engine(model_id, eng, tok)
+    warm = methods.get_method_generator("beam_search", dict(gcfg, max_tokens=3), model_id)
+    warm.generate_statement(SCENARIO_ISSUE, opinions)
+    gen = methods.get_method_generator("beam_search", dict(gcfg), model_id)
+    _barrier_sync(world)
+    t0 = time.perf_counter()
+    gen.generate_statement(SCENARIO_ISSUE, opinions)
+    _barrier_sync(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    d = np.diff(np.asarray(gen.step_times))
+    step_s = _max_over_ranks(float(np.median(d[1:] if d.size > 2 else d)) if d.size else el,
+                             world, dev)
+    A, B, K = mc["agents"], mc["beam_width"], mc["top_k"]
+    R.clear_engines()
+    del eng, gen, warm
+    _free()
+    return {"workload": mc["desc"].replace("bf16", "fp32"), "dtype": "f32",
+            "decode_path": "eager (BeamState, fp32)", "ms_per_step": step_s * 1e3,
+            "decode_steps_per_s": 1.0 / step_s, "scorings_per_s": A * B * K / step_s,
+            "statement_s": el, "steps_per_statement": len(d) + 1 if d.size else 1}
 
 
 def _graph_step_ms(eng, tok, opinions, mc, dev, reps=20):
@@ -860,6 +895,35 @@ def cpu_baseline(seconds, V=128_256, T=150):
                   f"get_prompt_logprobs; torch {cores} threads (model init {init_s:.1f} s, not timed)"}
     del model
     gc.collect()
+    # (1d) BASELINE C5's scoring call: Llama-3.3-70B fp32, the agent prompt + a 60-token beam
+    # (260 tokens) + one candidate token.  A whole 80-layer fp32 call is ~0.5 minute of host
+    # time, so it is timed on 2- and 4-layer subsets of the full-width model and stated as
+    # the extrapolation fixed + 80 x per-layer (per-layer = the difference / 2; fixed =
+    # embedding, final norm, LM head over 128,256 and the log-softmax)
+    sub = {}
+    for nl in (2, 4):
+        cfg_s = M.preset("llama-3.3-70b", n_layers=nl)
+        ms = M.Model.__new__(M.Model)
+        ms.cfg = cfg_s
+        w = {n_: torch.full(shp, 1.0 if "norm" in n_ else 0.01, dtype=torch.float32)
+             for n_, shp in ms.shapes().items()}
+        model = M.Model(cfg_s, "cpu", torch.float32, weights=w)
+        _per_call_scoring(model, 260, 1, 0.0)                 # warm (first-touch pages)
+        n, el = _per_call_scoring(model, 260, 1, seconds / 8)
+        sub[nl] = el / n
+        del model, w, ms
+        gc.collect()
+    per_layer = max(0.0, (sub[4] - sub[2]) / 2)
+    fixed = max(0.0, sub[2] - 2 * per_layer)
+    call_s = fixed + 80 * per_layer
+    out["c5_per_call"] = {
+        "value": 1.0 / call_s, "unit": "scorings/s", "extrapolated": True,
+        "sample": f"Llama-3.3-70B fp32 (constant weights, full widths) forward of a 260-token agent "
+                  f"prompt + beam and one candidate token, log-softmax over 128,256 + the token's "
+                  f"log-prob, per (agent, beam, token) as beam_search.py:358-390 calls "
+                  f"get_prompt_logprobs; timed on 2 / 4 of its 80 layers ({sub[2]:.2f} / "
+                  f"{sub[4]:.2f} s per call) and extrapolated: {fixed:.2f} s fixed + 80 x "
+                  f"{per_layer:.3f} s per layer = {call_s:.1f} s per call; torch {cores} threads"}
     # (2) C1 config: 1B fp32, 200 + 10 tokens per call
     t0 = time.perf_counter()
     model = _const_model(M, "llama-3.2-1b")
@@ -1266,8 +1330,13 @@ def main():
         if e2e is not None:
             line["end_to_end"] = e2e
         if method:
-            if cpu and cpu.get("c1_per_call") and "c1" in method:
-                method["c1"]["vs_cpu"] = method["c1"]["scorings_per_s"] / cpu["c1_per_call"]["value"]
+            for cname in ("c1", "c3", "c4", "c5"):
+                ref = (cpu or {}).get(f"{cname}_per_call")
+                if ref and cname in method and method[cname].get("scorings_per_s"):
+                    method[cname]["vs_cpu"] = method[cname]["scorings_per_s"] / ref["value"]
+                    if method[cname].get("fp32"):
+                        method[cname]["fp32"]["vs_cpu"] = (method[cname]["fp32"]["scorings_per_s"]
+                                                           / ref["value"])
             line["method_decode"] = method
         if beam:
             line["beam_kernel"] = beam
