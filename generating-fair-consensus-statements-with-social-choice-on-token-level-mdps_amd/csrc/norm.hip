@@ -81,18 +81,32 @@ __global__ __launch_bounds__(BLOCK) void add_rms_kernel(
         // flight together; a select, not an added zero, skips the ones past `splits`)
         const float* q = bp + r * d + 8 * v;
         const int64_t sstride = static_cast<int64_t>(gridDim.x) * d;
-        f32x4 p0[NSP], p1[NSP];
+        // at 1024 threads (d > 4096) 16 splits in flight would need 128 VGPRs and spill:
+        // there the splits go in two batches of 8 (the same additions in the same order)
+        constexpr int NB = (BLOCK >= 1024 && NSP > 8) ? 8 : NSP;
+        f32x4 x0 = {0.0f, 0.0f, 0.0f, 0.0f}, x1 = x0;
 #pragma unroll
-        for (int sp = 0; sp < NSP; ++sp) {
-          const float* qs = q + (sp < splits ? sp : splits - 1) * sstride;
-          p0[sp] = *reinterpret_cast<const f32x4*>(qs);
-          p1[sp] = *reinterpret_cast<const f32x4*>(qs + 4);
-        }
-        f32x4 x0 = p0[0], x1 = p1[0];
+        for (int s0 = 0; s0 < NSP; s0 += NB) {
+          if (s0 > 0 && s0 >= splits) break;
+          f32x4 p0[NB], p1[NB];
 #pragma unroll
-        for (int sp = 1; sp < NSP; ++sp) {
-          x0 = sp < splits ? x0 + p0[sp] : x0;
-          x1 = sp < splits ? x1 + p1[sp] : x1;
+          for (int j = 0; j < NB; ++j) {
+            const int sp = s0 + j;
+            const float* qs = q + (sp < splits ? sp : splits - 1) * sstride;
+            p0[j] = *reinterpret_cast<const f32x4*>(qs);
+            p1[j] = *reinterpret_cast<const f32x4*>(qs + 4);
+          }
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const int sp = s0 + j;
+            if (sp == 0) {
+              x0 = p0[0];
+              x1 = p1[0];
+            } else {
+              x0 = sp < splits ? x0 + p0[j] : x0;
+              x1 = sp < splits ? x1 + p1[j] : x1;
+            }
+          }
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

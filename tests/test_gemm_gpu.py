@@ -224,7 +224,10 @@ def test_gemm_rejects_unsupported_shapes(ops, dev):
 
 
 @pytest.mark.parametrize("M,d,K,splits,variant", [(272, 3584, 2048, 8, 3), (37, 2048, 1024, 2, 2),
-                                                  (72, 8192, 1024, 4, 4), (520, 8192, 1024, 4, 2)])
+                                                  (72, 8192, 1024, 4, 4), (520, 8192, 1024, 4, 2),
+                                                  # d = 8192 (1024-thread rows) with > 8 splits:
+                                                  # the two 8-split batches of the fold
+                                                  (72, 8192, 2048, 16, 2), (48, 8192, 1536, 12, 2)])
 @pytest.mark.parametrize("plus_one,post_norm", [(False, False), (True, True)])
 def test_split_partials_folded_by_add_rms_norm_is_bitwise(ops, dev, M, d, K, splits, variant,
                                                           plus_one, post_norm):
