@@ -249,10 +249,20 @@ __device__ __forceinline__ void dma16(const uint16_t* src, unsigned char* lds_ba
   __builtin_amdgcn_global_load_lds(src, (gl_lds_ptr)lds_base, 16, 0, 0);
 }
 
-// a 16-byte global load the compiler does not track (its vmcnt is counted by hand)
+// a 16-byte global load the compiler does not track (its vmcnt is counted by hand).  NT: the
+// non-temporal policy (`nt`), for weights one CU streams once -- the row blocks of <= 80 rows
+// (per-rank and C1 shapes), where the weight stream is latency-bound and nt shortens a
+// load's issue-to-landed time (MI355X_MICROARCH.md "nt-weights"): per-rank C5 graph step
+// 29.44 -> 27.14 ms, C3 5.94 -> 5.75 ms; on the one-GPU C3 / C5 shapes (two row blocks
+// sharing a column tile's weights through L2, compute-leaning) nt measured 3 % / 1.5 %
+// SLOWER, so those keep the default policy (profiles/r06f_*.jsonl)
+template <bool NT = false>
 __device__ __forceinline__ gbf16x8 asm_load16(const uint16_t* p) {
   gbf16x8 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  if constexpr (NT)
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+  else
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
 
@@ -350,8 +360,8 @@ __device__ __forceinline__ void ws2_accumulate(
     const int64_t o = static_cast<int64_t>(kt) * (PACKED ? 1024 : kGemmBK);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      w[j][0] = asm_load16(wp[j] + o);
-      w[j][1] = asm_load16(wp[j] + o + (PACKED ? 512 : 32));
+      w[j][0] = asm_load16<(MT <= 5)>(wp[j] + o);
+      w[j][1] = asm_load16<(MT <= 5)>(wp[j] + o + (PACKED ? 512 : 32));
     }
   };
   const int xr = lane & 15;
@@ -659,8 +669,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void thin_gemm_kernel(
     const int64_t o = static_cast<int64_t>(s) * 64;
 #pragma unroll
     for (int j = 0; j < FT; ++j) {
-      wr[r][j][0] = *reinterpret_cast<const gbf16x8*>(wp[j] + o);
-      wr[r][j][1] = *reinterpret_cast<const gbf16x8*>(wp[j] + o + 8);
+      // (<= 80 rows: the weights one CU streams once, non-temporal as in asm_load16<true>)
+      wr[r][j][0] = __builtin_nontemporal_load(reinterpret_cast<const gbf16x8*>(wp[j] + o));
+      wr[r][j][1] = __builtin_nontemporal_load(reinterpret_cast<const gbf16x8*>(wp[j] + o + 8));
     }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
