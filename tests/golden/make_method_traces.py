@@ -157,7 +157,8 @@ MAIN128_TAIL = {"beam_search": 32, "best_of_n": 320, "finite_lookahead": 32, "ev
 # the same for the short-candidate traces regenerated on bf16-representable weights (C1:
 # Best-of-N candidates <= 16 tokens, gemma256: <= 8)
 SHORT_TAIL = {"beam_search": 32, "best_of_n": 96, "finite_lookahead": 32, "eval": None}
-TAILS = {"main128": MAIN128_TAIL, "c1": SHORT_TAIL, "gemma256": SHORT_TAIL}
+TAILS = {"main128": MAIN128_TAIL, "c1": SHORT_TAIL, "gemma256": SHORT_TAIL, "c1long": SHORT_TAIL,
+         "fl4": SHORT_TAIL, "wide": SHORT_TAIL}
 
 
 WIDE_AGENTS = 16
