@@ -250,12 +250,14 @@ __device__ __forceinline__ void dma16(const uint16_t* src, unsigned char* lds_ba
 }
 
 // a 16-byte global load the compiler does not track (its vmcnt is counted by hand).  NT: the
-// non-temporal policy (`nt`), for weights one CU streams once -- the row blocks of <= 80 rows
-// (per-rank and C1 shapes), where the weight stream is latency-bound and nt shortens a
-// load's issue-to-landed time (MI355X_MICROARCH.md "nt-weights"): per-rank C5 graph step
-// 29.44 -> 27.14 ms, C3 5.94 -> 5.75 ms; on the one-GPU C3 / C5 shapes (two row blocks
-// sharing a column tile's weights through L2, compute-leaning) nt measured 3 % / 1.5 %
-// SLOWER, so those keep the default policy (profiles/r06f_*.jsonl)
+// non-temporal policy (`nt`), for PACKED weights one CU streams once -- the row blocks of
+// <= 80 rows (per-rank and C1 shapes), where the weight stream is latency-bound and nt
+// shortens a load's issue-to-landed time (MI355X_MICROARCH.md "nt-weights"): per-rank C5
+// graph step 29.44 -> 27.14 ms, C3 5.94 -> 5.75 ms.  Kept off (measured slower,
+// profiles/r06f_*.jsonl, r06i_*.json): the one-GPU C3 / C5 shapes (two row blocks sharing a
+// column tile's weights through L2, compute-leaning: 3 % / 1.5 %), and row-major weights
+// (each 16-byte load takes a quarter of a 64-byte line whose rest the next K steps read:
+// the per-rank C3 down projection 27.6 -> 32.6 us unpacked, 23.2 -> 21.6 us packed)
 template <bool NT = false>
 __device__ __forceinline__ gbf16x8 asm_load16(const uint16_t* p) {
   gbf16x8 v;
@@ -360,8 +362,8 @@ __device__ __forceinline__ void ws2_accumulate(
     const int64_t o = static_cast<int64_t>(kt) * (PACKED ? 1024 : kGemmBK);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      w[j][0] = asm_load16<(MT <= 5)>(wp[j] + o);
-      w[j][1] = asm_load16<(MT <= 5)>(wp[j] + o + (PACKED ? 512 : 32));
+      w[j][0] = asm_load16<(PACKED && MT <= 5)>(wp[j] + o);
+      w[j][1] = asm_load16<(PACKED && MT <= 5)>(wp[j] + o + (PACKED ? 512 : 32));
     }
   };
   const int xr = lane & 15;
@@ -669,9 +671,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void thin_gemm_kernel(
     const int64_t o = static_cast<int64_t>(s) * 64;
 #pragma unroll
     for (int j = 0; j < FT; ++j) {
-      // (<= 80 rows: the weights one CU streams once, non-temporal as in asm_load16<true>)
-      wr[r][j][0] = __builtin_nontemporal_load(reinterpret_cast<const gbf16x8*>(wp[j] + o));
-      wr[r][j][1] = __builtin_nontemporal_load(reinterpret_cast<const gbf16x8*>(wp[j] + o + 8));
+      wr[r][j][0] = *reinterpret_cast<const gbf16x8*>(wp[j] + o);
+      wr[r][j][1] = *reinterpret_cast<const gbf16x8*>(wp[j] + o + 8);
     }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
