@@ -132,6 +132,7 @@ class Backend:
             if i in self.tok.eos_ids:
                 break
             cur.append(i)
+        self.last_drawn = list(drawn)
         return drawn, lps
 
 

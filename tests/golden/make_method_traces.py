@@ -206,6 +206,16 @@ def write_traces(name: str, out) -> None:
     print("wrote", name)
 
 
+def load_existing(name: str):
+    path = os.path.join(HERE, name)
+    if name.endswith(".gz"):
+        import gzip
+        with gzip.open(path, "rt") as f:
+            return json.load(f)
+    with open(path) as f:
+        return json.load(f)
+
+
 def install(reference: str, backend) -> None:
     import fake_together
 
@@ -229,6 +239,9 @@ def main() -> None:
                     help="round the seeded fixture weights to bf16 once (kept as fp32), so the "
                          "reference's fp32 run and the product's bf16 path hold IDENTICAL "
                          "weights; recorded as weights_bf16 in the trace")
+    ap.add_argument("--only", default="",
+                    help="run only this method's runs and replace them in the existing trace "
+                         "file (the other runs, evaluations and prompt records are kept)")
     ap.add_argument("--resume", action="store_true",
                     help="reuse the runs a previous (killed) generation of this family finished")
     args = ap.parse_args()
@@ -326,6 +339,10 @@ def main() -> None:
     if args.resume and os.path.exists(partial):
         with open(partial) as f:
             done = json.load(f)
+    if args.only:
+        prev = load_existing(out_name)
+        assert prev.get("weights_bf16") == bool(args.bf16_weights), "weights differ from the file's"
+        runs = [(m, c) for m, c in runs if m == args.only]
     for ri, (method, mcfg) in enumerate(runs):
         if ri < len(done) and done[ri]["method"] == method and done[ri]["config"] == mcfg:
             out["runs"].append(done[ri])
@@ -354,6 +371,19 @@ def main() -> None:
 
             gen._calculate_candidate_rewards = rec_rewards
             gen._calculate_egalitarian_welfare = rec_welfare
+            if args.bf16_weights:
+                # every candidate's draws (ids incl. the stop id, with the Gumbel-max margin of
+                # each), keyed by its seed: a free-running bf16 replay that draws another token
+                # must do so only where the reference's draw was a near-tie
+                extra["bon_draws"] = []
+                orig_bon_gen = best_of_n.generate_text
+
+                def rec_bon_text(*a, **k):
+                    out_text = orig_bon_gen(*a, **k)
+                    extra["bon_draws"].append({"seed": k.get("seed"), "ids": backend.last_drawn,
+                                               "margins": backend.last_margins})
+                    return out_text
+                best_of_n.generate_text = rec_bon_text
         if method == "finite_lookahead" and args.family in ("fl4", "gemma256", "main128"):
             # the reference's tree of every step and every one-token draw, so the bf16 replay
             # can teacher-force the tree (its draws from bf16 logits could flip near-ties of
@@ -407,6 +437,8 @@ def main() -> None:
 
             gen._select_best_child = rec_best
         stmt = gen.generate_statement(issue, opinions)
+        if method == "best_of_n" and "bon_draws" in extra:
+            best_of_n.generate_text = orig_bon_gen
         if method == "beam_search" and args.bf16_weights:
             assert all(d["prompt"].startswith(beam_static) for d in backend.draw_log)
             extra["draws"] = [{"suffix": d["prompt"][len(beam_static):], "seed": d["seed"],
@@ -420,6 +452,12 @@ def main() -> None:
         with open(partial, "w") as f:
             json.dump(out["runs"], f)
 
+    if args.only:
+        # the new runs replace the file's runs of that method (same configs, in order)
+        new = iter(out["runs"])
+        prev["runs"] = [next(new) if r["method"] == args.only else r for r in prev["runs"]]
+        write_traces(out_name, prev)
+        return
     if args.family == "main128":
         import math
         assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]

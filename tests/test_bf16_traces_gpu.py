@@ -458,6 +458,74 @@ def test_best_of_n_scoring_fused_against_reference(bf16_traces):
             assert int(W.argmax()) == int(w_ref.argmax())
 
 
+def test_best_of_n_free_running_against_reference(bf16_traces):
+    """The whole shipped Best-of-N -- its OWN seeded candidates (runtime.generate on the
+    bf16 stream path, cs_vocab_sample per token), then _score_fused and the welfare argmax
+    -- against the reference's run (best_of_n.py:104-136 generate_text(seed=seed+i) per
+    candidate, :198 argmax).  Every drawn token is compared with the reference's draw of the
+    same (candidate seed, t); a different token is accepted only where the reference's
+    Gumbel-max margin was a near-tie (<= MARGIN_TOL), and the replay then follows the
+    reference's token.  The candidates must then be the reference's, their rewards within
+    TOL_BF16, and the chosen statement the reference's wherever its top-2 welfare gap
+    exceeds 2 x TOL_BF16."""
+    traces, eng, tok = bf16_traces
+    runs = [r for r in traces["runs"] if r["method"] == "best_of_n" and "bon_draws" in r]
+    if not runs:
+        pytest.skip("trace has no recorded Best-of-N draws (make_method_traces.py --bf16-weights)")
+    methods = importlib.import_module(mp.PKG + ".methods")
+    runtime = importlib.import_module(mp.PKG + ".runtime")
+    ops = importlib.import_module(mp.PKG + ".ops")
+    tol, _ = _tols(traces)
+    for run in runs:
+        ref_draw = {}
+        for d in run["bon_draws"]:
+            for t, (i, m) in enumerate(zip(d["ids"], d["margins"])):
+                ref_draw[runtime.to_i64(runtime.draw_seed(int(d["seed"]), t))] = (int(i), float(m))
+        stats = {"draws": 0, "resynced": 0, "max_resync_margin": 0.0}
+        saved = ops.vocab_sample
+
+        def follow(logits, sd, *a, **k):
+            ids, rest = saved(logits, sd, *a, **k)
+            ids_h = ids[:, 0].tolist()
+            fixed = False
+            for j, s in enumerate(sd[:, 0].tolist()):
+                assert s in ref_draw, "a draw the reference never made (stream ran past its end)"
+                ref_id, margin = ref_draw[s]
+                stats["draws"] += 1
+                if ids_h[j] != ref_id:
+                    assert margin <= MARGIN_TOL, (
+                        f"drew {ids_h[j]} where the reference drew {ref_id} at margin {margin}")
+                    stats["resynced"] += 1
+                    stats["max_resync_margin"] = max(stats["max_resync_margin"], margin)
+                    ids_h[j], fixed = ref_id, True
+            if fixed:
+                ids = ids.clone()
+                ids[:, 0] = torch.tensor(ids_h, dtype=ids.dtype, device=ids.device)
+            return ids, rest
+
+        gen = methods.get_method_generator("best_of_n", dict(run["config"]), traces["model_id"])
+        ops.vocab_sample = follow
+        try:
+            stmt = gen.generate_statement(traces["issue"], dict(traces["agent_opinions"]))
+        finally:
+            ops.vocab_sample = saved
+        assert stats["draws"] == sum(len(d["ids"]) for d in run["bon_draws"]), stats
+        assert gen.last_candidates == run["candidates"]
+        U = torch.tensor([gen.last_agent_rewards[aid] for aid in traces["agent_opinions"]],
+                         dtype=torch.float64)
+        ref = torch.tensor([run["agent_rewards"][aid] for aid in traces["agent_opinions"]],
+                           dtype=torch.float64)
+        err = float((U - ref).abs().max())
+        name = f"{traces['_file']} best_of_n free-running"
+        _report(name, "max_abs_reward_err", err)
+        _report(name, "draws", stats)
+        assert err <= tol, err
+        w_ref = torch.tensor(run["welfare"], dtype=torch.float64)
+        top2 = torch.topk(w_ref, 2).values if w_ref.numel() > 1 else None
+        if top2 is None or float(top2[0] - top2[1]) > 2 * tol:
+            assert stmt == run["pre_brushup"] or stmt == run["statement"], (stmt, run["statement"])
+
+
 def test_evaluator_fused_against_reference(bf16_traces):
     traces, eng, tok = bf16_traces
     ev_mod = importlib.import_module(mp.PKG + ".evaluation")
