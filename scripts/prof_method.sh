@@ -9,6 +9,8 @@ export TMPDIR=/tmp
 TAG=""
 EXTRA=""
 if [ -n "${EMULATE:-}" ]; then TAG="_r$EMULATE"; EXTRA="--emulate-ranks $EMULATE"; fi
+# SUFFIX: appended to the output name (A/B runs of one config)
+TAG="$TAG${SUFFIX:-}"
 for c in "$@"; do
   D="$R/gpurun_out/prof_method_$c$TAG"
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$D" -o run -f csv -- \
