@@ -270,10 +270,18 @@ class StepComm:
 def _probe_capture(comm: RcclComm) -> bool:
     """Whether ``comm``'s collectives record into and replay from a hipGraph on this
     system: a graph of (broadcast from rank 0, kernel, all-reduce MIN) captured, replayed
-    twice with new inputs and checked; every rank's verdict MIN-reduced over the process
-    group so all ranks agree."""
+    twice with new inputs and checked.  Two verdicts, each MIN-reduced over the process group
+    (torch.distributed, not ``comm``): whether every rank captured -- a rank replays only
+    when all did, since a replayed collective waits for every rank's -- and whether every
+    rank's replays were right, so all ranks take the same path."""
     dev = torch.device("cuda", torch.cuda.current_device())
-    ok = 1
+
+    def agreed(ok: bool) -> bool:
+        v = torch.tensor([int(ok)], dtype=torch.int64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return bool(int(v.item()))
+
+    g = None
     try:
         x = torch.zeros(64, dtype=torch.float32, device=dev)
         ids = torch.zeros(16, dtype=torch.int32, device=dev)
@@ -290,17 +298,19 @@ def _probe_capture(comm: RcclComm) -> bool:
                         + float(comm.rank))
                 comm.all_reduce(x, RcclComm.MIN)
         torch.cuda.current_stream(dev).wait_stream(s)
-        for v in (5, 9):
-            ids.fill_(v if comm.rank == 0 else -1)
-            g.replay()
-            torch.cuda.synchronize(dev)
-            # every rank: rank 0's ids, then the MIN over ranks of ids + rank = v
-            if int(ids[0]) != v or float(x.min()) != v or float(x.max()) != v:
-                ok = 0
-        del g
-    except Exception:          # capture refused by the runtime: take the uncaptured path
-        ok = 0
         torch.cuda.synchronize(dev)
-    verdict = torch.tensor([ok], dtype=torch.int64, device=dev)
-    dist.all_reduce(verdict, op=dist.ReduceOp.MIN)
-    return bool(int(verdict.item()))
+    except Exception:          # capture refused by the runtime: take the uncaptured path
+        g = None
+        torch.cuda.synchronize(dev)
+    if not agreed(g is not None):
+        return False
+    ok = True
+    for v in (5, 9):
+        ids.fill_(v if comm.rank == 0 else -1)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        # every rank: rank 0's ids, then the MIN over ranks of ids + rank = v
+        if int(ids[0]) != v or float(x.min()) != v or float(x.max()) != v:
+            ok = False
+    del g
+    return agreed(ok)
