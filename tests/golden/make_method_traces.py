@@ -452,16 +452,16 @@ def main() -> None:
         with open(partial, "w") as f:
             json.dump(out["runs"], f)
 
+    if args.family == "main128" or (args.only and args.family in TAILS):
+        import math
+        assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
+                   if v is not None), "a recorded tail reaches past the computed positions"
     if args.only:
         # the new runs replace the file's runs of that method (same configs, in order)
         new = iter(out["runs"])
         prev["runs"] = [next(new) if r["method"] == args.only else r for r in prev["runs"]]
         write_traces(out_name, prev)
         return
-    if args.family == "main128":
-        import math
-        assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
-                   if v is not None), "a recorded tail reaches past the computed positions"
     if args.family in ("c1long", "fl4"):   # method runs only (no evaluator pass)
         import math
         assert all(math.isfinite(v) for r in out["runs"] for c in r["calls"] for v in c["tail"]
