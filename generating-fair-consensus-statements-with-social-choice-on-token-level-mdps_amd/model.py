@@ -103,11 +103,15 @@ def rope_inv_freq(cfg: ModelConfig, device) -> torch.Tensor:
 
 # where a K-split projection's partials are folded in the stream forward: q|k|v inside
 # cs_rope_place_splitk (CS_FOLD_IN_ROPE=0: in cs_gemm_bf16's own launch); the output
-# projection in its own launch (CS_FOLD_IN_NORM=1: inside the residual add's
-# cs_add_rms_norm -- within noise, 0.4 ms slower at C5; profiles/r04s_fold_ab.jsonl)
+# projection inside the residual add's cs_add_rms_norm (CS_FOLD_IN_NORM=0: in its own
+# launch).  Round 4 measured the norm fold 0.4 ms slower at C5 (profiles/r04s_fold_ab.jsonl);
+# since round 5 it loads only its splits' partials, and round 6 measured it faster or equal
+# on every decode step: per-rank C3 5.76 -> 5.67 ms (with the per-rank output projection on
+# the packed K-split GEMM), per-rank C5 27.10 -> 26.94, one-GPU C5 76.4 -> 76.0, C1 / one-GPU
+# C3 within noise (profiles/r06v_fold_ab/)
 _FOLD_IN_ROPE = os.environ.get("CS_FOLD_IN_ROPE", "1") != "0"
 _PACK_LOCK = threading.Lock()
-_FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "0") == "1"
+_FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "1") != "0"
 
 
 class Model:
