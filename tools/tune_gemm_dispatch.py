@@ -31,6 +31,12 @@ model = importlib.import_module(PKG + ".model")
 # (q|k|v in cs_rope_place_splitk, down in cs_add_rms_norm_splitk): their split forms are
 # timed without cs_gemm_bf16's own fold
 FOLDED_BY_CONSUMER = ("qkv", "down")
+# the output projection's consumer is the residual add + RMSNorm, which folds its K-split
+# partials itself (model._FOLD_IN_NORM, the default since round 6): every form of it is
+# timed TOGETHER with that cs_add_rms_norm launch (hipBLASLt / unsplit: the bf16 product
+# added; split: the partials folded in the norm), so the fold's bytes are priced where
+# they are read ("with_norm" in the record)
+WITH_NORM = ("o",) if model._FOLD_IN_NORM else ()
 
 CONFIGS = {"c1": ("llama-3.2-1b", 4, 4), "c3": ("gemma-2-9b", 16, 16), "c5": ("llama-3.3-70b", 64, 8),
            "c4": ("llama-3.1-8b", 32, 0)}
@@ -106,6 +112,16 @@ def main() -> int:
             pws = [ops.gemm_pack(w) for w in ws] if args.packed else []
             for M in Ms:
                 x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+                pair = name in WITH_NORM
+                if pair:
+                    h_res = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+                    n_w = torch.ones(N, device=dev, dtype=torch.bfloat16)
+
+                    def norm(y):   # the residual add's launch in the stream forward
+                        return ops.add_rms_norm(h_res, n_w, 1e-5, b=y, s_out=h_res)
+                else:
+                    def norm(y):
+                        return y
                 if gated:
                     Fh = N // 2
 
@@ -116,7 +132,7 @@ def main() -> int:
                 else:
                     def tfn():
                         for i in range(calls):
-                            x @ ws[i % nw].t()
+                            norm(x @ ws[i % nw].t())
                 t_torch = timed(tfn) / calls * 1e3
                 best = ("torch", 0, 0, t_torch)
                 cands = []
@@ -128,13 +144,13 @@ def main() -> int:
                             continue
                         if (K % (64 * sp) or K // (64 * sp) < 2):
                             continue
-                        if sp > 1 and name in FOLDED_BY_CONSUMER:
-                            t = timed(lambda: [ops.gemm_partials(x, ws[i % nw], splits=sp,
-                                                                 variant=var)
+                        if sp > 1 and (name in FOLDED_BY_CONSUMER or pair):
+                            t = timed(lambda: [norm(ops.gemm_partials(x, ws[i % nw], splits=sp,
+                                                                      variant=var))
                                                for i in range(calls)]) / calls * 1e3
                         else:
-                            t = timed(lambda: [ops.gemm(x, ws[i % nw], gated=bool(gated),
-                                                        act=act, splits=sp, variant=var)
+                            t = timed(lambda: [norm(ops.gemm(x, ws[i % nw], gated=bool(gated),
+                                                             act=act, splits=sp, variant=var))
                                                for i in range(calls)]) / calls * 1e3
                         cands.append({"variant": var, "splits": sp, "us": round(t, 2)})
                         if t < best[3]:
@@ -149,13 +165,13 @@ def main() -> int:
                             continue
                         if K % (64 * sp) or K // (64 * sp) < 2:
                             continue
-                        if sp > 1 and name in FOLDED_BY_CONSUMER:
-                            t = timed(lambda: [ops.gemm_packed_partials(x, pws[i % nw],
-                                                                        splits=sp, variant=var)
+                        if sp > 1 and (name in FOLDED_BY_CONSUMER or pair):
+                            t = timed(lambda: [norm(ops.gemm_packed_partials(x, pws[i % nw],
+                                                                             splits=sp, variant=var))
                                                for i in range(calls)]) / calls * 1e3
                         else:
-                            t = timed(lambda: [ops.gemm_packed(x, pws[i % nw], gated=bool(gated),
-                                                               act=act, splits=sp, variant=var)
+                            t = timed(lambda: [norm(ops.gemm_packed(x, pws[i % nw], gated=bool(gated),
+                                                                    act=act, splits=sp, variant=var))
                                                for i in range(calls)]) / calls * 1e3
                         pcands.append({"variant": var, "splits": sp, "us": round(t, 2)})
                         if pbest is None or t < pbest[2]:
@@ -163,6 +179,8 @@ def main() -> int:
                 rec = {"config": cname, "gemm": name, "M": M, "N": N, "K": K, "gated": gated,
                        "torch_us": round(t_torch, 2), "cs_gemm": cands, "choice": best[0],
                        "best_us": round(best[3], 2)}
+                if pair:
+                    rec["with_norm"] = True
                 if args.packed:
                     rec["cs_gemm_packed"] = pcands
                 record.append(rec)
