@@ -270,19 +270,10 @@ class StepComm:
 def _probe_capture(comm: RcclComm) -> bool:
     """Whether ``comm``'s collectives record into and replay from a hipGraph on this
     system: a graph of (broadcast from rank 0, kernel, all-reduce MIN) captured, replayed
-    twice with new inputs and checked.  Two verdicts, each MIN-reduced over the process group
-    (torch.distributed, not ``comm``): whether every rank captured -- a rank replays only
-    when all did, since a replayed collective waits for every rank's -- and whether every
-    rank's replays were right, so all ranks take the same path."""
+    twice with new inputs and checked, every rank agreeing (agree_capture)."""
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    def agreed(ok: bool) -> bool:
-        v = torch.tensor([int(ok)], dtype=torch.int64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MIN)
-        return bool(int(v.item()))
-
-    g = None
-    try:
+    def capture():
         x = torch.zeros(64, dtype=torch.float32, device=dev)
         ids = torch.zeros(16, dtype=torch.int32, device=dev)
         # warm the communicator's channels outside the capture
@@ -299,18 +290,40 @@ def _probe_capture(comm: RcclComm) -> bool:
                 comm.all_reduce(x, RcclComm.MIN)
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
+
+        def replay_ok() -> bool:
+            ok = True
+            for v in (5, 9):
+                ids.fill_(v if comm.rank == 0 else -1)
+                g.replay()
+                torch.cuda.synchronize(dev)
+                # every rank: rank 0's ids, then the MIN over ranks of ids + rank = v
+                if int(ids[0]) != v or float(x.min()) != v or float(x.max()) != v:
+                    ok = False
+            return ok
+        return replay_ok
+
+    return agree_capture(capture, dev, on_fail=lambda: torch.cuda.synchronize(dev))
+
+
+def agree_capture(capture, dev: torch.device, on_fail=None) -> bool:
+    """The probe's protocol over the default process group (torch.distributed, not the
+    communicator under test): ``capture()`` records the collectives and returns a callable
+    that replays and checks them (or raises: the runtime refused the capture).  Two
+    verdicts, each MIN-reduced over the ranks: whether every rank captured -- a rank
+    replays only when all did, since a replayed collective waits for every rank's -- and
+    whether every rank's replays were right, so all ranks take the same path."""
+    def agreed(ok: bool) -> bool:
+        v = torch.tensor([int(ok)], dtype=torch.int64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return bool(int(v.item()))
+
+    try:
+        replay_ok = capture()
     except Exception:          # capture refused by the runtime: take the uncaptured path
-        g = None
-        torch.cuda.synchronize(dev)
-    if not agreed(g is not None):
+        replay_ok = None
+        if on_fail is not None:
+            on_fail()
+    if not agreed(replay_ok is not None):
         return False
-    ok = True
-    for v in (5, 9):
-        ids.fill_(v if comm.rank == 0 else -1)
-        g.replay()
-        torch.cuda.synchronize(dev)
-        # every rank: rank 0's ids, then the MIN over ranks of ids + rank = v
-        if int(ids[0]) != v or float(x.min()) != v or float(x.max()) != v:
-            ok = False
-    del g
-    return agreed(ok)
+    return agreed(bool(replay_ok()))
