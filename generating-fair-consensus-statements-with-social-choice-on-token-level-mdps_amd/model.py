@@ -112,6 +112,10 @@ def rope_inv_freq(cfg: ModelConfig, device) -> torch.Tensor:
 _FOLD_IN_ROPE = os.environ.get("CS_FOLD_IN_ROPE", "1") != "0"
 _PACK_LOCK = threading.Lock()
 _FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "1") != "0"
+# many-row stream forwards (T >= 32: the scoring chunks) of models without branch norms
+# (Llama): the output and down projections add into the residual in hipBLASLt's epilogue
+# (ops.linear_into_residual), and the residual add's launch only normalises
+_RESID_IN_GEMM = os.environ.get("CS_RESID_IN_GEMM", "1") != "0"
 
 
 class Model:
@@ -539,19 +543,28 @@ class Model:
                                      group_prefix=group_prefix,
                                      prefix_len_host=getattr(pfx, "lens_host", None),
                                      group_prefix_host=group_prefix_host, hist_rows=hist_rows)
-            o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"], packed=wp.get(p + "wo"),
-                           fold=not _FOLD_IN_NORM)
-            # Gemma-2's post-attention / post-MLP norms of the branch ride in the residual
-            # add's launch (b_weight): one cs_add_rms_norm per residual add
-            x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2,
-                                 b_weight=self.w[p + "post_attn_norm"] if g2 else None)
-            # a K-split down projection hands its partials to the residual add's launch
-            y = ops.linear(ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act,
-                                      packed=wp.get(p + "gate_up")),
-                           self.w[p + "w_down"], fold=False, packed=wp.get(p + "w_down"))
+            resid = T >= 32 and not g2 and _RESID_IN_GEMM
+            if resid and ops.linear_into_residual(o.view(n_tok, H * D), self.w[p + "wo"], h,
+                                                  packed=wp.get(p + "wo")):
+                x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps)
+            else:
+                o = ops.linear(o.view(n_tok, H * D), self.w[p + "wo"], packed=wp.get(p + "wo"),
+                               fold=not _FOLD_IN_NORM)
+                # Gemma-2's post-attention / post-MLP norms of the branch ride in the residual
+                # add's launch (b_weight): one cs_add_rms_norm per residual add
+                x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps, b=o, s_out=h, plus_one=g2,
+                                     b_weight=self.w[p + "post_attn_norm"] if g2 else None)
+            act_x = ops.linear(x, self.wf[p + "gate_up"], gated=True, act=act,
+                               packed=wp.get(p + "gate_up"))
             nxt = self.w[f"l{i + 1}.attn_norm"] if i + 1 < c.n_layers else self.w["norm"]
-            x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2,
-                                 b_weight=self.w[p + "post_mlp_norm"] if g2 else None)
+            if resid and ops.linear_into_residual(act_x, self.w[p + "w_down"], h,
+                                                  packed=wp.get(p + "w_down")):
+                x = ops.add_rms_norm(h, nxt, eps)
+            else:
+                # a K-split down projection hands its partials to the residual add's launch
+                y = ops.linear(act_x, self.w[p + "w_down"], fold=False, packed=wp.get(p + "w_down"))
+                x = ops.add_rms_norm(h, nxt, eps, b=y, s_out=h, plus_one=g2,
+                                     b_weight=self.w[p + "post_mlp_norm"] if g2 else None)
         return x
 
 

@@ -874,6 +874,22 @@ def linear(x: torch.Tensor, w: torch.Tensor, *, gated: bool = False, act: str = 
     return x @ w.t()
 
 
+def linear_into_residual(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, *,
+                         packed: Optional["PackedWeight"] = None) -> bool:
+    """h += x @ w.T in the GEMM's own epilogue (hipBLASLt, beta = 1: the product is added in
+    fp32 and rounded once) when the dispatch table leaves this shape on hipBLASLt; returns
+    False (nothing done) otherwise, and the caller takes ``linear`` + the residual add.
+    For the many-row scoring forward: the residual add's launch then only normalises (one
+    read and one write of the rows instead of two and two)."""
+    if not (x.is_cuda and x.dim() == 2 and h.dim() == 2 and h.is_contiguous() and
+            h.dtype == x.dtype == w.dtype == torch.bfloat16 and h.shape == (x.shape[0], w.shape[0])):
+        return False
+    if gemm_choice(x.shape[0], w.shape[0], w.shape[1], False, packed=packed is not None) is not None:
+        return False
+    h.addmm_(x, w.t())
+    return True
+
+
 def gemm_ok(x: torch.Tensor, w: torch.Tensor, gated: bool = False) -> bool:
     """Whether cs_gemm_bf16 takes y = x @ w.T: bf16 2-D operands with unit column stride,
     N a multiple of 128, K of 64, 16-byte aligned rows."""
