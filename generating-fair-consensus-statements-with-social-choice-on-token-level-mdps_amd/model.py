@@ -112,9 +112,10 @@ def rope_inv_freq(cfg: ModelConfig, device) -> torch.Tensor:
 _FOLD_IN_ROPE = os.environ.get("CS_FOLD_IN_ROPE", "1") != "0"
 _PACK_LOCK = threading.Lock()
 _FOLD_IN_NORM = os.environ.get("CS_FOLD_IN_NORM", "1") != "0"
-# many-row stream forwards (T >= 32: the scoring chunks) of models without branch norms
-# (Llama): the output and down projections add into the residual in hipBLASLt's epilogue
-# (ops.linear_into_residual), and the residual add's launch only normalises
+# models without branch norms (Llama): an output or down projection that runs on hipBLASLt
+# (the scoring chunks, prompt prefill, C4's largest tree segments) adds into the residual in
+# hipBLASLt's epilogue (ops.linear_into_residual), and the residual add's launch only
+# normalises; the cs_gemm shapes keep their K-split fold in the residual add
 _RESID_IN_GEMM = os.environ.get("CS_RESID_IN_GEMM", "1") != "0"
 
 
@@ -543,7 +544,7 @@ class Model:
                                      group_prefix=group_prefix,
                                      prefix_len_host=getattr(pfx, "lens_host", None),
                                      group_prefix_host=group_prefix_host, hist_rows=hist_rows)
-            resid = T >= 32 and not g2 and _RESID_IN_GEMM
+            resid = not g2 and _RESID_IN_GEMM
             if resid and ops.linear_into_residual(o.view(n_tok, H * D), self.w[p + "wo"], h,
                                                   packed=wp.get(p + "wo")):
                 x = ops.add_rms_norm(h, self.w[p + "mlp_norm"], eps)
